@@ -1,0 +1,139 @@
+/*
+ * nbgpu.h — C-ABI of the MI355X-native Maglev flow-steering path.
+ *
+ * This is the drop-in boundary for NetBricks' test/maglev hot path.  The
+ * reference runs, per packet, inside its batch operators:
+ *
+ *   parse::<MacHeader>()            framework/src/operators/mod.rs:59-64
+ *   transform(swap_addresses)       test/maglev/src/nf.rs:94-98, headers/mac.rs:140-145
+ *   group_by(ct, group_fn)          test/maglev/src/nf.rs:99-108, operators/group_by.rs:43-55
+ *     group_fn = lut[fnv(flow) % M] test/maglev/src/nf.rs:101-106, utils/flow.rs:53-62,96-110
+ *
+ * A per-packet FFI call is infeasible, so the boundary sits at the batch level:
+ * one call classifies a whole batch (parse + MAC swap + 5-tuple FNV-1a + Maglev
+ * lookup) and emits the per-group FIFO order that the reference's MPSC queues
+ * hold (framework/src/queues/mpsc_mbuf_queue.rs:91-115,197-212).  Plain C types
+ * only; device pointers are caller-owned HBM allocations.
+ *
+ * Errors: 0 on success, negative errno-style codes otherwise, mirroring
+ * libzcsi (native/pmd.c:128,154,165; native/init.c:176-177).  The message of
+ * the last error on the calling thread is returned by nbg_last_error().
+ *
+ * Threading: a handle is used by one thread / one stream at a time (the
+ * reference runs one pipeline per pinned scheduler core, scheduler/context.rs:55-69).
+ * Use one handle per concurrent stream.
+ */
+#ifndef NBGPU_H
+#define NBGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NBG_OK 0
+#define NBG_EINVAL (-22)
+#define NBG_ENOMEM (-12)
+#define NBG_ENODEV (-19)
+#define NBG_EIO (-5)
+#define NBG_ETIMEDOUT (-110)
+
+/* backend value for a packet on which the reference would panic:
+ * data_len < 14 (Packet::parse_header assert, interface/packet.rs:392-399) or a
+ * payload shorter than max(20, 4*IHL+4) (slice OOB in utils/flow.rs:53-62).
+ * Such packets land in group n_backends (the last of n_backends+1 groups). */
+#define NBG_SENTINEL 0xFFFFu
+
+/* classify flags */
+#define NBG_SWAP_MACS 0x1u     /* apply MacHeader::swap_addresses in place (nf.rs:94-98) */
+#define NBG_LUT_GLOBAL 0x2u    /* force the L2-gather LUT variant instead of the LDS-staged one */
+
+typedef struct nbg_maglev nbg_maglev;
+
+/* Build the Maglev LUT on the host exactly as Maglev::new (nf.rs:70-76:
+ * offset_skip_for_name nf.rs:21-31, generate_lut nf.rs:44-68) and upload it to
+ * `device`.  names[i] has name_lens[i] bytes (UTF-8, no terminator needed).
+ * Replaces: `Maglev::new(backends, 65537)` at test/maglev/src/nf.rs:90.
+ * table_size must be >= 2 (the reference hard-codes 65537); n_backends in [1, 65534]. */
+int nbg_maglev_create(const char* const* names, const uint32_t* name_lens, uint32_t n_backends,
+                      uint64_t table_size, int device, nbg_maglev** out);
+
+/* Same as nbg_maglev_create but adopts a LUT the caller already holds (e.g. one
+ * broadcast over RCCL from rank 0): lut[j] < n_backends for all j. */
+int nbg_maglev_create_from_lut(const uint16_t* lut, uint64_t table_size, uint32_t n_backends, int device,
+                               nbg_maglev** out);
+
+void nbg_maglev_destroy(nbg_maglev* h);
+
+uint32_t nbg_maglev_backends(const nbg_maglev* h);
+uint64_t nbg_maglev_table_size(const nbg_maglev* h);
+
+/* Copy the LUT (entries as u16; the reference stores usize) to host memory `out` of n entries. */
+int nbg_maglev_lut(const nbg_maglev* h, uint16_t* out, uint64_t n);
+
+/* Pre-allocate the per-call scratch for batches of up to max_pkts packets so that
+ * later classify calls allocate nothing (needed before hipGraph capture). */
+int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts);
+
+/*
+ * Device-resident batch classify (the hot path).  Replaces the per-packet loop of
+ * GroupByProducer::execute (operators/group_by.rs:43-55) for a whole batch.
+ *
+ *   d_pkts     packet bytes in HBM; packet i starts at d_pkts + (d_off ? d_off[i] : i*stride)
+ *   d_off      nullable u32 byte offsets (descriptor mode, e.g. IMIX)
+ *   d_len      nullable u16 frame lengths (mbuf data_len); NULL => every frame is fixed_len
+ *   n_pkts     packets in the batch, < 2^30
+ *   flags      NBG_SWAP_MACS | NBG_LUT_GLOBAL
+ *   d_backend  out, n_pkts u16: backend index, or NBG_SENTINEL
+ *   d_perm     out (nullable), n_pkts u32: packet indices grouped by backend 0..n-1 then the
+ *              sentinel group, ascending index inside each group (per-group FIFO order)
+ *   d_counts   out (nullable unless d_perm set), n_backends+1 u32: group sizes
+ *   stream     hipStream_t (NULL = default stream); the call is asynchronous
+ *
+ * Frames shorter than 48 B, unaligned or with IHL != 5 take a byte-wise slow path
+ * with identical results.
+ */
+int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
+                               uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
+                               uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, void* stream);
+
+/* Synchronise the handle's last stream and report a device-side fault (a bounded
+ * look-back spin that gave up) as NBG_ETIMEDOUT.  Not needed on the hot path. */
+int nbg_maglev_check(nbg_maglev* h);
+
+/*
+ * Host-resident batch (the PCIe path): packet i is the mbuf data at pkt_ptrs[i]
+ * with lens[i] bytes (MBuf::data_address / data_len, native/zcsi/mbuf.rs:34-49).
+ * Header windows are gathered into pinned staging, copied H2D, classified on the
+ * GPU, and the results (plus the swapped MAC bytes when NBG_SWAP_MACS) copied back
+ * and written into the mbufs.  perm_out / counts_out are nullable.  Synchronous.
+ * Replaces one GroupByProducer::execute over a batch of host mbufs.
+ */
+int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
+                             uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out);
+
+const char* nbg_last_error(void);
+
+/* ---- host-only helpers (no GPU needed) ---------------------------------- */
+
+/* The product's own LUT builder (what nbg_maglev_create uploads), for tests. */
+int nbg_lut_build_host(const char* const* names, const uint32_t* name_lens, uint32_t n_backends,
+                       uint64_t table_size, uint16_t* out);
+
+/* Synthetic trace (DESIGN.md "Synthetic traces"): frame layout then bytes.
+ * mode: 0 = fixed 60-B UDP frames in 64-B slots, 1 = IMIX 7:4:1 of 60/572/1496-B frames
+ * at 64-B aligned offsets.  nbg_trace_layout fills off/len (n entries each) and
+ * returns the buffer size in bytes. */
+uint64_t nbg_trace_layout(uint64_t n, int mode, uint64_t seed, uint32_t* off, uint16_t* len);
+
+#define NBG_TRACE_UNIQUE 0x1u  /* every packet a new flow */
+/* Fill buf with n frames described by off/len; flows drawn from n_flows random 5-tuples. */
+int nbg_trace_fill(uint8_t* buf, const uint32_t* off, const uint16_t* len, uint64_t n, uint64_t seed,
+                   uint32_t n_flows, uint32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NBGPU_H */

@@ -1,0 +1,78 @@
+"""ctypes binding of the in-tree C-ABI library `netbricks_amd/libnbgpu.so` (include/nbgpu.h).
+
+The product path has no CPU fallback: if the HIP library is missing this module
+raises at import time, and every device entry point returns -ENODEV without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnbgpu.so")
+
+NBG_OK = 0
+NBG_SENTINEL = 0xFFFF
+NBG_SWAP_MACS = 0x1
+NBG_LUT_GLOBAL = 0x2
+NBG_TRACE_UNIQUE = 0x1
+
+# every symbol include/nbgpu.h declares: name -> (restype, argtypes)
+_P = C.c_void_p
+SIGNATURES = {
+    "nbg_maglev_create": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_uint64,
+                                    C.c_int, C.POINTER(_P)]),
+    "nbg_maglev_create_from_lut": (C.c_int, [_P, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(_P)]),
+    "nbg_maglev_destroy": (None, [_P]),
+    "nbg_maglev_backends": (C.c_uint32, [_P]),
+    "nbg_maglev_table_size": (C.c_uint64, [_P]),
+    "nbg_maglev_lut": (C.c_int, [_P, _P, C.c_uint64]),
+    "nbg_maglev_reserve": (C.c_int, [_P, C.c_uint64]),
+    "nbg_maglev_classify_device": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64, C.c_uint32,
+                                             _P, _P, _P, _P]),
+    "nbg_maglev_check": (C.c_int, [_P]),
+    "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
+    "nbg_last_error": (C.c_char_p, []),
+    "nbg_lut_build_host": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_uint64, _P]),
+    "nbg_trace_layout": (C.c_uint64, [C.c_uint64, C.c_int, C.c_uint64, _P, _P]),
+    "nbg_trace_fill": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),
+}
+
+
+class NbgError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        super().__init__(f"{where} failed ({code}): {last_error()}")
+
+
+def _load() -> C.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback for the Maglev path)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    msg = lib.nbg_last_error()
+    return msg.decode(errors="replace") if msg else ""
+
+
+def check(rc: int, where: str) -> None:
+    if rc != NBG_OK:
+        raise NbgError(rc, where)
+
+
+def names_args(names):
+    enc = [n.encode("utf-8") for n in names]
+    arr = (C.c_char_p * len(enc))(*enc)
+    lens = (C.c_uint32 * len(enc))(*[len(e) for e in enc])
+    return arr, lens, enc

@@ -1,0 +1,150 @@
+"""Python surface of the MI355X Maglev path (thin wrapper over include/nbgpu.h).
+
+Mirrors the reference's Maglev NF (test/maglev/src/nf.rs): `Maglev(backends, 65537)`
+builds the consistent-hash LUT (nf.rs:70-76) and `Maglev.group_by(...)` performs, for a
+whole device-resident batch, what `parse::<MacHeader>().transform(swap).group_by(ct,
+group_fn)` does per packet (nf.rs:92-108): MAC swap, 5-tuple FNV-1a, `lut[hash % M]`,
+and the per-group FIFO order of the group_by MPSC queues (operators/group_by.rs:43-55).
+PyTorch is only used for device memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import NBG_LUT_GLOBAL, NBG_SENTINEL, NBG_SWAP_MACS, check, lib
+
+__all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def build_lut(backends: Sequence[str], lut_size: int = 65537) -> np.ndarray:
+    """The product's host LUT builder (Maglev::new, nf.rs:70-76) -> u16 entries."""
+    arr, lens, _keep = _lib.names_args(backends)
+    out = np.empty(lut_size, dtype=np.uint16)
+    check(lib.nbg_lut_build_host(arr, lens, len(backends), lut_size, out.ctypes.data), "nbg_lut_build_host")
+    return out
+
+
+def make_trace(n: int, mode: int = 0, seed: int = 0x4E42474D41474C56, n_flows: int = 65536,
+               unique: bool = False):
+    """Synthetic trace on the host: (bytes u8[size], offsets u32[n], lens u16[n])."""
+    off = np.empty(n, dtype=np.uint32)
+    ln = np.empty(n, dtype=np.uint16)
+    size = lib.nbg_trace_layout(n, mode, seed, off.ctypes.data, ln.ctypes.data)
+    buf = np.zeros(max(size, 1), dtype=np.uint8)
+    flags = _lib.NBG_TRACE_UNIQUE if unique else 0
+    check(lib.nbg_trace_fill(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, n, seed, n_flows, flags),
+          "nbg_trace_fill")
+    return buf, off, ln
+
+
+@dataclass
+class GroupedBatch:
+    """Result of one batch: per-packet backend (NBG_SENTINEL = would-panic packet), and
+    the per-group FIFO order: perm[group_start[g]:group_start[g]+counts[g]] are the
+    packets of group g in arrival order (groups 0..n-1, then the sentinel group)."""
+    backend: "object"
+    perm: "object"
+    counts: "object"
+
+    def group_start(self):
+        c = self.counts.cpu().numpy().view(np.uint32).astype(np.int64)
+        return np.concatenate([[0], np.cumsum(c)[:-1]])
+
+
+class Maglev:
+    """Device-resident Maglev consistent-hash steering (test/maglev/src/nf.rs:14-111)."""
+
+    def __init__(self, backends: Optional[Sequence[str]] = None, lut_size: int = 65537, device: int = 0,
+                 lut: Optional[np.ndarray] = None, n_backends: Optional[int] = None):
+        self._h = C.c_void_p()
+        self.device = device
+        if lut is not None:
+            lut = np.ascontiguousarray(lut, dtype=np.uint16)
+            nb = int(n_backends if n_backends is not None else int(lut.max()) + 1)
+            check(lib.nbg_maglev_create_from_lut(lut.ctypes.data, lut.size, nb, device, C.byref(self._h)),
+                  "nbg_maglev_create_from_lut")
+        else:
+            if not backends:
+                raise ValueError("backends must be non-empty")
+            arr, lens, _keep = _lib.names_args(backends)
+            check(lib.nbg_maglev_create(arr, lens, len(backends), lut_size, device, C.byref(self._h)),
+                  "nbg_maglev_create")
+        self.n_backends = lib.nbg_maglev_backends(self._h)
+        self.lut_size = lib.nbg_maglev_table_size(self._h)
+
+    def close(self) -> None:
+        if self._h:
+            lib.nbg_maglev_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def lut(self) -> np.ndarray:
+        out = np.empty(self.lut_size, dtype=np.uint16)
+        check(lib.nbg_maglev_lut(self._h, out.ctypes.data, out.size), "nbg_maglev_lut")
+        return out
+
+    def reserve(self, max_pkts: int) -> None:
+        check(lib.nbg_maglev_reserve(self._h, max_pkts), "nbg_maglev_reserve")
+
+    def check(self) -> None:
+        check(lib.nbg_maglev_check(self._h), "nbg_maglev_check")
+
+    def group_by(self, pkts, n_pkts: int, *, stride: int = 64, frame_len: int = 60, offsets=None, lens=None,
+                 swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_global: bool = False,
+                 backend=None, perm=None, counts=None, stream=None) -> GroupedBatch:
+        """Classify a device-resident batch (torch uint8 tensor on this device).
+
+        Packet i starts at pkts[offsets[i]] (u32 tensor) or pkts[i*stride]; its length is
+        lens[i] (u16 tensor) or frame_len.  Asynchronous on `stream` (default: torch's
+        current stream)."""
+        import torch
+
+        dev = pkts.device
+        if backend is None:
+            backend = torch.empty(n_pkts, dtype=torch.uint16, device=dev)
+        scatter = group and scatter
+        if scatter and perm is None:
+            perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev)
+        if group and counts is None:
+            counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        flags = (NBG_SWAP_MACS if swap_macs else 0) | (NBG_LUT_GLOBAL if lut_global else 0)
+        rc = lib.nbg_maglev_classify_device(self._h, _ptr(pkts), _ptr(offsets), _ptr(lens), stride, frame_len,
+                                            n_pkts, flags, _ptr(backend), _ptr(perm) if scatter else None,
+                                            _ptr(counts) if group else None, stream)
+        check(rc, "nbg_maglev_classify_device")
+        return GroupedBatch(backend, perm if scatter else None, counts if group else None)
+
+    def group_by_host(self, frames: Sequence[bytearray], swap_macs: bool = True, group: bool = True):
+        """Host mbuf path: frames are mutable byte buffers (their MACs are swapped in place).
+        Returns numpy (backend u16[n], perm u32[n] | None, counts u32[nb+1] | None)."""
+        n = len(frames)
+        keep = [(C.c_char * len(f)).from_buffer(f) if len(f) else (C.c_char * 1)() for f in frames]
+        ptrs = (C.c_void_p * max(n, 1))(*[C.addressof(k) for k in keep])
+        lens = np.array([len(f) for f in frames], dtype=np.uint16)
+        backend = np.empty(max(n, 1), dtype=np.uint16)
+        perm = np.empty(max(n, 1), dtype=np.uint32) if group else None
+        counts = np.empty(self.n_backends + 1, dtype=np.uint32) if group else None
+        flags = NBG_SWAP_MACS if swap_macs else 0
+        rc = lib.nbg_maglev_classify_host(self._h, ptrs, lens.ctypes.data, n, flags, backend.ctypes.data,
+                                          perm.ctypes.data if group else None,
+                                          counts.ctypes.data if group else None)
+        check(rc, "nbg_maglev_classify_host")
+        return backend[:n], (perm[:n] if group else None), counts

@@ -1,0 +1,207 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the C oracle on the same seeded inputs.
+
+Bit-exact on backend[], on the MAC-swapped packet bytes, on the per-group FIFO order
+(perm) and on the group sizes.  Reference semantics: test/maglev/src/nf.rs:92-108.
+"""
+import numpy as np
+import pytest
+
+import orc
+
+pytestmark = pytest.mark.gpu
+
+NAMES65 = [f"backend-{i}" for i in range(65)]
+
+
+@pytest.fixture(scope="module")
+def mg65(torch_cuda):
+    from netbricks_amd import Maglev
+
+    m = Maglev(NAMES65, 65537)
+    yield m
+    m.close()
+
+
+def _run(torch, mg, buf, n, *, offs=None, lens=None, stride=64, frame_len=60, swap=True, lut_global=False):
+    dev = torch.device("cuda:0")
+    d_buf = torch.from_numpy(buf.copy()).to(dev)
+    d_off = None if offs is None else torch.from_numpy(offs.astype(np.uint32).view(np.int32)).to(dev)
+    d_len = None if lens is None else torch.from_numpy(lens.astype(np.uint16).view(np.int16)).to(dev)
+    d_off = None if d_off is None else d_off.view(torch.uint32)
+    d_len = None if d_len is None else d_len.view(torch.uint16)
+    r = mg.group_by(d_buf, n, stride=stride, frame_len=frame_len, offsets=d_off, lens=d_len, swap_macs=swap,
+                    lut_global=lut_global)
+    torch.cuda.synchronize()
+    mg.check()
+    backend = r.backend.view(torch.int16).cpu().numpy().view(np.uint16)
+    perm = r.perm.view(torch.int32).cpu().numpy().view(np.uint32)[:n]
+    counts = r.counts.view(torch.int32).cpu().numpy().view(np.uint32)
+    return d_buf.cpu().numpy(), backend, perm, counts
+
+
+def _oracle(buf, n, lut, nb, **kw):
+    ref = buf.copy()
+    be = orc.classify(ref, n, lut, **kw)
+    perm, counts = orc.group(be, nb)
+    return ref, be, perm, counts
+
+
+def _assert_same(got, exp):
+    gbuf, gbe, gperm, gcnt = got
+    ebuf, ebe, eperm, ecnt = exp
+    np.testing.assert_array_equal(gbe, ebe)
+    np.testing.assert_array_equal(gcnt, ecnt)
+    np.testing.assert_array_equal(gperm, eperm)
+    np.testing.assert_array_equal(gbuf, ebuf)
+
+
+def test_lut_matches_oracle(mg65):
+    np.testing.assert_array_equal(mg65.lut(), orc.lut_build(NAMES65, 65537).astype(np.uint16))
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 1024, 1025, 4096, 65536 + 77])
+@pytest.mark.parametrize("lut_global", [False, True])
+def test_c2_small(torch_cuda, mg65, n, lut_global):
+    from netbricks_amd import make_trace
+
+    buf, _, _ = make_trace(n, 0, seed=1234 + n)
+    lut = orc.lut_build(NAMES65, 65537)
+    got = _run(torch_cuda, mg65, buf, n, lut_global=lut_global)
+    _assert_same(got, _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
+
+
+def test_c2_full_1m(torch_cuda, mg65):
+    """BASELINE config C2 size: 1,048,576 x 64-B frames, 65 backends, M=65537."""
+    from netbricks_amd import make_trace
+
+    n = 1 << 20
+    buf, _, _ = make_trace(n, 0)
+    lut = orc.lut_build(NAMES65, 65537)
+    got = _run(torch_cuda, mg65, buf, n)
+    exp = _oracle(buf, n, lut, 65, stride=64, fixed_len=60)
+    _assert_same(got, exp)
+    # size-independent properties: perm is a permutation, groups sorted, counts sum to n
+    perm, counts = got[2], got[3]
+    assert counts.sum() == n
+    assert np.array_equal(np.sort(perm), np.arange(n, dtype=np.uint32))
+
+
+def test_no_swap_and_no_group(torch_cuda, mg65):
+    from netbricks_amd import make_trace
+
+    n = 5000
+    buf, _, _ = make_trace(n, 0, seed=7)
+    lut = orc.lut_build(NAMES65, 65537)
+    dev = torch_cuda.device("cuda:0")
+    d_buf = torch_cuda.from_numpy(buf.copy()).to(dev)
+    r = mg65.group_by(d_buf, n, swap_macs=False, group=False)
+    torch_cuda.cuda.synchronize()
+    ref = buf.copy()
+    exp = orc.classify(ref, n, lut, stride=64, fixed_len=60, swap=False)
+    np.testing.assert_array_equal(r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16), exp)
+    np.testing.assert_array_equal(d_buf.cpu().numpy(), buf)  # untouched
+
+
+def test_reference_names_lut3(torch_cuda):
+    """The reference's own backend list (test/maglev/src/main.rs:36)."""
+    from netbricks_amd import Maglev, make_trace
+
+    names = ["Larry", "Curly", "Moe"]
+    mg = Maglev(names, 65537)
+    n = 10000
+    buf, _, _ = make_trace(n, 0, seed=99)
+    lut = orc.lut_build(names, 65537)
+    _assert_same(_run(torch_cuda, mg, buf, n), _oracle(buf, n, lut, 3, stride=64, fixed_len=60))
+    mg.close()
+
+
+@pytest.mark.parametrize("nb,m", [(1000, 655373), (300, 65537), (2, 7), (257, 1009)])
+def test_imix_descriptors(torch_cuda, nb, m):
+    """C3-like: IMIX frames at 64-B aligned offsets with a length array; wide/global LUTs."""
+    from netbricks_amd import Maglev, make_trace
+
+    names = [f"be{i}" for i in range(nb)]
+    mg = Maglev(names, m)
+    n = 20000
+    buf, off, ln = make_trace(n, 1, seed=nb)
+    lut = orc.lut_build(names, m)
+    got = _run(torch_cuda, mg, buf, n, offs=off, lens=ln)
+    _assert_same(got, _oracle(buf, n, lut, nb, offs=off, lens=ln))
+    mg.close()
+
+
+def _edge_frames(rng):
+    """Hand-built edge cases: IHL 0..15 with options, runts, non-IPv4, odd lengths."""
+    frames = []
+    base = bytearray(rng.integers(0, 256, 128, dtype=np.uint8).tobytes())
+    base[12:14] = b"\x08\x00"
+    for ihl in range(16):
+        for ln in (13, 14, 15, 33, 34, 37, 38, 47, 48, 49, 60, 64, 78, 79, 100, 128):
+            f = bytearray(base[:ln])
+            if ln > 14:
+                f[14] = 0x40 | ihl
+            frames.append(f)
+    for et in (b"\x86\xdd", b"\x08\x06", b"\x81\x00"):
+        f = bytearray(base[:64])
+        f[12:14] = et
+        frames.append(f)
+    frames.append(bytearray())
+    return frames
+
+
+def _pack(frames, align):
+    offs, lens, pos = [], [], 0
+    for f in frames:
+        offs.append(pos)
+        lens.append(len(f))
+        pos += (len(f) + align - 1) // align * align + align
+    buf = np.zeros(pos + 128, dtype=np.uint8)
+    for o, f in zip(offs, frames):
+        buf[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
+    return buf, np.array(offs, dtype=np.uint32), np.array(lens, dtype=np.uint16)
+
+
+@pytest.mark.parametrize("align", [1, 4, 64])
+def test_edge_cases(torch_cuda, mg65, align):
+    rng = np.random.default_rng(5)
+    frames = _edge_frames(rng)
+    buf, off, ln = _pack(frames, align)
+    if align == 1:
+        off = off + 3  # deliberately misaligned frame starts
+        buf = np.concatenate([np.zeros(3, np.uint8), buf])
+    lut = orc.lut_build(NAMES65, 65537)
+    n = len(frames)
+    got = _run(torch_cuda, mg65, buf, n, offs=off, lens=ln)
+    exp = _oracle(buf, n, lut, 65, offs=off, lens=ln)
+    _assert_same(got, exp)
+    assert (got[1] == 0xFFFF).any() and (got[1] != 0xFFFF).any()
+
+
+def test_repeat_calls_epochs(torch_cuda, mg65):
+    """Many back-to-back calls reuse the look-back scratch via epochs (no memset)."""
+    from netbricks_amd import make_trace
+
+    lut = orc.lut_build(NAMES65, 65537)
+    for k, n in enumerate([3000, 100000, 1024, 77777, 3000]):
+        buf, _, _ = make_trace(n, 0, seed=k)
+        _assert_same(_run(torch_cuda, mg65, buf, n), _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
+
+
+def test_host_path(torch_cuda, mg65):
+    """nbg_maglev_classify_host: mbuf-like host frames -> H2D -> kernel -> D2H, MACs swapped in place."""
+    rng = np.random.default_rng(11)
+    from netbricks_amd import make_trace
+
+    n = 3000
+    buf, off, ln = make_trace(n, 1, seed=3)
+    frames = [bytearray(buf[o:o + l].tobytes()) for o, l in zip(off, ln)]
+    frames += _edge_frames(rng)
+    lut = orc.lut_build(NAMES65, 65537)
+    pbuf, poff, pln = _pack([bytearray(f) for f in frames], 64)
+    exp = _oracle(pbuf, len(frames), lut, 65, offs=poff, lens=pln)
+    be, perm, counts = mg65.group_by_host(frames)
+    np.testing.assert_array_equal(be, exp[1])
+    np.testing.assert_array_equal(perm, exp[2])
+    np.testing.assert_array_equal(counts, exp[3])
+    for f, o, l in zip(frames, poff, pln):
+        assert bytes(f) == exp[0][o:o + l].tobytes()
