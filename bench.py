@@ -3,8 +3,14 @@
 
 Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,576 synthetic
 64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM.  One step = one batch
-through `nbg_maglev_classify_device` (classify kernel + group scatter kernel).  Steps rotate
-over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache) so repeats are not cache hits.
+through `nbg_maglev_classify_device` (classify kernel + grouping kernel), MAC swap in place.
+Steps rotate over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache) and are issued
+round-robin on `--streams` HIP streams (independent batches, one handle per stream: NetBricks
+runs one pipeline per RX queue), so one batch's latency-bound grouping overlaps the next
+batch's bandwidth-bound classify.
+
+Roofline: the classify kernel (dominant) is timed with HIP events around each launch in a
+separate single-stream pass (NBG_DEFER_GROUP splits it from the grouping kernel).
 
 Multi-GPU (`torch.distributed.run --nproc-per-node N`): packet batches shard trivially; each
 rank owns its own batches (weak scaling, no data-path collective).  The LUT is built on rank 0
@@ -15,6 +21,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -33,7 +40,7 @@ FRAME = 60
 N_BATCHES = 8
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet: classify kernel = 64 B read + 12 B MAC write
-# + 2 B backend write; whole path adds the scatter's 4 B perm write (= 82 B, C2).
+# + 2 B backend write; the whole path adds the grouping kernel's 4 B perm write (= 82 B, C2).
 CLASSIFY_BYTES = 64 + 12 + 2
 PATH_BYTES = 82
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -43,12 +50,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(batches_host, lut, target_cpu_s=12.0):
+def cpu_baseline(batch_host, lut, target_cpu_s=12.0):
     """Reference per-core loop restated in C (oracle/, kind "port"), timed on this host's cores."""
-    import ctypes as C
-
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import orc  # test infrastructure: the oracle is only the baseline/checker here
+    import orc  # test infrastructure: the oracle is the baseline/checker only
 
     L = orc.lib()
     try:
@@ -57,39 +62,33 @@ def cpu_baseline(batches_host, lut, target_cpu_s=12.0):
         cores = os.cpu_count() or 1
     threads = max(1, min(cores, 16))
     lut32 = np.ascontiguousarray(lut, dtype=np.uint32)
-    bufs = [b.copy() for b in batches_host[:2]]
-    # one timing pass to size the sample
-    t = L.orc_cpu_baseline(bufs[0].ctypes.data, None, SLOT, None, FRAME, BATCH, lut32.ctypes.data, TABLE,
-                           N_BACKENDS, 1, threads, None)
-    passes = max(1, int(target_cpu_s / max(t * threads, 1e-6)))
-    passes = min(passes, 400)
-    total_s = 0.0
-    for p in range(passes):
-        b = bufs[p % len(bufs)]
-        total_s += L.orc_cpu_baseline(b.ctypes.data, None, SLOT, None, FRAME, BATCH, lut32.ctypes.data, TABLE,
-                                      N_BACKENDS, 1, threads, None)
+    buf = batch_host.copy()
+
+    def one():
+        return L.orc_cpu_baseline(buf.ctypes.data, None, SLOT, None, FRAME, BATCH, lut32.ctypes.data, TABLE,
+                                  N_BACKENDS, 1, threads, None)
+
+    t = one()  # sizes the sample (and warms the memo map)
+    passes = int(min(max(1, target_cpu_s / max(t * threads, 1e-6)), 400))
+    total_s = sum(one() for _ in range(passes))
     mpps = passes * BATCH / total_s / 1e6
     try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+        model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:
         model = "unknown"
-    _ = C
     return {"value": round(mpps, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-            "sample": f"{passes} passes x 1,048,576 C2 packets (64-B UDP, 65 backends, FNV memo map as "
-                      f"nf.rs:91,104, 32-pkt bursts, per-group rings), {threads} pinned threads, "
-                      f"{total_s * threads:.1f} CPU-s; host CPU: {model}"}
+            "sample": f"{passes} passes over one 1,048,576-packet C2 batch (64-B UDP, 65 backends, M=65537; "
+                      f"FNV-keyed memo map nf.rs:91,104, 32-pkt bursts, per-group 1024-slot rings), "
+                      f"{threads} pinned threads, {total_s * threads:.1f} CPU-s; host CPU: {model}"}
 
 
 def read_traffic():
     """HBM bytes per classify launch from the committed PMC profile (profiles/pmc_*.json), if any."""
-    import glob
-
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
-        d = json.load(open(files[-1]))
-        return d.get("classify_hbm_bytes_per_launch")
+        return json.load(open(files[-1])).get("classify_hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -97,10 +96,12 @@ def read_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--mac-record", action="store_true",
+                    help="write the swapped MACs as dense 12-B egress records instead of in place")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--lut-global", action="store_true", help="L2-gather LUT instead of LDS-staged")
     args = ap.parse_args()
 
     import torch
@@ -109,11 +110,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     import netbricks_amd as nb
 
@@ -124,85 +124,93 @@ def main():
             lut_t.copy_(torch.from_numpy(nb.build_lut(names, TABLE).astype(np.int32)))
         dist.broadcast(lut_t, 0)  # RCCL over xGMI, once per backend set
         lut = lut_t.cpu().numpy().astype(np.uint16)
-        mg = nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local)
+        mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(args.streams)]
     else:
-        mg = nb.Maglev(names, TABLE, device=local)
-        lut = mg.lut()
-    mg.reserve(BATCH)
+        mgs = [nb.Maglev(names, TABLE, device=local) for _ in range(args.streams)]
+        lut = mgs[0].lut()
 
     t0 = time.time()
-    host = []
+    host0 = None
     dbufs = []
     for b in range(N_BATCHES):
         buf, _, _ = nb.make_trace(BATCH, 0, seed=SEED + 1000003 * rank + b)
-        host.append(buf)
+        if b == 0:
+            host0 = buf.copy()
         dbufs.append(torch.from_numpy(buf).to(dev))
     log(f"[rank {rank}] traces ready in {time.time() - t0:.1f}s")
-    backend = torch.empty(BATCH, dtype=torch.uint16, device=dev)
-    perm = torch.empty(BATCH, dtype=torch.uint32, device=dev)
-    counts = torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    streams = [torch.cuda.Stream(dev) for _ in range(args.streams)]
+    outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                 perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                 counts=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev),
+                 mac_out=torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) if args.mac_record else None)
+            for _ in range(args.streams)]
 
-    def step(i, ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        mg.group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
-                    lut_global=args.lut_global, backend=backend, perm=perm, counts=counts, stream=sp)
-        if ev is not None:
-            ev[1].record(stream)
+    def step(i):
+        j = i % args.streams
+        mgs[j].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
+                        stream=streams[j].cuda_stream, **outs[j])
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize(dev)
-    mg.check()
+    sync_all()
+    for m in mgs:
+        m.check()
 
-    # ---- timed region: K steps, events around each step on the launch stream
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # ---- timed region: K steps over all streams, bracketed by barrier + synchronize
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync_all()
+    start_ev = torch.cuda.Event(enable_timing=True)
+    start_ev.record(torch.cuda.current_stream(dev))
+    for st in streams:
+        st.wait_event(start_ev)
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(i, evs[i])
-    torch.cuda.synchronize(dev)
+        step(i)
+    sync_all()
     elapsed = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
-    step_ms = np.array([a.elapsed_time(b) for a, b in evs])
-    dev_elapsed = evs[0][0].elapsed_time(evs[-1][1]) / 1e3
-    mg.check()
-
-    t = torch.tensor([elapsed, dev_elapsed], dtype=torch.float64, device=dev)
+    for m in mgs:
+        m.check()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, dev_elapsed = float(t[0]), float(t[1])
+    elapsed = float(t[0])
 
-    # ---- per-kernel roofline: split classify / scatter with events in a second pass
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # ---- roofline pass: classify kernel timed alone (single stream, events around each launch)
+    st = streams[0]
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for i in range(args.steps):
-        kev[i][0].record(stream)
-        mg.group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
-                    lut_global=args.lut_global, backend=backend, counts=counts, scatter=False, stream=sp)
-        kev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    classify_only_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in kev]))
+        kev[i][0].record(st)
+        mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
+                        defer_group=True, stream=st.cuda_stream, **outs[0])
+        kev[i][1].record(st)
+        gev[i][0].record(st)
+        mgs[0].finish_group(st.cuda_stream)
+        gev[i][1].record(st)
+    sync_all()
+    classify_ms = np.array([a.elapsed_time(b) for a, b in kev])
+    group_ms = np.array([a.elapsed_time(b) for a, b in gev])
+    single_ms = kev[0][0].elapsed_time(gev[-1][1]) / args.steps
 
     total_pkts = BATCH * args.steps * world
     mpps = total_pkts / elapsed / 1e6
-    step_med = float(np.median(step_ms))
-    step_avg = float(np.mean(step_ms))
-    path_gbps = BATCH * PATH_BYTES / (step_avg / 1e3) / 1e9
-    ach = BATCH * CLASSIFY_BYTES / (classify_only_ms / 1e3) / 1e9
+    ms_step = elapsed / args.steps * 1e3
+    path_gbps = BATCH * PATH_BYTES * args.steps / elapsed / 1e9  # per GPU
+    ach = BATCH * CLASSIFY_BYTES / (classify_ms.mean() / 1e3) / 1e9
     traffic = read_traffic()
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             try:
-                cpu = cpu_baseline(host, lut)
-            except Exception as e:  # baseline is informational; never fail the bench on it
+                cpu = cpu_baseline(host0, lut)
+            except Exception as e:  # the baseline is informational; never fail the bench on it
                 log(f"cpu baseline failed: {e}")
         line = {
             "metric": "Mpps + HBM GB/s device-resident Maglev (64B pkts)",
@@ -211,7 +219,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -220,19 +228,22 @@ def main():
             "config": {"workload": "C2: Maglev 65 backends / 65537-slot LUT, 64B synthetic UDP, "
                                    "1M-packet device-resident batch per GPU",
                        "backends": N_BACKENDS, "table_size": TABLE, "batch_pkts": BATCH, "slot_bytes": SLOT,
-                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "swap_macs": True, "group_by": True,
-                       "lut": "global" if args.lut_global else "lds", "parallelism": f"shard{world}"},
-            "hbm_gbps_path": round(path_gbps, 1),
-            "step_ms_median": round(step_med, 4),
-            "device_mpps_per_gpu": round(BATCH * args.steps / dev_elapsed / 1e6, 1),
+                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES,
+                       "mac_swap": "12-B egress records" if args.mac_record else "in place",
+                       "group_by": "perm + counts", "streams": args.streams, "parallelism": f"shard{world}"},
+            "hbm_gbps_per_gpu": round(path_gbps, 1),
+            "hbm_bytes_per_pkt": PATH_BYTES,
+            "single_stream_ms_per_step": round(single_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "classify_kernel (grouping variant, as in the step)", "bytes_per_pkt": CLASSIFY_BYTES,
-                         "avg_launch_us": round(classify_only_ms * 1e3, 2)},
+                         "kernel": "classify_kernel<GlobalU8,F4,HIST,1>", "bytes_per_pkt": CLASSIFY_BYTES,
+                         "pkts_per_launch": BATCH, "avg_launch_us": round(classify_ms.mean() * 1e3, 2),
+                         "group_kernel_avg_us": round(group_ms.mean() * 1e3, 2)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    mg.close()
+    for m in mgs:
+        m.close()
     if world > 1:
         dist.destroy_process_group()
 

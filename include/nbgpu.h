@@ -46,8 +46,14 @@ extern "C" {
 #define NBG_SENTINEL 0xFFFFu
 
 /* classify flags */
-#define NBG_SWAP_MACS 0x1u     /* apply MacHeader::swap_addresses in place (nf.rs:94-98) */
-#define NBG_LUT_GLOBAL 0x2u    /* force the L2-gather LUT variant instead of the LDS-staged one */
+#define NBG_SWAP_MACS 0x1u      /* apply MacHeader::swap_addresses in place (nf.rs:94-98) */
+#define NBG_LUT_LDS 0x2u        /* stage the LUT in LDS per workgroup instead of gathering from L2
+                                   (u8/u16 LUT <= 72 KiB; lower occupancy, kept as a measured variant) */
+#define NBG_OWNED_WINDOWS 0x4u  /* descriptor mode: the 64 B at every packet start belong to that
+                                   packet (true for DPDK mbufs, whose data room is >= 2 KiB) */
+#define NBG_WB_PARTIAL 0x8u     /* write back only the 16 B holding the MACs (measurement knob) */
+#define NBG_DEFER_GROUP 0x10u   /* launch only the classify kernel; nbg_maglev_finish_group launches
+                                   the grouping kernel (e.g. on another stream, after an event) */
 
 typedef struct nbg_maglev nbg_maglev;
 
@@ -84,7 +90,7 @@ int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts);
  *   d_off      nullable u32 byte offsets (descriptor mode, e.g. IMIX)
  *   d_len      nullable u16 frame lengths (mbuf data_len); NULL => every frame is fixed_len
  *   n_pkts     packets in the batch, < 2^30
- *   flags      NBG_SWAP_MACS | NBG_LUT_GLOBAL
+ *   flags      NBG_SWAP_MACS | NBG_LUT_LDS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP
  *   d_backend  out, n_pkts u16: backend index, or NBG_SENTINEL
  *   d_perm     out (nullable), n_pkts u32: packet indices grouped by backend 0..n-1 then the
  *              sentinel group, ascending index inside each group (per-group FIFO order)
@@ -92,14 +98,30 @@ int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts);
  *   stream     hipStream_t (NULL = default stream); the call is asynchronous
  *
  * Frames shorter than 48 B, unaligned or with IHL != 5 take a byte-wise slow path
- * with identical results.
+ * with identical results.  The kernel reads (and, with NBG_SWAP_MACS, rewrites with
+ * their own values) the bytes of the 64-B window at each packet start that lie inside
+ * the frame, or the whole window when it is owned: fixed slots with stride >= 64, or
+ * NBG_OWNED_WINDOWS.  Windows of distinct packets must not overlap in that case.
  */
 int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
                                uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
                                uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, void* stream);
 
-/* Synchronise the handle's last stream and report a device-side fault (a bounded
- * look-back spin that gave up) as NBG_ETIMEDOUT.  Not needed on the hot path. */
+/* As nbg_maglev_classify_device, plus d_mac_out (nullable, n_pkts x 12 B): with NBG_SWAP_MACS
+ * the swapped MAC pair of packet i (its new bytes 0..11) is written to d_mac_out + 12*i and
+ * the packet bytes are left untouched — the egress rewrite record a host-mbuf pipeline
+ * applies before TX (what nbg_maglev_classify_host does).  Packets shorter than 14 B get no
+ * record (their 12 bytes are left as they were). */
+int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
+                                  uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
+                                  uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
+                                  void* stream);
+
+/* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP on
+ * `stream` (which must be ordered after that classify).  No-op when nothing is pending. */
+int nbg_maglev_finish_group(nbg_maglev* h, void* stream);
+
+/* Synchronise the handle's last stream and report any HIP error.  Not needed on the hot path. */
 int nbg_maglev_check(nbg_maglev* h);
 
 /*

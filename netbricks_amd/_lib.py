@@ -14,7 +14,10 @@ LIB_PATH = os.path.join(_HERE, "libnbgpu.so")
 NBG_OK = 0
 NBG_SENTINEL = 0xFFFF
 NBG_SWAP_MACS = 0x1
-NBG_LUT_GLOBAL = 0x2
+NBG_LUT_LDS = 0x2
+NBG_OWNED_WINDOWS = 0x4
+NBG_WB_PARTIAL = 0x8
+NBG_DEFER_GROUP = 0x10
 NBG_TRACE_UNIQUE = 0x1
 
 # every symbol include/nbgpu.h declares: name -> (restype, argtypes)
@@ -30,6 +33,9 @@ SIGNATURES = {
     "nbg_maglev_reserve": (C.c_int, [_P, C.c_uint64]),
     "nbg_maglev_classify_device": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64, C.c_uint32,
                                              _P, _P, _P, _P]),
+    "nbg_maglev_classify_device_ex": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64, C.c_uint32,
+                                                _P, _P, _P, _P, _P]),
+    "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_last_error": (C.c_char_p, []),

@@ -1,18 +1,22 @@
 // CDNA4 (gfx950) kernels for the Maglev flow-steering hot path.
 //
-// classify_kernel — one lane per packet (4 packets per lane per tile):
-//   parse::<MacHeader> (offset 14, framework/src/headers/mac.rs:96-106)
-//   swap_addresses      (headers/mac.rs:140-145)            -> 12-B store
-//   ipv4_extract_flow   (utils/flow.rs:53-62)
+// classify_kernel — per packet (test/maglev/src/nf.rs:92-106):
+//   parse::<MacHeader>   offset 14 (framework/src/headers/mac.rs:96-106, feature "performance")
+//   swap_addresses       headers/mac.rs:140-145
+//   ipv4_extract_flow    utils/flow.rs:53-62
 //   FNV-1a 64 over the packed little-endian Flow (utils/flow.rs:10-18,105-110)
-//   lut[hash % M]       (test/maglev/src/nf.rs:78-81)       -> u16 store
-//   per-tile histogram of backends + decoupled look-back over tiles, giving every
-//   tile its exclusive per-backend prefix (the stable FIFO order of group_by.rs:46-51).
-// scatter_kernel — per tile, wave ballot multisplit ranks + per-wave LDS counters,
-//   writes perm[] = packet indices grouped by backend in arrival order.
+//   lut[hash % M]        test/maglev/src/nf.rs:78-81
+//   + a per-tile backend histogram for the group_by FIFO order (operators/group_by.rs:46-51).
+//   Loads are cooperative: a wave reads 64 packets' 64-B header windows as 16-B chunks
+//   (4 lanes per window, contiguous 1 KiB per instruction for the 64-B slot layout),
+//   transposes them through LDS to one packet per lane, and the lane holding chunk 0
+//   applies the MAC swap in registers and writes the window back with full-line stores.
+// scan_kernel — per backend bin, exclusive scan of the tile histograms over tiles; the
+//   last block to arrive scans the group totals into group bases.
+// scatter_kernel — per tile, wave ballot multisplit ranks (stable), a local counting sort
+//   in LDS, and coalesced stores of perm[] = packet indices grouped by backend.
 //
-// Integer-only; no MFMA.  HBM-bound: 64 B read + 12 B + 2 B written per packet in
-// classify, 2 B read + 4 B written in scatter.
+// Integer/byte work only; no MFMA.  HBM-bound.
 #include <hip/hip_runtime.h>
 
 #include "nbgpu_internal.h"
@@ -23,9 +27,6 @@ namespace {
 
 constexpr uint32_t kSentinel = NBG_SENTINEL;
 constexpr uint32_t kEth = 14;
-constexpr uint32_t kFlagAggregate = 1;
-constexpr uint32_t kFlagPrefix = 2;
-constexpr uint32_t kSpinLimit = 1u << 22;
 
 // LUT placement / width variants.
 enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3 };
@@ -55,26 +56,25 @@ __device__ __forceinline__ uint32_t mod_barrett(uint32_t lo, uint32_t hi, uint32
   return static_cast<uint32_t>(r);
 }
 
-// FNV over Flow{src_ip, dst_ip, src_port, dst_port, proto} (LE fields of BE-read values):
-// byte order = p[15],p[14],p[13],p[12], p[19..16], p[ps+1],p[ps], p[ps+3],p[ps+2], p[9]
-// where p = frame + 14.
-__device__ __forceinline__ void fnv_flow(uint32_t& lo, uint32_t& hi, uint32_t src_be, uint32_t dst_be, uint32_t ports_be,
+// FNV over Flow{src_ip, dst_ip, src_port, dst_port, proto} (LE fields of BE-read values).
+// src/dst/ports are the wire bytes packed little-endian (wire byte k at bits 8k), so the
+// hashed byte order is src[3..0], dst[3..0], ports[1],ports[0], ports[3],ports[2], proto.
+__device__ __forceinline__ void fnv_flow(uint32_t& lo, uint32_t& hi, uint32_t src, uint32_t dst, uint32_t ports,
                                          uint32_t proto) {
-  // src_be / dst_be / ports_be are the wire bytes packed little-endian (byte k at bits 8k).
   lo = 0x84222325u;  // 0xcbf29ce484222325
   hi = 0xcbf29ce4u;
-  fnv_step(lo, hi, src_be >> 24);
-  fnv_step(lo, hi, (src_be >> 16) & 0xffu);
-  fnv_step(lo, hi, (src_be >> 8) & 0xffu);
-  fnv_step(lo, hi, src_be & 0xffu);
-  fnv_step(lo, hi, dst_be >> 24);
-  fnv_step(lo, hi, (dst_be >> 16) & 0xffu);
-  fnv_step(lo, hi, (dst_be >> 8) & 0xffu);
-  fnv_step(lo, hi, dst_be & 0xffu);
-  fnv_step(lo, hi, (ports_be >> 8) & 0xffu);
-  fnv_step(lo, hi, ports_be & 0xffu);
-  fnv_step(lo, hi, ports_be >> 24);
-  fnv_step(lo, hi, (ports_be >> 16) & 0xffu);
+  fnv_step(lo, hi, src >> 24);
+  fnv_step(lo, hi, (src >> 16) & 0xffu);
+  fnv_step(lo, hi, (src >> 8) & 0xffu);
+  fnv_step(lo, hi, src & 0xffu);
+  fnv_step(lo, hi, dst >> 24);
+  fnv_step(lo, hi, (dst >> 16) & 0xffu);
+  fnv_step(lo, hi, (dst >> 8) & 0xffu);
+  fnv_step(lo, hi, dst & 0xffu);
+  fnv_step(lo, hi, (ports >> 8) & 0xffu);
+  fnv_step(lo, hi, ports & 0xffu);
+  fnv_step(lo, hi, ports >> 24);
+  fnv_step(lo, hi, (ports >> 16) & 0xffu);
   fnv_step(lo, hi, proto);
 }
 
@@ -95,19 +95,20 @@ __device__ __forceinline__ uint32_t lookup(const ClassifyArgs& a, const uint8_t*
 // Byte-wise path: any alignment, any length, any IHL.  Returns the bin (nb = sentinel).
 template <int LUTM, bool F4>
 __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const uint8_t* lut_lds, uint8_t* p,
-                                               uint32_t len) {
+                                                  uint32_t len, uint32_t pkt) {
   if (len < kEth) return a.nb;  // Packet::parse_header assert (interface/packet.rs:392-399)
   if (a.swap) {                 // transform runs before group_by over the batch
+    uint8_t* o = a.mac_out ? a.mac_out + static_cast<size_t>(pkt) * 12u : p;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const uint8_t d = p[k], s = p[k + 6];
-      p[k] = s;
-      p[k + 6] = d;
+      o[k] = s;
+      o[k + 6] = d;
     }
   }
   const uint8_t* q = p + kEth;
   const uint32_t plen = len - kEth;
-  if (plen < 20) return a.nb;
+  if (plen < 20) return a.nb;  // slice OOB in ipv4_extract_flow
   const uint32_t ps = (q[0] & 0xfu) * 4u;
   if (plen < ps + 4) return a.nb;
   const uint32_t src = q[12] | (q[13] << 8) | (q[14] << 16) | (static_cast<uint32_t>(q[15]) << 24);
@@ -119,222 +120,334 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
   return lookup<LUTM, F4>(a, lut_lds, lo, hi);
 }
 
-__device__ __forceinline__ unsigned long long pack_desc(uint32_t epoch, uint32_t flag, uint32_t v) {
-  return (static_cast<unsigned long long>((epoch << 2) | flag) << 32) | v;
+__device__ __forceinline__ uint4 ldg16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+// Non-temporal 16-B store: in-place window write-back streams ~10 % faster with nt (tools/membench).
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
+  const u32x4_t w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
 }
 
-template <int LUTM, bool F4, bool GROUP>
+template <int LUTM, bool F4, bool HIST, int R>
 __global__ __launch_bounds__(kBlock) void classify_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ uint32_t s_tile;
-  __shared__ uint32_t s_part[kBlock];
+  constexpr uint32_t kT = kBlock * R;  // packets per tile
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t part = lane & 3u, quad = lane >> 2;
   const uint32_t nbins = a.nb + 1;
-  const uint32_t hist_bytes = (nbins * 4u + 15u) & ~15u;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem);
-  uint8_t* lut_lds = smem + hist_bytes;
-  const uint32_t tid = threadIdx.x;
+  constexpr bool kLdsLut = LUTM == kLdsU8 || LUTM == kLdsU16;
+  const uint32_t lut_bytes = kLdsLut ? a.lut_lds_bytes : 0u;
+  uint8_t* lut_lds = smem;
+  uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + 4u * 64u * kXStride);
+  const bool desc = a.off != nullptr;
 
-  if constexpr (LUTM == kLdsU8 || LUTM == kLdsU16) {
+  if constexpr (kLdsLut) {
     const uint4* src = static_cast<const uint4*>(a.lut);
     uint4* dst = reinterpret_cast<uint4*>(lut_lds);
-    for (uint32_t k = tid; k < a.lut_lds_bytes / 16u; k += kBlock) dst[k] = src[k];
+    for (uint32_t k = tid; k < lut_bytes / 16u; k += kBlock) dst[k] = src[k];
   }
 
-  for (uint32_t iter = 0;; ++iter) {
-    if constexpr (GROUP) {
-      if (tid == 0) s_tile = static_cast<uint32_t>(atomicAdd(&a.ticket[0], 1ull));
+  for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    if constexpr (HIST) {
       for (uint32_t b = tid; b < nbins; b += kBlock) hist[b] = 0;
     }
     __syncthreads();
-    const uint32_t tile = GROUP ? s_tile : blockIdx.x + iter * gridDim.x;
-    if (tile >= a.n_tiles) {
-      if constexpr (GROUP) {
-        // Every block has taken its last ticket once it gets here; the last block to
-        // arrive resets both counters for the next launch on the stream.
-        if (tid == 0 && atomicAdd(&a.ticket[1], 1ull) == gridDim.x - 1) {
-          atomicExch(&a.ticket[0], 0ull);
-          atomicExch(&a.ticket[1], 0ull);
-        }
-      }
-      break;
-    }
+    const uint32_t wbase = tile * kT + wave * (64u * R);
 
-    // ---- issue every packet's header loads first (48 B per packet, 12 in flight per lane)
-    uint4 c0[kPktsPerThread], c1[kPktsPerThread], c2[kPktsPerThread];
-    uint8_t* pp[kPktsPerThread];
-    uint32_t plen[kPktsPerThread];
-    bool fast[kPktsPerThread];
-    const uint32_t base = tile * kTile;
 #pragma unroll
-    for (int k = 0; k < kPktsPerThread; ++k) {
-      const uint32_t i = base + k * kBlock + tid;
-      const bool valid = i < a.n_pkts;
-      const uint32_t ii = valid ? i : 0;
-      pp[k] = a.pkts + (a.off ? static_cast<size_t>(a.off[ii]) : static_cast<size_t>(ii) * a.stride);
-      plen[k] = a.len ? a.len[ii] : a.fixed_len;
-      fast[k] = valid && ((reinterpret_cast<uintptr_t>(pp[k]) & 15u) == 0) && plen[k] >= 48u;
-      if (fast[k]) {
-        const uint4* v = reinterpret_cast<const uint4*>(pp[k]);
-        c0[k] = v[0];
-        c1[k] = v[1];
-        c2[k] = v[2];
-      }
-    }
-    // ---- hash, swap, lookup
-#pragma unroll
-    for (int k = 0; k < kPktsPerThread; ++k) {
-      const uint32_t i = base + k * kBlock + tid;
-      if (i >= a.n_pkts) continue;
-      uint32_t bin;
-      // bytes 12..15 = c0.w: byte 14 = version/IHL
-      if (fast[k] && ((c0[k].w >> 16) & 0xfu) == 5u) {
-        // frame bytes: src 26..29 = c1.z>>16 | c1.w<<16 ; dst 30..33 = c1.w>>16 | c2.x<<16
-        //              ports 34..37 = c2.x>>16 | c2.y<<16 ; proto 23 = c1.y>>24
-        const uint32_t src = (c1[k].z >> 16) | (c1[k].w << 16);
-        const uint32_t dst = (c1[k].w >> 16) | (c2[k].x << 16);
-        const uint32_t ports = (c2[k].x >> 16) | (c2[k].y << 16);
-        uint32_t lo, hi;
-        fnv_flow(lo, hi, src, dst, ports, c1[k].y >> 24);
-        bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
-        if (a.swap) {
-          const uint32_t w0 = c0[k].x, w1 = c0[k].y, w2 = c0[k].z;
-          uint32_t* o = reinterpret_cast<uint32_t*>(pp[k]);
-          // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
-          o[0] = (w1 >> 16) | (w2 << 16);
-          o[1] = (w2 >> 16) | (w0 << 16);
-          o[2] = (w0 >> 16) | (w1 << 16);
-        }
-      } else {
-        bin = classify_slow<LUTM, F4>(a, lut_lds, pp[k], plen[k]);
-      }
-      a.backend[i] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-      if constexpr (GROUP) atomicAdd(&hist[bin], 1u);
-    }
+    for (int r = 0; r < R; ++r) {
+      const uint32_t rbase = wbase + r * 64u;
+      // ---- own packet (compute lane) metadata
+      const uint32_t p_own = rbase + lane;
+      const bool v_own = p_own < a.n_pkts;
+      const uint32_t off_own = desc ? (v_own ? a.off[p_own] : 0u) : 0u;
+      const uint32_t len_own = a.len ? (v_own ? a.len[p_own] : 0u) : a.fixed_len;
 
-    if constexpr (GROUP) {
-      __syncthreads();
-      // ---- decoupled look-back, one lane per bin
-      const bool last = tile == a.n_tiles - 1;
-      for (uint32_t b = tid; b < nbins; b += kBlock) {
-        const uint32_t agg = hist[b];
-        unsigned long long* d = a.desc + static_cast<size_t>(tile) * nbins + b;
-        uint32_t excl = 0;
-        if (tile == 0) {
-          __hip_atomic_store(d, pack_desc(a.epoch, kFlagPrefix, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          __hip_atomic_store(d, pack_desc(a.epoch, kFlagAggregate, agg), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-          for (int64_t j = static_cast<int64_t>(tile) - 1; j >= 0; --j) {
-            const unsigned long long* pd = a.desc + static_cast<size_t>(j) * nbins + b;
-            unsigned long long w;
-            uint32_t spins = 0;
-            for (;;) {
-              w = __hip_atomic_load(pd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              const uint32_t tag = static_cast<uint32_t>(w >> 32);
-              if ((tag >> 2) == a.epoch && (tag & 3u)) break;
-              if (++spins >= kSpinLimit) {
-                atomicOr(a.err, 1u);
-                w = pack_desc(a.epoch, kFlagPrefix, 0);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
+      // ---- cooperative window loads: lane = (quad, part) holds chunk `part` of packet k*16+quad
+      uint4 ch[4];
+      uint8_t* cp[4];
+      uint32_t cflag = 0;  // bit k: chunk k may be written back if the packet is fast-path
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t src = k * 16u + quad;
+        const uint32_t p = rbase + src;
+        const bool pv = p < a.n_pkts;
+        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own), src)) : 0u;
+        const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(len_own), src)) : a.fixed_len;
+        uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(p) * a.stride);
+        const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
+        // chunk readable/writable: inside the frame, or the window is owned by this packet
+        const bool inwin = a.win_owned || (part * 16u + 16u <= l);
+        const bool rd = pv && aligned && inwin;
+        cp[k] = base + part * 16u;
+        ch[k] = rd ? ldg16(cp[k]) : make_uint4(0, 0, 0, 0);
+        if (rd && l >= 48u) cflag |= 1u << k;
+      }
+      // ---- transpose: chunks 0..2 -> LDS [packet][80 B]
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = ch[k];
+      }
+      // ---- MAC swap in the loader lanes + window write-back (fast-path packets only)
+      if (a.swap) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
+          const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(ch[k].w), lane & ~3u));
+          const bool fast = ((cflag >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
+          if (!fast) continue;
+          uint4 v = ch[k];
+          if (part == 0u) {
+            const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
+            // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
+            v = make_uint4((w1 >> 16) | (w2 << 16), (w2 >> 16) | (w0 << 16), (w0 >> 16) | (w1 << 16), v.w);
+          }
+          if (a.mac_out) {
+            // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
+            if (part == 0u) {
+              uint32_t* o = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(rbase + k * 16u + quad) * 12u);
+              o[0] = v.x;
+              o[1] = v.y;
+              o[2] = v.z;
             }
-            excl += static_cast<uint32_t>(w);
-            if (((w >> 32) & 3u) == kFlagPrefix) break;
+          } else if (part == 0u || a.wb_full) {
+            stg16_nt(cp[k], v);  // chunks 1..3 unchanged: makes the write whole lines
           }
-          __hip_atomic_store(d, pack_desc(a.epoch, kFlagPrefix, excl + agg), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
         }
-        a.tile_prefix[static_cast<size_t>(tile) * nbins + b] = excl;
-        if (last) hist[b] = excl + agg;  // grand totals
       }
-      if (last) {
-        // ---- group sizes and exclusive group bases (one block, once per call)
-        __syncthreads();
-        const uint32_t chunk = (nbins + kBlock - 1) / kBlock;
-        const uint32_t lo = tid * chunk, hi = min(lo + chunk, nbins);
-        uint32_t s = 0;
-        for (uint32_t b = lo; b < hi; ++b) s += hist[b];
-        s_part[tid] = s;
-        __syncthreads();
-        if (tid == 0) {
-          uint32_t acc = 0;
-          for (int t = 0; t < kBlock; ++t) {
-            const uint32_t v = s_part[t];
-            s_part[t] = acc;
-            acc += v;
-          }
+      // ---- compute lane: one packet
+      if (v_own) {
+        const uint8_t* x = xp + lane * kXStride;
+        const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
+        uint8_t* pown = a.pkts + (desc ? static_cast<size_t>(off_own) : static_cast<size_t>(p_own) * a.stride);
+        const bool aligned = (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
+        uint32_t bin;
+        // same decision as the loader lanes: chunks 0..2 were loaded and (if swapping) written
+        if (aligned && len_own >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
+          const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
+          const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
+          // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
+          const uint32_t src = (c1.z >> 16) | (c1.w << 16);
+          const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
+          const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
+          uint32_t lo, hi;
+          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+          bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
+        } else {
+          bin = classify_slow<LUTM, F4>(a, lut_lds, pown, len_own, p_own);
         }
-        __syncthreads();
-        uint32_t acc = s_part[tid];
-        for (uint32_t b = lo; b < hi; ++b) {
-          a.group_base[b] = acc;
-          a.counts[b] = hist[b];
-          acc += hist[b];
-        }
+        a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+        if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+      }
+    }
+
+    if constexpr (HIST) {
+      __syncthreads();
+      // partition histogram: few tiles share a partition row, so the adds rarely contend
+      uint32_t* row = a.part_hist + static_cast<size_t>(tile * kT / a.part_pkts) * nbins;
+      for (uint32_t b = tid; b < nbins; b += kBlock) {
+        const uint32_t h = hist[b];
+        if (h) atomicAdd(&row[b], h);
       }
     }
     __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(kBlock) void scatter_kernel(ScatterArgs a) {
-  extern __shared__ __align__(16) uint32_t cnt[];  // [4 waves][nbins]
+// Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
+// exclusive prefix and the total.
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
+    if (lane >= static_cast<uint32_t>(d)) x += y;
+  }
+  if (lane == 63u) s_wave[wave] = x;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / 64; ++w) {
+    const uint32_t t = s_wave[w];
+    if (w < wave) wpre += t;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return wpre + x - v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the exclusive prefix and the total.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
+    if (lane >= static_cast<uint32_t>(d)) x += y;
+  }
+  if (lane == 63u) s_wave[wave] = x;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kBlock / 64; ++w) {
+    const uint32_t t = s_wave[w];
+    if (w < wave) wpre += t;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return wpre + x - v;
+}
+
+// Fallback for many backends: one block per bin, exclusive scan of part_hist[.][bin] over
+// partitions and the bin's grand total.
+__global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
+  __shared__ uint32_t s_wave[kBlock / 64];
+  const uint32_t tid = threadIdx.x, b = blockIdx.x;
+  const uint32_t v = tid < a.n_parts ? a.part_hist[static_cast<size_t>(tid) * a.nbins + b] : 0u;
+  uint32_t total;
+  const uint32_t pre = block_excl_scan(v, s_wave, total);
+  if (tid < a.n_parts) a.part_prefix[static_cast<size_t>(tid) * a.nbins + b] = pre;
+  if (tid == 0) a.totals[b] = total;
+}
+
+// One 1024-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
+// Prologue: prefix of this partition over earlier partitions and the group bases, either
+// reduced here from the partition histograms staged in LDS, or read from scan_kernel's
+// output.  Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local
+// counting sort in LDS and coalesced perm stores.
+template <bool LDS_SCAN>
+__global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
+  extern __shared__ __align__(16) uint32_t gs[];
+  __shared__ uint32_t s_wave[kGBlock / 64];
+  constexpr uint32_t kW = kGBlock / 64;  // waves
   const uint32_t nbins = a.nb + 1;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-  const uint32_t tile = blockIdx.x;
-  for (uint32_t k = tid; k < 4u * nbins; k += kBlock) cnt[k] = 0;
+  const uint32_t c = blockIdx.x;
+  uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
+  uint32_t* tot = base + nbins;        // [nbins]
+  uint32_t* cnt = tot + nbins;         // [kW][nbins]
+  uint32_t* sidx = cnt + kW * nbins;   // [kChunk]
+  uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
+  uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (LDS_SCAN)
+
+  // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
+  if constexpr (LDS_SCAN) {
+    const uint32_t words = a.n_parts * nbins;
+    for (uint32_t i = tid; i < words; i += kGBlock) ph[i] = a.part_hist[i];
+    __syncthreads();
+    for (uint32_t b = tid; b < nbins; b += kGBlock) {
+      uint32_t pre = 0, all = 0;
+      for (uint32_t q = 0; q < a.n_parts; ++q) {
+        const uint32_t h = ph[q * nbins + b];
+        pre += q < c ? h : 0u;
+        all += h;
+      }
+      base[b] = pre;
+      tot[b] = all;
+    }
+  } else {
+    for (uint32_t b = tid; b < nbins; b += kGBlock) {
+      base[b] = a.part_prefix[static_cast<size_t>(c) * nbins + b];
+      tot[b] = a.totals[b];
+    }
+  }
+  // the next call accumulates into the other buffer: zero it (every block a slice)
+  for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
   __syncthreads();
+  {
+    const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
+    const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
+    uint32_t s = 0;
+    for (uint32_t b = lo; b < hi; ++b) s += tot[b];
+    uint32_t all;
+    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave, all);
+    for (uint32_t b = lo; b < hi; ++b) {
+      const uint32_t t = tot[b];
+      if (c == 0 && a.counts) a.counts[b] = t;
+      base[b] += gb;  // group base + prefix over earlier partitions
+      gb += t;
+    }
+  }
+  __syncthreads();
+  if (!a.perm) return;
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t bins[kPktsPerThread], ranks[kPktsPerThread];
   uint32_t* mycnt = cnt + wave * nbins;
-  // wave w owns packets [tile*kTile + w*256, +256) in 4 rounds of 64
+  const uint32_t pbeg = c * a.part_pkts;
+  const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
+  for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
+    for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
+    __syncthreads();
+    uint32_t bins[kGRounds], ranks[kGRounds];
+    const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
-  for (int r = 0; r < kPktsPerThread; ++r) {
-    const uint32_t i = tile * kTile + wave * (64u * kPktsPerThread) + r * 64u + lane;
-    const bool valid = i < a.n_pkts;
-    uint32_t bin = 0;
-    if (valid) {
-      const uint32_t v = a.backend[i];
-      bin = v == kSentinel ? a.nb : v;
+    for (int r = 0; r < kGRounds; ++r) {
+      const uint32_t i = wbase + r * 64u + lane;
+      const bool valid = i < pend;
+      uint32_t bin = 0;
+      if (valid) {
+        const uint32_t v = a.backend[i];
+        bin = v == NBG_SENTINEL ? a.nb : v;
+      }
+      unsigned long long eq = __ballot(valid);
+      for (uint32_t bit = 0; bit < a.bits; ++bit) {
+        const bool set = (bin >> bit) & 1u;
+        const unsigned long long bb = __ballot(set);
+        eq &= set ? bb : ~bb;
+      }
+      uint32_t rank = 0;
+      if (valid) {
+        const uint32_t prior = mycnt[bin];
+        rank = prior + __popcll(eq & lt);
+        if ((eq & lt) == 0) mycnt[bin] = prior + __popcll(eq);
+      }
+      bins[r] = valid ? bin : 0xffffffffu;
+      ranks[r] = rank;
     }
-    unsigned long long eq = __ballot(valid);
-    for (uint32_t bit = 0; bit < a.bits; ++bit) {
-      const bool set = (bin >> bit) & 1u;
-      const unsigned long long bb = __ballot(set);
-      eq &= set ? bb : ~bb;
+    __syncthreads();
+    // per bin: chunk-local start (scan over bins) and wave offsets
+    const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
+    const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
+    uint32_t csum = 0;
+    for (uint32_t b = lo; b < hi; ++b)
+      for (uint32_t w = 0; w < kW; ++w) csum += cnt[w * nbins + b];
+    uint32_t ctotal;
+    uint32_t lstart = block_excl_scan_n<kGBlock>(csum, s_wave, ctotal);
+    for (uint32_t b = lo; b < hi; ++b) {
+      tot[b] = base[b] - lstart;  // perm position of sorted slot j of bin b = tot[b] + j
+      uint32_t acc = lstart;
+      for (uint32_t w = 0; w < kW; ++w) {
+        const uint32_t n = cnt[w * nbins + b];
+        cnt[w * nbins + b] = acc;
+        acc += n;
+      }
+      base[b] += acc - lstart;  // advance past this chunk's packets of bin b
+      lstart = acc;
     }
-    uint32_t rank = 0;
-    if (valid) {
-      const uint32_t prior = mycnt[bin];
-      rank = prior + __popcll(eq & lt);
-      if ((eq & lt) == 0) mycnt[bin] = prior + __popcll(eq);
-    }
-    bins[r] = bin;
-    ranks[r] = rank;
-  }
-  __syncthreads();
-  for (uint32_t b = tid; b < nbins; b += kBlock) {
-    uint32_t acc = a.group_base[b] + a.tile_prefix[static_cast<size_t>(tile) * nbins + b];
+    __syncthreads();
 #pragma unroll
-    for (uint32_t w = 0; w < 4; ++w) {
-      const uint32_t c = cnt[w * nbins + b];
-      cnt[w * nbins + b] = acc;
-      acc += c;
+    for (int r = 0; r < kGRounds; ++r) {
+      if (bins[r] != 0xffffffffu) {
+        const uint32_t j = mycnt[bins[r]] + ranks[r];
+        sidx[j] = wbase + r * 64u + lane;
+        sbin[j] = static_cast<uint16_t>(bins[r]);
+      }
     }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < kPktsPerThread; ++r) {
-    const uint32_t i = tile * kTile + wave * (64u * kPktsPerThread) + r * 64u + lane;
-    if (i < a.n_pkts) a.perm[mycnt[bins[r]] + ranks[r]] = i;
+    __syncthreads();
+    // coalesced output: consecutive sorted slots of one bin are consecutive perm entries
+    for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
+    __syncthreads();
   }
 }
 
-template <int LUTM, bool F4, bool GROUP>
+template <int LUTM, bool F4, bool HIST, int R>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  auto fn = classify_kernel<LUTM, F4, GROUP>;
+  auto fn = classify_kernel<LUTM, F4, HIST, R>;
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess)
@@ -346,50 +459,77 @@ int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   return NBG_OK;
 }
 
+template <int LUTM, bool F4, bool HIST>
+int launch_r(const ClassifyArgs& a, int rounds, int grid, size_t lds, hipStream_t s) {
+  switch (rounds) {
+    case 1: return launch_one<LUTM, F4, HIST, 1>(a, grid, lds, s);
+    case 2: return launch_one<LUTM, F4, HIST, 2>(a, grid, lds, s);
+    default: return launch_one<LUTM, F4, HIST, 4>(a, grid, lds, s);
+  }
+}
+
 template <int LUTM>
-int launch_mode(const ClassifyArgs& a, bool group, int grid, size_t lds, hipStream_t s) {
-  const bool f4 = a.m == 65537u;
-  if (f4) return group ? launch_one<LUTM, true, true>(a, grid, lds, s) : launch_one<LUTM, true, false>(a, grid, lds, s);
-  return group ? launch_one<LUTM, false, true>(a, grid, lds, s) : launch_one<LUTM, false, false>(a, grid, lds, s);
+int launch_mode(const ClassifyArgs& a, bool hist, int rounds, int grid, size_t lds, hipStream_t s) {
+  if (a.m == 65537u)
+    return hist ? launch_r<LUTM, true, true>(a, rounds, grid, lds, s)
+                : launch_r<LUTM, true, false>(a, rounds, grid, lds, s);
+  return hist ? launch_r<LUTM, false, true>(a, rounds, grid, lds, s)
+              : launch_r<LUTM, false, false>(a, rounds, grid, lds, s);
 }
 
 size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
-  return ((static_cast<size_t>(nb + 1) * 4 + 15) & ~size_t(15)) + lut_lds_bytes;
+  return static_cast<size_t>(lut_lds_bytes) + 4u * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
 }
 
 }  // namespace
 
-int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream) {
-  const bool group = a.desc != nullptr;
+int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int rounds, int grid, void* stream) {
+  const bool hist = a.part_hist != nullptr;
   const size_t lds = classify_lds(a.nb, lds_lut ? a.lut_lds_bytes : 0);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (lds_lut) return wide_lut ? launch_mode<kLdsU16>(a, group, grid, lds, s) : launch_mode<kLdsU8>(a, group, grid, lds, s);
-  return wide_lut ? launch_mode<kGlobalU16>(a, group, grid, lds, s) : launch_mode<kGlobalU8>(a, group, grid, lds, s);
+  if (lds_lut)
+    return wide_lut ? launch_mode<kLdsU16>(a, hist, rounds, grid, lds, s)
+                    : launch_mode<kLdsU8>(a, hist, rounds, grid, lds, s);
+  return wide_lut ? launch_mode<kGlobalU16>(a, hist, rounds, grid, lds, s)
+                  : launch_mode<kGlobalU8>(a, hist, rounds, grid, lds, s);
 }
 
-int launch_scatter(const ScatterArgs& a, uint32_t n_tiles, void* stream) {
-  const size_t lds = static_cast<size_t>(a.nb + 1) * 4 * 4;
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(scatter_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess)
-      (void)hipGetLastError();
-  }
-  hipLaunchKernelGGL(scatter_kernel, dim3(n_tiles), dim3(kBlock), lds, static_cast<hipStream_t>(stream), a);
+int launch_scan(const ScanArgs& a, void* stream) {
+  hipLaunchKernelGGL(scan_kernel, dim3(a.nbins), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_error(NBG_EIO, "scatter launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return set_error(NBG_EIO, "scan launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 
-// Resident workgroups for the classify kernel: CUs x blocks/CU as limited by LDS
-// (the LDS-staged LUT amortises its staging over the tiles a resident block takes).
-int max_classify_grid(bool /*wide_lut*/, bool lds_lut, uint32_t lds_bytes, int device, int* grid) {
+size_t group_lds(uint32_t nbins, uint32_t n_parts, bool lds_scan) {
+  size_t w = static_cast<size_t>(nbins) * (2 + kGBlock / 64) + kChunk + kChunk / 2;
+  if (lds_scan) w += static_cast<size_t>(n_parts) * nbins;
+  return w * 4;
+}
+
+int launch_group(const GroupArgs& a, bool lds_scan, void* stream) {
+  const size_t lds = group_lds(a.nb + 1, a.n_parts, lds_scan);
+  auto fn = lds_scan ? group_kernel<true> : group_kernel<false>;
+  if (lds > 64 * 1024) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+      (void)hipGetLastError();
+  }
+  hipLaunchKernelGGL(fn, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "group launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+// Grid for the classify kernel: resident blocks (CUs x blocks/CU by LDS), so that the
+// LDS-staged LUT is loaded once per resident block and amortised over its tiles.
+int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
     return set_error(NBG_ENODEV, "hipDeviceGetAttribute(CU count) failed");
-  const size_t lds = classify_lds(0, lds_lut ? lds_bytes : 0) + 2048;  // + static LDS
-  int per_cu = lds_lut ? static_cast<int>((160 * 1024) / lds) : 8;
-  if (per_cu < 1) per_cu = 1;
-  if (per_cu > 8) per_cu = 8;
+  const size_t lds = classify_lds(nb, lds_lut ? lut_bytes : 0);
+  int per_cu = static_cast<int>((160 * 1024) / lds);
+  per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
   *grid = cus * per_cu;
   return NBG_OK;
 }

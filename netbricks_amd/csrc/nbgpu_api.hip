@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -46,15 +47,18 @@ struct nbg_maglev {
   void* d_lut = nullptr;      // u8 (nb <= 256) or u16 entries, padded to 16 B
   bool wide = false;
   uint32_t lut_bytes = 0;     // padded device LUT bytes
-  // per-call scratch
-  uint64_t cap_tiles = 0;
-  unsigned long long* d_desc = nullptr;
-  uint32_t* d_tile_prefix = nullptr;
-  uint32_t* d_group_base = nullptr;
-  uint32_t* d_counts = nullptr;     // used when the caller passes no counts buffer
-  unsigned long long* d_ticket = nullptr;
-  uint32_t* d_err = nullptr;
-  uint32_t epoch = 0;
+  // grouping scratch (independent of the batch size: at most kMaxParts partitions)
+  uint32_t* d_part_hist = nullptr;    // [2][kMaxParts][nb+1] ping-pong partition histograms
+  uint32_t* d_part_prefix = nullptr;  // [kMaxParts][nb+1] (scan-kernel fallback)
+  uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
+  uint32_t parity = 0;
+  uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
+  int rounds = 1;                     // classify rounds of 64 packets per wave per tile
+  // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
+  bool pending = false;
+  bool pending_lds_scan = false;
+  GroupArgs pending_args{};
+  ScanArgs pending_scan{};
   hipStream_t last_stream = nullptr;
   int grid_lds = 0, grid_global = 0;
   // host-path staging (pinned host + device)
@@ -64,6 +68,7 @@ struct nbg_maglev {
   uint16_t* h_len = nullptr;
   uint8_t* h_mac = nullptr;
   uint8_t* d_win = nullptr;
+  uint8_t* d_mac = nullptr;
   uint16_t* d_len = nullptr;
   uint16_t* d_backend = nullptr;
   uint32_t* d_perm = nullptr;
@@ -84,11 +89,14 @@ struct DeviceGuard {
 };
 
 void free_scratch(nbg_maglev* h) {
-  (void)hipFree(h->d_desc);
-  (void)hipFree(h->d_tile_prefix);
-  h->d_desc = nullptr;
-  h->d_tile_prefix = nullptr;
-  h->cap_tiles = 0;
+  (void)hipFree(h->d_part_hist);
+  (void)hipFree(h->d_part_prefix);
+  (void)hipFree(h->d_totals);
+  (void)hipFree(h->d_counts);
+  h->d_part_hist = nullptr;
+  h->d_part_prefix = nullptr;
+  h->d_totals = nullptr;
+  h->d_counts = nullptr;
 }
 
 void free_host_path(nbg_maglev* h) {
@@ -96,6 +104,7 @@ void free_host_path(nbg_maglev* h) {
   (void)hipHostFree(h->h_len);
   (void)hipHostFree(h->h_mac);
   (void)hipFree(h->d_win);
+  (void)hipFree(h->d_mac);
   (void)hipFree(h->d_len);
   (void)hipFree(h->d_backend);
   (void)hipFree(h->d_perm);
@@ -103,24 +112,12 @@ void free_host_path(nbg_maglev* h) {
   h->h_len = nullptr;
   h->h_mac = nullptr;
   h->d_win = nullptr;
+  h->d_mac = nullptr;
   h->d_len = nullptr;
   h->d_backend = nullptr;
   h->d_perm = nullptr;
   h->host_cap = 0;
   h->host_win = 0;
-}
-
-int ensure_scratch(nbg_maglev* h, uint64_t n_pkts) {
-  const uint64_t tiles = (n_pkts + kTile - 1) / kTile;
-  if (tiles <= h->cap_tiles) return NBG_OK;
-  free_scratch(h);
-  const uint64_t cap = std::max<uint64_t>(tiles, 64);
-  const size_t words = static_cast<size_t>(cap) * (h->nb + 1);
-  NBG_HIP(hipMalloc(&h->d_desc, words * sizeof(unsigned long long)));
-  NBG_HIP(hipMalloc(&h->d_tile_prefix, words * sizeof(uint32_t)));
-  NBG_HIP(hipMemset(h->d_desc, 0, words * sizeof(unsigned long long)));
-  h->cap_tiles = cap;
-  return NBG_OK;
 }
 
 int upload(nbg_maglev* h) {
@@ -136,20 +133,22 @@ int upload(nbg_maglev* h) {
   }
   NBG_HIP(hipMalloc(&h->d_lut, h->lut_bytes));
   NBG_HIP(hipMemcpy(h->d_lut, buf.data(), h->lut_bytes, hipMemcpyHostToDevice));
-  NBG_HIP(hipMalloc(&h->d_group_base, (h->nb + 1) * sizeof(uint32_t)));
-  NBG_HIP(hipMalloc(&h->d_counts, (h->nb + 1) * sizeof(uint32_t)));
-  NBG_HIP(hipMalloc(&h->d_ticket, 2 * sizeof(unsigned long long)));
-  NBG_HIP(hipMalloc(&h->d_err, sizeof(uint32_t)));
-  NBG_HIP(hipMemset(h->d_ticket, 0, 2 * sizeof(unsigned long long)));
-  NBG_HIP(hipMemset(h->d_err, 0, sizeof(uint32_t)));
-  int rc = max_classify_grid(h->wide, true, h->lut_bytes, h->device, &h->grid_lds);
+  const size_t nbins = h->nb + 1;
+  NBG_HIP(hipMalloc(&h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMemset(h->d_part_hist, 0, 2 * kMaxParts * nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
+  if (const char* e = std::getenv("NBG_ROUNDS")) h->rounds = std::atoi(e) >= 4 ? 4 : (std::atoi(e) >= 2 ? 2 : 1);
+  int rc = classify_grid(true, h->lut_bytes, h->nb, h->device, &h->grid_lds);
   if (rc) return rc;
-  return max_classify_grid(h->wide, false, 0, h->device, &h->grid_global);
+  return classify_grid(false, 0, h->nb, h->device, &h->grid_global);
 }
 
-// LDS staging pays when the LUT fits two blocks per CU (<= 72 KiB).
+// The LUT is gathered from L2 by default (measured faster: the LDS-staged copy costs
+// occupancy); NBG_LUT_LDS stages it in LDS when it fits.
 bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
-  return !(flags & NBG_LUT_GLOBAL) && h->lut_bytes <= 72 * 1024;
+  return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024;
 }
 
 int finish_create(nbg_maglev* h, int device, nbg_maglev** out) {
@@ -219,10 +218,6 @@ void nbg_maglev_destroy(nbg_maglev* h) {
     free_scratch(h);
     free_host_path(h);
     (void)hipFree(h->d_lut);
-    (void)hipFree(h->d_group_base);
-    (void)hipFree(h->d_counts);
-    (void)hipFree(h->d_ticket);
-    (void)hipFree(h->d_err);
     if (h->host_stream) (void)hipStreamDestroy(h->host_stream);
   }
   delete h;
@@ -241,14 +236,23 @@ int nbg_maglev_lut(const nbg_maglev* h, uint16_t* out, uint64_t n) {
 
 int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts) {
   if (!h) return set_error(NBG_EINVAL, "nbg_maglev_reserve: null handle");
-  DeviceGuard g(h->device);
-  return ensure_scratch(h, max_pkts);
+  (void)max_pkts;  // scratch is sized per handle (at most kMaxParts partitions), never per call
+  return NBG_OK;
 }
 
 int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
                                uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
                                uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
+  return nbg_maglev_classify_device_ex(h, d_pkts, d_off, d_len, stride, fixed_len, n_pkts, flags, d_backend, d_perm,
+                                       d_counts, nullptr, stream);
+}
+
+int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
+                                  uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
+                                  uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
+                                  void* stream) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
+  if (h->pending) return set_error(NBG_EINVAL, "classify: a deferred group is pending (nbg_maglev_finish_group)");
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify: n_pkts must be < 2^30");
   if (n_pkts == 0) {
     if (d_counts) NBG_HIP(hipMemsetAsync(d_counts, 0, (h->nb + 1) * sizeof(uint32_t), (hipStream_t)stream));
@@ -260,13 +264,19 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
     return set_error(NBG_EINVAL, "classify: batch too large");
   DeviceGuard g(h->device);
   const bool group = d_perm || d_counts;
-  if (group) {
-    int rc = ensure_scratch(h, n_pkts);
-    if (rc) return rc;
-  }
+  const uint32_t nbins = h->nb + 1;
+  if (group && nbins > kMaxGroupBins)
+    return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
   const bool lds = use_lds_lut(h, flags);
-  const uint32_t n_tiles = static_cast<uint32_t>((n_pkts + kTile - 1) / kTile);
-  int grid = std::min<int>(lds ? h->grid_lds : h->grid_global, static_cast<int>(n_tiles));
+  const uint32_t hist_tile = kBlock * h->rounds;
+  const uint32_t n_tiles = static_cast<uint32_t>((n_pkts + hist_tile - 1) / hist_tile);
+  // LDS-staged LUT: persistent resident grid; L2 LUT: one tile per block
+  const int grid = lds ? std::min<int>(h->grid_lds, static_cast<int>(n_tiles)) : static_cast<int>(n_tiles);
+  const uint64_t per = (n_pkts + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
+  const uint32_t part_pkts = static_cast<uint32_t>(per * kChunk);
+  const uint32_t n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
+  uint32_t* part_cur = h->d_part_hist + static_cast<size_t>(h->parity) * kMaxParts * nbins;
+  uint32_t* part_next = h->d_part_hist + static_cast<size_t>(h->parity ^ 1u) * kMaxParts * nbins;
 
   ClassifyArgs a{};
   a.pkts = d_pkts;
@@ -282,34 +292,63 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
   a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
   a.nb = h->nb;
   a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  // a 64-B window per packet start is owned: fixed slots of >= 64 B, or the caller says so
+  a.win_owned = (!d_off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
+  a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
   a.backend = d_backend;
-  if (group) {
-    h->epoch = (h->epoch + 1) & 0x3fffffffu;
-    if (h->epoch == 0) h->epoch = 1;
-    a.desc = h->d_desc;
-    a.tile_prefix = h->d_tile_prefix;
-    a.group_base = h->d_group_base;
-    a.counts = d_counts ? d_counts : h->d_counts;
-    a.ticket = h->d_ticket;
-    a.epoch = h->epoch;
-    a.err = h->d_err;
-  }
-  int rc = launch_classify(a, h->wide, lds, grid, stream);
+  a.mac_out = d_mac_out;
+  a.part_hist = group ? part_cur : nullptr;
+  a.part_pkts = part_pkts;
+  int rc = launch_classify(a, h->wide, lds, h->rounds, grid, stream);
   if (rc) return rc;
-  if (d_perm) {
-    ScatterArgs s{};
-    s.backend = d_backend;
-    s.n_pkts = static_cast<uint32_t>(n_pkts);
-    s.nb = h->nb;
+  if (group) {
+    // partition prefixes reduced inside the group kernel when the histograms fit in LDS
+    const bool lds_scan = group_lds(nbins, n_parts, true) <= 100 * 1024;
+    ScanArgs sa{};
+    sa.part_hist = part_cur;
+    sa.part_prefix = h->d_part_prefix;
+    sa.totals = h->d_totals;
+    sa.n_parts = n_parts;
+    sa.nbins = nbins;
+    GroupArgs ga{};
+    ga.backend = d_backend;
+    ga.n_pkts = static_cast<uint32_t>(n_pkts);
+    ga.nb = h->nb;
     uint32_t bits = 0;
-    while ((1u << bits) < h->nb + 1) ++bits;
-    s.bits = bits;
-    s.tile_prefix = h->d_tile_prefix;
-    s.group_base = h->d_group_base;
-    s.perm = d_perm;
-    rc = launch_scatter(s, n_tiles, stream);
-    if (rc) return rc;
+    while ((1u << bits) < nbins) ++bits;
+    ga.bits = bits;
+    ga.n_parts = n_parts;
+    ga.part_pkts = part_pkts;
+    ga.part_hist = part_cur;
+    ga.part_prefix = h->d_part_prefix;
+    ga.totals = h->d_totals;
+    ga.part_hist_next = part_next;
+    ga.next_words = kMaxParts * nbins;
+    ga.counts = d_counts ? d_counts : h->d_counts;
+    ga.perm = d_perm;
+    h->parity ^= 1u;
+    if (flags & NBG_DEFER_GROUP) {
+      h->pending = true;
+      h->pending_lds_scan = lds_scan;
+      h->pending_args = ga;
+      h->pending_scan = sa;
+    } else {
+      if (!lds_scan && (rc = launch_scan(sa, stream))) return rc;
+      if ((rc = launch_group(ga, lds_scan, stream))) return rc;
+    }
   }
+  h->last_stream = static_cast<hipStream_t>(stream);
+  return NBG_OK;
+}
+
+int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
+  if (!h) return set_error(NBG_EINVAL, "finish_group: null handle");
+  if (!h->pending) return NBG_OK;
+  DeviceGuard g(h->device);
+  h->pending = false;
+  int rc;
+  if (!h->pending_lds_scan && (rc = launch_scan(h->pending_scan, stream))) return rc;
+  if ((rc = launch_group(h->pending_args, h->pending_lds_scan, stream))) return rc;
   h->last_stream = static_cast<hipStream_t>(stream);
   return NBG_OK;
 }
@@ -318,9 +357,7 @@ int nbg_maglev_check(nbg_maglev* h) {
   if (!h) return set_error(NBG_EINVAL, "check: null handle");
   DeviceGuard g(h->device);
   NBG_HIP(hipStreamSynchronize(h->last_stream));
-  uint32_t err = 0;
-  NBG_HIP(hipMemcpy(&err, h->d_err, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return set_error(NBG_ETIMEDOUT, "look-back spin limit reached (device flag %u)", err);
+  NBG_HIP(hipGetLastError());
   return NBG_OK;
 }
 
@@ -351,6 +388,7 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
     NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_len), cap * 2, hipHostMallocDefault));
     NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_mac), cap * 12, hipHostMallocDefault));
     NBG_HIP(hipMalloc(&h->d_win, cap * win));
+    NBG_HIP(hipMalloc(&h->d_mac, cap * 12));
     NBG_HIP(hipMalloc(&h->d_len, cap * 2));
     NBG_HIP(hipMalloc(&h->d_backend, cap * 2));
     NBG_HIP(hipMalloc(&h->d_perm, cap * 4));
@@ -366,22 +404,21 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
   NBG_HIP(hipMemcpyAsync(h->d_win, h->h_win, n * win, hipMemcpyHostToDevice, s));
   NBG_HIP(hipMemcpyAsync(h->d_len, h->h_len, n * 2, hipMemcpyHostToDevice, s));
   uint32_t* d_counts = counts_out || perm_out ? h->d_counts : nullptr;
-  int rc = nbg_maglev_classify_device(h, h->d_win, nullptr, h->d_len, win, 0, n, flags, h->d_backend,
-                                      perm_out ? h->d_perm : nullptr, d_counts, s);
+  const bool swap = flags & NBG_SWAP_MACS;
+  // the swap comes back as dense 12-B records (no in-place rewrite of the staging windows)
+  int rc = nbg_maglev_classify_device_ex(h, h->d_win, nullptr, h->d_len, win, 0, n, flags | NBG_OWNED_WINDOWS,
+                                         h->d_backend, perm_out ? h->d_perm : nullptr, d_counts,
+                                         swap ? h->d_mac : nullptr, s);
   if (rc) return rc;
   NBG_HIP(hipMemcpyAsync(backend_out, h->d_backend, n * 2, hipMemcpyDeviceToHost, s));
   if (perm_out) NBG_HIP(hipMemcpyAsync(perm_out, h->d_perm, n * 4, hipMemcpyDeviceToHost, s));
   if (counts_out) NBG_HIP(hipMemcpyAsync(counts_out, h->d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, s));
-  const bool swap = flags & NBG_SWAP_MACS;
-  if (swap) NBG_HIP(hipMemcpy2DAsync(h->h_mac, 12, h->d_win, win, 12, n, hipMemcpyDeviceToHost, s));
+  if (swap) NBG_HIP(hipMemcpyAsync(h->h_mac, h->d_mac, n * 12, hipMemcpyDeviceToHost, s));
   NBG_HIP(hipStreamSynchronize(s));
   if (swap) {
     for (uint64_t i = 0; i < n; ++i)
       if (lens[i] >= 14) std::memcpy(pkt_ptrs[i], h->h_mac + i * 12, 12);
   }
-  uint32_t err = 0;
-  NBG_HIP(hipMemcpy(&err, h->d_err, sizeof(err), hipMemcpyDeviceToHost));
-  if (err) return set_error(NBG_ETIMEDOUT, "look-back spin limit reached");
   return NBG_OK;
 }
 

@@ -16,10 +16,14 @@ uint64_t fnv1a64(const uint8_t* p, size_t n);
 uint64_t xxh64(const uint8_t* p, size_t n, uint64_t seed);
 int build_lut(const char* const* names, const uint32_t* lens, uint32_t n, uint64_t m, std::vector<uint32_t>& entry);
 
-// Kernel geometry shared by the classify and scatter kernels.
-constexpr int kBlock = 256;          // threads per workgroup (4 waves)
-constexpr int kPktsPerThread = 4;    // packets per thread per tile
-constexpr int kTile = kBlock * kPktsPerThread;  // packets per tile (look-back unit)
+// Kernel geometry.
+constexpr int kBlock = 256;          // classify threads per workgroup (4 waves)
+constexpr int kXStride = 80;         // LDS bytes per packet in the transpose (64 + 16: conflict-free b128)
+constexpr int kGBlock = 1024;        // group kernel threads per workgroup (16 waves)
+constexpr int kGRounds = 4;          // group kernel rounds of 64 packets per wave per chunk
+constexpr int kChunk = kGBlock * kGRounds;  // packets per group-kernel chunk (4096)
+constexpr uint32_t kMaxParts = 256;  // partitions per batch (part_pkts is a multiple of kChunk)
+constexpr uint32_t kMaxGroupBins = 1024;  // group output supports n_backends + 1 <= 1024
 
 struct ClassifyArgs {
   uint8_t* pkts;
@@ -35,30 +39,43 @@ struct ClassifyArgs {
   uint64_t mu;              // floor(2^64 / m) for Barrett
   uint32_t nb;              // backends; bins = nb + 1 (sentinel bin = nb)
   uint32_t swap;
+  uint32_t win_owned;       // every packet start owns 64 readable/writable bytes
+  uint32_t wb_full;         // write back the whole owned window (full lines) instead of 16 B
   uint16_t* backend;
-  // grouping (nullable when no perm requested)
-  unsigned long long* desc;   // [n_tiles][nb+1] look-back words
-  uint32_t* tile_prefix;      // [n_tiles][nb+1] exclusive prefix over earlier tiles
-  uint32_t* group_base;       // [nb+1] exclusive prefix over groups
-  uint32_t* counts;           // [nb+1]
-  unsigned long long* ticket; // [0] tile ticket, [1] exit count; reset by the last block
-  uint32_t epoch;
-  uint32_t* err;
+  uint8_t* mac_out;         // nullable: dense 12-B swapped-MAC records instead of in-place swap
+  uint32_t* part_hist;      // nullable: [n_parts][nb+1] partition histograms (pre-zeroed)
+  uint32_t part_pkts;       // packets per partition
 };
 
-struct ScatterArgs {
+struct ScanArgs {
+  const uint32_t* part_hist;  // [n_parts][nbins]
+  uint32_t* part_prefix;      // [n_parts][nbins] exclusive prefix over earlier partitions
+  uint32_t* totals;           // [nbins]
+  uint32_t n_parts;
+  uint32_t nbins;
+};
+
+struct GroupArgs {
   const uint16_t* backend;
   uint32_t n_pkts;
   uint32_t nb;
   uint32_t bits;              // ceil(log2(nb+1))
-  const uint32_t* tile_prefix;
-  const uint32_t* group_base;
-  uint32_t* perm;
+  uint32_t n_parts;
+  uint32_t part_pkts;
+  const uint32_t* part_hist;  // [n_parts][nb+1]      (LDS_SCAN)
+  const uint32_t* part_prefix;// [n_parts][nb+1]      (scan_kernel path)
+  const uint32_t* totals;     // [nb+1]               (scan_kernel path)
+  uint32_t* part_hist_next;   // zeroed for the next call
+  uint32_t next_words;
+  uint32_t* counts;           // nullable
+  uint32_t* perm;             // nullable (counts only)
 };
 
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
-int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
-int launch_scatter(const ScatterArgs& a, uint32_t n_tiles, void* stream);
-int max_classify_grid(bool wide_lut, bool lds_lut, uint32_t lds_bytes, int device, int* grid);
+int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int rounds, int grid, void* stream);
+int launch_scan(const ScanArgs& a, void* stream);
+int launch_group(const GroupArgs& a, bool lds_scan, void* stream);
+size_t group_lds(uint32_t nbins, uint32_t n_parts, bool lds_scan);
+int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid);
 
 }  // namespace nbg

@@ -16,7 +16,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import NBG_LUT_GLOBAL, NBG_SENTINEL, NBG_SWAP_MACS, check, lib
+from ._lib import (NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_SENTINEL, NBG_SWAP_MACS, NBG_WB_PARTIAL,
+                   check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
 
@@ -106,8 +107,10 @@ class Maglev:
         check(lib.nbg_maglev_check(self._h), "nbg_maglev_check")
 
     def group_by(self, pkts, n_pkts: int, *, stride: int = 64, frame_len: int = 60, offsets=None, lens=None,
-                 swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_global: bool = False,
-                 backend=None, perm=None, counts=None, stream=None) -> GroupedBatch:
+                 swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_lds: bool = False,
+                 owned_windows: bool = False, wb_partial: bool = False,
+                 defer_group: bool = False,
+                 backend=None, perm=None, counts=None, mac_out=None, stream=None) -> GroupedBatch:
         """Classify a device-resident batch (torch uint8 tensor on this device).
 
         Packet i starts at pkts[offsets[i]] (u32 tensor) or pkts[i*stride]; its length is
@@ -125,12 +128,22 @@ class Maglev:
             counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev)
         if stream is None:
             stream = torch.cuda.current_stream(dev).cuda_stream
-        flags = (NBG_SWAP_MACS if swap_macs else 0) | (NBG_LUT_GLOBAL if lut_global else 0)
-        rc = lib.nbg_maglev_classify_device(self._h, _ptr(pkts), _ptr(offsets), _ptr(lens), stride, frame_len,
-                                            n_pkts, flags, _ptr(backend), _ptr(perm) if scatter else None,
-                                            _ptr(counts) if group else None, stream)
-        check(rc, "nbg_maglev_classify_device")
+        flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_LUT_LDS if lut_lds else 0)
+                 | (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_WB_PARTIAL if wb_partial else 0)
+                 | (NBG_DEFER_GROUP if defer_group else 0))
+        rc = lib.nbg_maglev_classify_device_ex(self._h, _ptr(pkts), _ptr(offsets), _ptr(lens), stride, frame_len,
+                                               n_pkts, flags, _ptr(backend), _ptr(perm) if scatter else None,
+                                               _ptr(counts) if group else None, _ptr(mac_out), stream)
+        check(rc, "nbg_maglev_classify_device_ex")
         return GroupedBatch(backend, perm if scatter else None, counts if group else None)
+
+    def finish_group(self, stream=None) -> None:
+        """Launch the grouping kernel deferred by group_by(..., defer_group=True)."""
+        import torch
+
+        if stream is None:
+            stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
+        check(lib.nbg_maglev_finish_group(self._h, stream), "nbg_maglev_finish_group")
 
     def group_by_host(self, frames: Sequence[bytearray], swap_macs: bool = True, group: bool = True):
         """Host mbuf path: frames are mutable byte buffers (their MACs are swapped in place).

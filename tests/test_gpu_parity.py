@@ -22,7 +22,7 @@ def mg65(torch_cuda):
     m.close()
 
 
-def _run(torch, mg, buf, n, *, offs=None, lens=None, stride=64, frame_len=60, swap=True, lut_global=False):
+def _run(torch, mg, buf, n, *, offs=None, lens=None, stride=64, frame_len=60, swap=True, lut_lds=False):
     dev = torch.device("cuda:0")
     d_buf = torch.from_numpy(buf.copy()).to(dev)
     d_off = None if offs is None else torch.from_numpy(offs.astype(np.uint32).view(np.int32)).to(dev)
@@ -30,7 +30,7 @@ def _run(torch, mg, buf, n, *, offs=None, lens=None, stride=64, frame_len=60, sw
     d_off = None if d_off is None else d_off.view(torch.uint32)
     d_len = None if d_len is None else d_len.view(torch.uint16)
     r = mg.group_by(d_buf, n, stride=stride, frame_len=frame_len, offsets=d_off, lens=d_len, swap_macs=swap,
-                    lut_global=lut_global)
+                    lut_lds=lut_lds)
     torch.cuda.synchronize()
     mg.check()
     backend = r.backend.view(torch.int16).cpu().numpy().view(np.uint16)
@@ -60,13 +60,13 @@ def test_lut_matches_oracle(mg65):
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 1000, 1024, 1025, 4096, 65536 + 77])
-@pytest.mark.parametrize("lut_global", [False, True])
-def test_c2_small(torch_cuda, mg65, n, lut_global):
+@pytest.mark.parametrize("lut_lds", [False, True])
+def test_c2_small(torch_cuda, mg65, n, lut_lds):
     from netbricks_amd import make_trace
 
     buf, _, _ = make_trace(n, 0, seed=1234 + n)
     lut = orc.lut_build(NAMES65, 65537)
-    got = _run(torch_cuda, mg65, buf, n, lut_global=lut_global)
+    got = _run(torch_cuda, mg65, buf, n, lut_lds=lut_lds)
     _assert_same(got, _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
 
 
@@ -205,3 +205,69 @@ def test_host_path(torch_cuda, mg65):
     np.testing.assert_array_equal(counts, exp[3])
     for f, o, l in zip(frames, poff, pln):
         assert bytes(f) == exp[0][o:o + l].tobytes()
+
+
+def test_mac_out_record(torch_cuda, mg65):
+    """classify_device_ex with d_mac_out: 12-B swapped-MAC records, packet bytes untouched."""
+    from netbricks_amd import make_trace
+
+    rng = np.random.default_rng(2)
+    frames = [bytearray(f) for f in _edge_frames(rng)]
+    buf0, off0, ln0 = make_trace(2000, 1, seed=21)
+    frames += [bytearray(buf0[o:o + l].tobytes()) for o, l in zip(off0, ln0)]
+    buf, off, ln = _pack(frames, 64)
+    n = len(frames)
+    lut = orc.lut_build(NAMES65, 65537)
+    exp = _oracle(buf, n, lut, 65, offs=off, lens=ln)
+    dev = torch_cuda.device("cuda:0")
+    d_buf = torch_cuda.from_numpy(buf.copy()).to(dev)
+    d_off = torch_cuda.from_numpy(off.view(np.int32)).to(dev).view(torch_cuda.uint32)
+    d_len = torch_cuda.from_numpy(ln.view(np.int16)).to(dev).view(torch_cuda.uint16)
+    mac = torch_cuda.zeros(n * 12, dtype=torch_cuda.uint8, device=dev)
+    r = mg65.group_by(d_buf, n, offsets=d_off, lens=d_len, mac_out=mac)
+    torch_cuda.cuda.synchronize()
+    np.testing.assert_array_equal(r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16), exp[1])
+    np.testing.assert_array_equal(r.perm.view(torch_cuda.int32).cpu().numpy().view(np.uint32), exp[2])
+    np.testing.assert_array_equal(d_buf.cpu().numpy(), buf)  # packets untouched
+    m = mac.cpu().numpy().reshape(n, 12)
+    for i, (o, l) in enumerate(zip(off, ln)):
+        if l >= 14:
+            assert m[i].tobytes() == exp[0][o:o + 12].tobytes(), i
+        else:
+            assert not m[i].any()
+
+
+def test_many_backends_group_limit(torch_cuda):
+    """Group output is limited to 1023 backends; backend-only classify has no limit."""
+    from netbricks_amd import Maglev, NbgError, make_trace
+
+    names = [f"b{i}" for i in range(1500)]
+    mg = Maglev(names, 65537)
+    n = 3000
+    buf, _, _ = make_trace(n, 0, seed=8)
+    d = torch_cuda.from_numpy(buf.copy()).to("cuda:0")
+    with pytest.raises(NbgError):
+        mg.group_by(d, n)
+    r = mg.group_by(d, n, group=False, swap_macs=False)
+    torch_cuda.cuda.synchronize()
+    exp = orc.classify(buf.copy(), n, orc.lut_build(names, 65537), stride=64, fixed_len=60, swap=False)
+    np.testing.assert_array_equal(r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16), exp)
+    mg.close()
+
+
+def test_defer_group_split(torch_cuda, mg65):
+    """NBG_DEFER_GROUP + nbg_maglev_finish_group == one combined call."""
+    from netbricks_amd import make_trace
+
+    n = 50000
+    buf, _, _ = make_trace(n, 0, seed=31)
+    lut = orc.lut_build(NAMES65, 65537)
+    exp = _oracle(buf, n, lut, 65, stride=64, fixed_len=60)
+    d = torch_cuda.from_numpy(buf.copy()).to("cuda:0")
+    r = mg65.group_by(d, n, defer_group=True)
+    mg65.finish_group()
+    torch_cuda.cuda.synchronize()
+    got = (d.cpu().numpy(), r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16),
+           r.perm.view(torch_cuda.int32).cpu().numpy().view(np.uint32),
+           r.counts.view(torch_cuda.int32).cpu().numpy().view(np.uint32))
+    _assert_same(got, exp)

@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Variant micro-benchmark (interleaved rounds in one process, hipEvent timing).
+
+Times the classify kernel with/without grouping, LDS vs L2 LUT, the full path, and a
+plain device copy of the same bytes as the achievable-bandwidth reference.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--nb", type=int, default=65)
+    ap.add_argument("--m", type=int, default=65537)
+    args = ap.parse_args()
+    import torch
+
+    import netbricks_amd as nb
+
+    dev = torch.device("cuda:0")
+    names = [f"backend-{i}" for i in range(args.nb)]
+    mg = nb.Maglev(names, args.m)
+    n = args.n
+    mg.reserve(n)
+    bufs, offs, lens = [], [], []
+    for b in range(8):
+        buf, off, ln = nb.make_trace(n, args.mode, seed=b + 17)
+        bufs.append(torch.from_numpy(buf).to(dev))
+        offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
+        lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
+    stride = 64
+    backend = torch.empty(n, dtype=torch.uint16, device=dev)
+    perm = torch.empty(n, dtype=torch.uint32, device=dev)
+    counts = torch.empty(args.nb + 1, dtype=torch.uint32, device=dev)
+    dst = torch.empty_like(bufs[0])
+    mac = torch.empty(n * 12, dtype=torch.uint8, device=dev)
+    desc = args.mode != 0
+
+    def kw(i):
+        if desc:
+            return dict(offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True)
+        return dict(stride=stride, frame_len=60)
+
+    variants = {
+        "copy(read+write all bytes)": lambda i: dst.copy_(bufs[i % 8]),
+        "classify noswap nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, swap_macs=False,
+                                                         backend=backend, **kw(i)),
+        "classify noswap nogroup ldslut": lambda i: mg.group_by(bufs[i % 8], n, group=False, swap_macs=False,
+                                                                lut_lds=True, backend=backend, **kw(i)),
+        "classify inplace nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, backend=backend, **kw(i)),
+        "classify inplace-wb16 nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, wb_partial=True,
+                                                               backend=backend, **kw(i)),
+        "classify mac_out nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, backend=backend,
+                                                          mac_out=mac, **kw(i)),
+        "classify inplace hist (deferred)": lambda i: (mg.group_by(bufs[i % 8], n, defer_group=True,
+                                                                   backend=backend, perm=perm, counts=counts,
+                                                                   **kw(i)), mg.finish_group()),
+        "classify inplace counts": lambda i: mg.group_by(bufs[i % 8], n, scatter=False, backend=backend,
+                                                         counts=counts, **kw(i)),
+        "full path inplace": lambda i: mg.group_by(bufs[i % 8], n, backend=backend, perm=perm, counts=counts,
+                                                   **kw(i)),
+        "full path mac_out": lambda i: mg.group_by(bufs[i % 8], n, backend=backend, perm=perm, counts=counts,
+                                                   mac_out=mac, **kw(i)),
+    }
+    # multi-stream: independent batches in flight on S streams, one handle (scratch) per stream
+    extra = {}
+    for S in (2, 3, 4):
+        mgs = [nb.Maglev(names, args.m) for _ in range(S)]
+        sts = [torch.cuda.Stream(dev) for _ in range(S)]
+        outs = [(torch.empty(n, dtype=torch.uint16, device=dev), torch.empty(n, dtype=torch.uint32, device=dev),
+                 torch.empty(args.nb + 1, dtype=torch.uint32, device=dev),
+                 torch.empty(n * 12, dtype=torch.uint8, device=dev)) for _ in range(S)]
+
+        def ms(i, S=S, mgs=mgs, sts=sts, outs=outs, mac=True):
+            j = i % S
+            be, pm, ct, mo = outs[j]
+            mgs[j].group_by(bufs[i % 8], n, backend=be, perm=pm, counts=ct,
+                            mac_out=mo if mac else None, stream=sts[j].cuda_stream, **kw(i))
+
+        extra[f"full path l2 mac_out x{S} streams"] = ms
+        extra[f"full path l2 inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False))
+        extra[f"_keep{S}"] = (mgs, sts, outs)
+    variants.update({k: v for k, v in extra.items() if not k.startswith("_keep")})
+    res = {k: [] for k in variants}
+    all_streams = [st for k, v in extra.items() if k.startswith("_keep") for st in v[1]]
+    for r in range(args.rounds):
+        for name, fn in variants.items():
+            for i in range(3):
+                fn(i)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            cur = torch.cuda.current_stream(dev)
+            for st in all_streams:
+                st.wait_event(e0)
+            for i in range(args.iters):
+                fn(i)
+            for st in all_streams:
+                ev = torch.cuda.Event()
+                ev.record(st)
+                cur.wait_event(ev)
+            e1.record()
+            torch.cuda.synchronize()
+            res[name].append(e0.elapsed_time(e1) / args.iters * 1e3)
+    mg.check()
+    data_bytes = sum(int(b.numel()) for b in bufs) / 8
+    for name, v in res.items():
+        v = np.array(v)
+        med = np.median(v)
+        print(f"{name:32s} median {med:8.2f} us  min {v.min():8.2f}  -> {n / med / 1e3:8.1f} Gpps "
+              f" read-GB/s {data_bytes / med / 1e3:8.1f}")
+
+
+if __name__ == "__main__":
+    main()

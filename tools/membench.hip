@@ -1,0 +1,139 @@
+// Memory-pattern ceilings on MI355X for the Maglev classify kernel's access shapes.
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/membench tools/membench.hip
+// Each pattern streams 8 rotating 64 MiB buffers (512 MiB > the 256 MiB Infinity Cache).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline void nt_store(uint4* p, uint4 v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+constexpr size_t kBytes = 64ull << 20;
+constexpr int kBufs = 8;
+
+// U uint4 per thread, contiguous 1 KiB per wave-instruction; MODE: 0 read, 1 rw full, 2 rw chunk0, 3 copy
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void pattern(uint4* __restrict__ buf, uint4* __restrict__ dst, uint32_t* sink) {
+  const size_t base = (static_cast<size_t>(blockIdx.x) * 256 * U) + threadIdx.x;
+  uint4 v[U];
+#pragma unroll
+  for (int k = 0; k < U; ++k) v[k] = buf[base + k * 256];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < U; ++k) {
+    acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    if (MODE == 1) buf[base + k * 256] = make_uint4(v[k].y, v[k].x, v[k].z, v[k].w);
+    if (MODE == 2 && (threadIdx.x & 3) == 0) buf[base + k * 256] = make_uint4(v[k].y, v[k].x, v[k].z, v[k].w);
+    if (MODE == 3) dst[base + k * 256] = v[k];
+    if (MODE == 4 && (threadIdx.x & 3) == 0) dst[(base + k * 256) >> 2] = v[k];  // dense 16 B per 64-B packet
+    if (MODE == 5) nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+    if (MODE == 6 && (threadIdx.x & 3) == 0)
+      nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// persistent grid-stride variant with U loads in flight
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void pattern_p(uint4* __restrict__ buf, uint4* __restrict__ dst, uint32_t* sink,
+                                                 size_t n16) {
+  uint32_t acc = 0;
+  for (size_t base = static_cast<size_t>(blockIdx.x) * 256 * U + threadIdx.x; base < n16;
+       base += static_cast<size_t>(gridDim.x) * 256 * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = buf[base + k * 256];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      if (MODE == 1) buf[base + k * 256] = make_uint4(v[k].y, v[k].x, v[k].z, v[k].w);
+      if (MODE == 2 && (threadIdx.x & 3) == 0) buf[base + k * 256] = make_uint4(v[k].y, v[k].x, v[k].z, v[k].w);
+      if (MODE == 3) dst[base + k * 256] = v[k];
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <typename F>
+float time_it(F f, int iters) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 8; ++i) f(i);
+  CK(hipEventRecord(a));
+  for (int i = 0; i < iters; ++i) f(i);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms * 1000.f / iters;
+}
+
+int main() {
+  std::vector<uint4*> bufs(kBufs);
+  for (auto& p : bufs) {
+    CK(hipMalloc(&p, kBytes));
+    CK(hipMemset(p, 1, kBytes));
+  }
+  uint4* dst;
+  CK(hipMalloc(&dst, kBytes));
+  uint32_t* sink;
+  CK(hipMalloc(&sink, 64));
+  const size_t n16 = kBytes / 16;
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int iters = 100;
+  auto report = [&](const char* name, float us, double rd, double wr) {
+    std::printf("%-34s %8.2f us  read %6.0f GB/s  write %6.0f GB/s  total %6.0f GB/s\n", name, us, rd / us / 1e3,
+                wr / us / 1e3, (rd + wr) / us / 1e3);
+  };
+#define RUN(U, MODE, NAME, RD, WR)                                                                      \
+  {                                                                                                     \
+    const int grid = static_cast<int>(n16 / (256 * U));                                                 \
+    float us = time_it([&](int i) { pattern<U, MODE><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters); \
+    report(NAME, us, RD, WR);                                                                           \
+  }
+#define RUNP(U, MODE, BPC, NAME, RD, WR)                                                                          \
+  {                                                                                                               \
+    const int grid = cus * BPC;                                                                                   \
+    float us = time_it([&](int i) { pattern_p<U, MODE><<<grid, 256>>>(bufs[i % kBufs], dst, sink, n16); }, iters); \
+    report(NAME, us, RD, WR);                                                                                     \
+  }
+  const double B = static_cast<double>(kBytes);
+  for (int rep = 0; rep < 1; ++rep) {
+    RUN(1, 0, "read U1", B, 0);
+    RUN(4, 0, "read U4", B, 0);
+    RUN(8, 0, "read U8", B, 0);
+    RUN(16, 0, "read U16", B, 0);
+    RUNP(4, 0, 4, "read persistent U4 x4/CU", B, 0);
+    RUNP(8, 0, 4, "read persistent U8 x4/CU", B, 0);
+    RUNP(8, 0, 8, "read persistent U8 x8/CU", B, 0);
+    RUN(4, 1, "rw full U4", B, B);
+    RUN(8, 1, "rw full U8", B, B);
+    RUNP(8, 1, 4, "rw full persistent U8 x4/CU", B, B);
+    RUN(4, 2, "rw chunk0 (16B/64B) U4", B, B / 4);
+    RUN(8, 2, "rw chunk0 (16B/64B) U8", B, B / 4);
+    RUN(4, 4, "read + dense 16B/pkt out U4", B, B / 4);
+    RUN(4, 5, "rw full nt-store U4", B, B);
+    RUN(4, 6, "rw chunk0 nt-store U4", B, B / 4);
+    RUN(4, 3, "copy U4", B, B);
+    RUN(8, 3, "copy U8", B, B);
+    std::printf("--\n");
+  }
+  return 0;
+}
