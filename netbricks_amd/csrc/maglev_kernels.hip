@@ -19,6 +19,8 @@
 // Integer/byte work only; no MFMA.  HBM-bound.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "nbgpu_internal.h"
 
 namespace nbg {
@@ -128,10 +130,12 @@ __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
 }
 
-template <int LUTM, bool F4, bool HIST, int R>
-__global__ __launch_bounds__(kBlock) void classify_kernel(ClassifyArgs a) {
+// ABL (diagnostic builds only, selected by NBG_ABL): 0 = full kernel; 1 = no hash/LUT (bin from a
+// header byte); 2 = also no LDS transpose (loads + backend store only).
+template <int LUTM, bool F4, bool HIST, int R, int ABL = 0, int NT = kBlock>
+__global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
-  constexpr uint32_t kT = kBlock * R;  // packets per tile
+  constexpr uint32_t kT = NT * R;  // packets per tile
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t part = lane & 3u, quad = lane >> 2;
   const uint32_t nbins = a.nb + 1;
@@ -139,65 +143,98 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(ClassifyArgs a) {
   const uint32_t lut_bytes = kLdsLut ? a.lut_lds_bytes : 0u;
   uint8_t* lut_lds = smem;
   uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + 4u * 64u * kXStride);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + (NT / 64u) * 64u * kXStride);
   const bool desc = a.off != nullptr;
 
   if constexpr (kLdsLut) {
+    // stage the LUT: all loads issued before the LDS stores (one round trip)
     const uint4* src = static_cast<const uint4*>(a.lut);
     uint4* dst = reinterpret_cast<uint4*>(lut_lds);
-    for (uint32_t k = tid; k < lut_bytes / 16u; k += kBlock) dst[k] = src[k];
+    const uint32_t nvec = lut_bytes / 16u;
+    constexpr int kS = 8;
+    for (uint32_t k0 = 0; k0 < nvec; k0 += kS * NT) {
+      uint4 t[kS];
+#pragma unroll
+      for (int j = 0; j < kS; ++j) {
+        const uint32_t k = k0 + j * NT + tid;
+        t[j] = k < nvec ? src[k] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < kS; ++j) {
+        const uint32_t k = k0 + j * NT + tid;
+        if (k < nvec) dst[k] = t[j];
+      }
+    }
   }
 
   for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
     if constexpr (HIST) {
-      for (uint32_t b = tid; b < nbins; b += kBlock) hist[b] = 0;
+      for (uint32_t b = tid; b < nbins; b += NT) hist[b] = 0;
     }
     __syncthreads();
     const uint32_t wbase = tile * kT + wave * (64u * R);
 
+    // ---- phase A: metadata and every round's window loads (R x 4 x 16 B in flight per lane);
+    //      lane = (quad, part) holds chunk `part` of packet k*16+quad of each round
+    uint32_t off_own[R], len_own[R], cflag[R];
+    uint4 ch[R][4];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const uint32_t rbase = wbase + r * 64u;
-      // ---- own packet (compute lane) metadata
-      const uint32_t p_own = rbase + lane;
+      const uint32_t p_own = wbase + r * 64u + lane;
       const bool v_own = p_own < a.n_pkts;
-      const uint32_t off_own = desc ? (v_own ? a.off[p_own] : 0u) : 0u;
-      const uint32_t len_own = a.len ? (v_own ? a.len[p_own] : 0u) : a.fixed_len;
-
-      // ---- cooperative window loads: lane = (quad, part) holds chunk `part` of packet k*16+quad
-      uint4 ch[4];
-      uint8_t* cp[4];
-      uint32_t cflag = 0;  // bit k: chunk k may be written back if the packet is fast-path
+      off_own[r] = desc ? (v_own ? a.off[p_own] : 0u) : 0u;
+      len_own[r] = a.len ? (v_own ? a.len[p_own] : 0u) : a.fixed_len;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      cflag[r] = 0;  // bit k: chunk k may be written back if the packet is fast-path
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const uint32_t src = k * 16u + quad;
-        const uint32_t p = rbase + src;
+        const uint32_t p = wbase + r * 64u + src;
         const bool pv = p < a.n_pkts;
-        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own), src)) : 0u;
-        const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(len_own), src)) : a.fixed_len;
-        uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(p) * a.stride);
+        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own[r]), src)) : 0u;
+        const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(len_own[r]), src)) : a.fixed_len;
+        const uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(p) * a.stride);
         const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
         // chunk readable/writable: inside the frame, or the window is owned by this packet
         const bool inwin = a.win_owned || (part * 16u + 16u <= l);
         const bool rd = pv && aligned && inwin;
-        cp[k] = base + part * 16u;
-        ch[k] = rd ? ldg16(cp[k]) : make_uint4(0, 0, 0, 0);
-        if (rd && l >= 48u) cflag |= 1u << k;
+        ch[r][k] = rd ? ldg16(base + part * 16u) : make_uint4(0, 0, 0, 0);
+        if (rd && l >= 48u) cflag[r] |= 1u << k;
       }
-      // ---- transpose: chunks 0..2 -> LDS [packet][80 B]
+    }
+
+    // ---- phase B: per round, transpose + swap + hash, and ISSUE the LUT gather (consumed in C)
+    uint32_t bin[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t rbase = wbase + r * 64u;
+      const uint32_t p_own = rbase + lane;
+      if constexpr (ABL == 2) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc ^= ch[r][k].x ^ ch[r][k].y ^ ch[r][k].z ^ ch[r][k].w;
+        bin[r] = acc & 63u;
+        continue;
+      }
+      // transpose: chunks 0..2 -> LDS [packet][80 B] (region reused per round, in wave order)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = ch[k];
+        if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = ch[r][k];
       }
-      // ---- MAC swap in the loader lanes + window write-back (fast-path packets only)
+      // MAC swap in the loader lanes + window write-back (fast-path packets only)
       if (a.swap) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
-          const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(ch[k].w), lane & ~3u));
-          const bool fast = ((cflag >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
+          const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(ch[r][k].w), lane & ~3u));
+          const bool fast = ((cflag[r] >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
+          const uint32_t src = k * 16u + quad;
+          const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own[r]), src)) : 0u;
           if (!fast) continue;
-          uint4 v = ch[k];
+          uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(rbase + src) * a.stride);
+          uint4 v = ch[r][k];
           if (part == 0u) {
             const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
             // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
@@ -206,39 +243,57 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(ClassifyArgs a) {
           if (a.mac_out) {
             // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
             if (part == 0u) {
-              uint32_t* o = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(rbase + k * 16u + quad) * 12u);
-              o[0] = v.x;
-              o[1] = v.y;
-              o[2] = v.z;
+              uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(rbase + src) * 12u);
+              mo[0] = v.x;
+              mo[1] = v.y;
+              mo[2] = v.z;
             }
           } else if (part == 0u || a.wb_full) {
-            stg16_nt(cp[k], v);  // chunks 1..3 unchanged: makes the write whole lines
+            stg16_nt(base + part * 16u, v);  // chunks 1..3 unchanged: makes the write whole lines
           }
         }
       }
-      // ---- compute lane: one packet
-      if (v_own) {
+      // compute lane: one packet
+      bin[r] = a.nb;
+      if (p_own < a.n_pkts) {
         const uint8_t* x = xp + lane * kXStride;
         const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
-        uint8_t* pown = a.pkts + (desc ? static_cast<size_t>(off_own) : static_cast<size_t>(p_own) * a.stride);
+        uint8_t* pown = a.pkts + (desc ? static_cast<size_t>(off_own[r]) : static_cast<size_t>(p_own) * a.stride);
         const bool aligned = (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
-        uint32_t bin;
         // same decision as the loader lanes: chunks 0..2 were loaded and (if swapping) written
-        if (aligned && len_own >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
+        if (aligned && len_own[r] >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
           const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
           const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
           // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
           const uint32_t src = (c1.z >> 16) | (c1.w << 16);
           const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
           const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
-          uint32_t lo, hi;
-          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-          bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
+          if constexpr (ABL == 1) {
+            bin[r] = (src ^ dst ^ ports) % a.nb;
+          } else if constexpr (ABL == 3) {  // FNV, no LUT gather
+            uint32_t lo, hi;
+            fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+            bin[r] = mod_f4(lo, hi) % a.nb;
+          } else if constexpr (ABL == 4) {  // LUT gather of a trivial hash
+            bin[r] = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
+          } else {
+            uint32_t lo, hi;
+            fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+            bin[r] = lookup<LUTM, F4>(a, lut_lds, lo, hi);  // gather issued; first use in phase C
+          }
         } else {
-          bin = classify_slow<LUTM, F4>(a, lut_lds, pown, len_own, p_own);
+          bin[r] = classify_slow<LUTM, F4>(a, lut_lds, pown, len_own[r], p_own);
         }
-        a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-        if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+      }
+    }
+
+    // ---- phase C: consume the gathers
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t p_own = wbase + r * 64u + lane;
+      if (p_own < a.n_pkts) {
+        a.backend[p_own] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
+        if constexpr (HIST) atomicAdd(&hist[bin[r]], 1u);
       }
     }
 
@@ -246,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void classify_kernel(ClassifyArgs a) {
       __syncthreads();
       // partition histogram: few tiles share a partition row, so the adds rarely contend
       uint32_t* row = a.part_hist + static_cast<size_t>(tile * kT / a.part_pkts) * nbins;
-      for (uint32_t b = tid; b < nbins; b += kBlock) {
+      for (uint32_t b = tid; b < nbins; b += NT) {
         const uint32_t h = hist[b];
         if (h) atomicAdd(&row[b], h);
       }
@@ -331,26 +386,62 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbins;        // [nbins]
   uint32_t* cnt = tot + nbins;         // [kW][nbins]
-  uint32_t* sidx = cnt + kW * nbins;   // [kChunk]
+  uint32_t* sub = cnt + kW * nbins;    // [nbins] per-chunk bin sizes, then chunk-local starts
+  uint32_t* sidx = sub + nbins;        // [kChunk]
   uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
   uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (LDS_SCAN)
 
+  // ---- the first chunk's backends are loaded up front: their latency overlaps the prologue
+  const uint32_t pbeg = c * a.part_pkts;
+  const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
+  uint32_t pre_bin[kGRounds];
+  {
+    const uint32_t wb = pbeg + wave * (64u * kGRounds);
+#pragma unroll
+    for (int r = 0; r < kGRounds; ++r) {
+      const uint32_t i = wb + r * 64u + lane;
+      pre_bin[r] = (a.perm && i < pend) ? a.backend[i] : 0u;
+    }
+  }
   // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
+  for (uint32_t b = tid; b < nbins; b += kGBlock) {
+    base[b] = 0;
+    tot[b] = 0;
+  }
   if constexpr (LDS_SCAN) {
+    // stage the partition histograms: every load issued before any LDS store (one round trip)
     const uint32_t words = a.n_parts * nbins;
-    for (uint32_t i = tid; i < words; i += kGBlock) ph[i] = a.part_hist[i];
+    constexpr int kStage = 8;  // 8 x 1024 x 16 B = 128 KiB >= the LDS_SCAN limit
+    const uint32_t nvec = words / 4;
+    const uint4* src = reinterpret_cast<const uint4*>(a.part_hist);
+    uint4 tmp[kStage];
+#pragma unroll
+    for (int k = 0; k < kStage; ++k) {
+      const uint32_t v = tid + k * kGBlock;
+      tmp[k] = v < nvec ? src[v] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kStage; ++k) {
+      const uint32_t v = tid + k * kGBlock;
+      if (v < nvec) reinterpret_cast<uint4*>(ph)[v] = tmp[k];
+    }
+    for (uint32_t i = nvec * 4 + tid; i < words; i += kGBlock) ph[i] = a.part_hist[i];
     __syncthreads();
-    for (uint32_t b = tid; b < nbins; b += kGBlock) {
+    // L threads per bin, each summing a strided subset of the partitions
+    const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
+    for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
+      const uint32_t b = t / L, j = t - b * L;
       uint32_t pre = 0, all = 0;
-      for (uint32_t q = 0; q < a.n_parts; ++q) {
+      for (uint32_t q = j; q < a.n_parts; q += L) {
         const uint32_t h = ph[q * nbins + b];
         pre += q < c ? h : 0u;
         all += h;
       }
-      base[b] = pre;
-      tot[b] = all;
+      if (pre) atomicAdd(&base[b], pre);
+      if (all) atomicAdd(&tot[b], all);
     }
   } else {
+    __syncthreads();
     for (uint32_t b = tid; b < nbins; b += kGBlock) {
       base[b] = a.part_prefix[static_cast<size_t>(c) * nbins + b];
       tot[b] = a.totals[b];
@@ -378,8 +469,6 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t* mycnt = cnt + wave * nbins;
-  const uint32_t pbeg = c * a.part_pkts;
-  const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
     for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
     __syncthreads();
@@ -391,7 +480,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       const bool valid = i < pend;
       uint32_t bin = 0;
       if (valid) {
-        const uint32_t v = a.backend[i];
+        const uint32_t v = cbase == pbeg ? pre_bin[r] : a.backend[i];
         bin = v == NBG_SENTINEL ? a.nb : v;
       }
       unsigned long long eq = __ballot(valid);
@@ -410,30 +499,39 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       ranks[r] = rank;
     }
     __syncthreads();
-    // per bin: chunk-local start (scan over bins) and wave offsets
+    // per bin: offsets of each wave inside the bin (16-lane segmented scan over waves) ...
+    for (uint32_t t = tid; t < nbins * kW; t += kGBlock) {
+      const uint32_t b = t / kW, w = t % kW;
+      const uint32_t v = cnt[w * nbins + b];
+      uint32_t x = v;
+#pragma unroll
+      for (uint32_t d = 1; d < kW; d <<= 1) {
+        const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d, kW));
+        if (w >= d) x += y;
+      }
+      cnt[w * nbins + b] = x - v;
+      if (w == kW - 1) sub[b] = x;  // the bin's packets in this chunk
+    }
+    __syncthreads();
+    // ... and the chunk-local start of each bin (scan over bins)
     const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
     const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
     uint32_t csum = 0;
-    for (uint32_t b = lo; b < hi; ++b)
-      for (uint32_t w = 0; w < kW; ++w) csum += cnt[w * nbins + b];
+    for (uint32_t b = lo; b < hi; ++b) csum += sub[b];
     uint32_t ctotal;
     uint32_t lstart = block_excl_scan_n<kGBlock>(csum, s_wave, ctotal);
     for (uint32_t b = lo; b < hi; ++b) {
+      const uint32_t n = sub[b];
       tot[b] = base[b] - lstart;  // perm position of sorted slot j of bin b = tot[b] + j
-      uint32_t acc = lstart;
-      for (uint32_t w = 0; w < kW; ++w) {
-        const uint32_t n = cnt[w * nbins + b];
-        cnt[w * nbins + b] = acc;
-        acc += n;
-      }
-      base[b] += acc - lstart;  // advance past this chunk's packets of bin b
-      lstart = acc;
+      sub[b] = lstart;            // chunk-local start of bin b
+      base[b] += n;               // advance past this chunk's packets of bin b
+      lstart += n;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       if (bins[r] != 0xffffffffu) {
-        const uint32_t j = mycnt[bins[r]] + ranks[r];
+        const uint32_t j = sub[bins[r]] + mycnt[bins[r]] + ranks[r];
         sidx[j] = wbase + r * 64u + lane;
         sbin[j] = static_cast<uint16_t>(bins[r]);
       }
@@ -447,13 +545,17 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 
 template <int LUTM, bool F4, bool HIST, int R>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  auto fn = classify_kernel<LUTM, F4, HIST, R>;
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds)) != hipSuccess)
-      (void)hipGetLastError();  // not required on gfx950; never leave a sticky error behind
-  }
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, s, a);
+  constexpr int NT = (LUTM == kLdsU8 || LUTM == kLdsU16) ? kLdsBlock : kBlock;
+  auto fn = classify_kernel<LUTM, F4, HIST, R, 0, NT>;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+template <int LUTM, bool F4, bool HIST, int R, int ABL>
+int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, R, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -461,6 +563,16 @@ int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
 
 template <int LUTM, bool F4, bool HIST>
 int launch_r(const ClassifyArgs& a, int rounds, int grid, size_t lds, hipStream_t s) {
+  if constexpr (LUTM == kGlobalU8 && F4 && !HIST) {
+    static const int abl = [] {
+      const char* e = std::getenv("NBG_ABL");
+      return e ? std::atoi(e) : 0;
+    }();
+    if (abl == 1) return launch_abl<LUTM, F4, HIST, 1, 1>(a, grid, lds, s);
+    if (abl == 2) return launch_abl<LUTM, F4, HIST, 1, 2>(a, grid, lds, s);
+    if (abl == 3) return launch_abl<LUTM, F4, HIST, 1, 3>(a, grid, lds, s);
+    if (abl == 4) return launch_abl<LUTM, F4, HIST, 1, 4>(a, grid, lds, s);
+  }
   switch (rounds) {
     case 1: return launch_one<LUTM, F4, HIST, 1>(a, grid, lds, s);
     case 2: return launch_one<LUTM, F4, HIST, 2>(a, grid, lds, s);
@@ -478,7 +590,8 @@ int launch_mode(const ClassifyArgs& a, bool hist, int rounds, int grid, size_t l
 }
 
 size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
-  return static_cast<size_t>(lut_lds_bytes) + 4u * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
+  const uint32_t waves = (lut_lds_bytes ? kLdsBlock : kBlock) / 64;
+  return static_cast<size_t>(lut_lds_bytes) + waves * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
 }
 
 }  // namespace
@@ -502,7 +615,7 @@ int launch_scan(const ScanArgs& a, void* stream) {
 }
 
 size_t group_lds(uint32_t nbins, uint32_t n_parts, bool lds_scan) {
-  size_t w = static_cast<size_t>(nbins) * (2 + kGBlock / 64) + kChunk + kChunk / 2;
+  size_t w = static_cast<size_t>(nbins) * (3 + kGBlock / 64) + kChunk + kChunk / 2;
   if (lds_scan) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }

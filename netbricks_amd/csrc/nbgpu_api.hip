@@ -268,7 +268,7 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   if (group && nbins > kMaxGroupBins)
     return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
   const bool lds = use_lds_lut(h, flags);
-  const uint32_t hist_tile = kBlock * h->rounds;
+  const uint32_t hist_tile = (lds ? kLdsBlock : kBlock) * h->rounds;
   const uint32_t n_tiles = static_cast<uint32_t>((n_pkts + hist_tile - 1) / hist_tile);
   // LDS-staged LUT: persistent resident grid; L2 LUT: one tile per block
   const int grid = lds ? std::min<int>(h->grid_lds, static_cast<int>(n_tiles)) : static_cast<int>(n_tiles);

@@ -17,7 +17,8 @@ uint64_t xxh64(const uint8_t* p, size_t n, uint64_t seed);
 int build_lut(const char* const* names, const uint32_t* lens, uint32_t n, uint64_t m, std::vector<uint32_t>& entry);
 
 // Kernel geometry.
-constexpr int kBlock = 256;          // classify threads per workgroup (4 waves)
+constexpr int kBlock = 256;          // classify threads per workgroup (4 waves), L2-gather LUT
+constexpr int kLdsBlock = 1024;      // classify threads per workgroup with the LDS-staged LUT (1 per CU)
 constexpr int kXStride = 80;         // LDS bytes per packet in the transpose (64 + 16: conflict-free b128)
 constexpr int kGBlock = 1024;        // group kernel threads per workgroup (16 waves)
 constexpr int kGRounds = 4;          // group kernel rounds of 64 packets per wave per chunk

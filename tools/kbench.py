@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--nb", type=int, default=65)
     ap.add_argument("--m", type=int, default=65537)
+    ap.add_argument("--only", default="", help="comma-separated substrings of variant names to run")
+    ap.add_argument("--no-multistream", action="store_true")
+    ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS for every variant")
     args = ap.parse_args()
     import torch
 
@@ -47,16 +50,15 @@ def main():
     desc = args.mode != 0
 
     def kw(i):
+        extra = dict(lut_lds=True) if args.lut_lds else {}
         if desc:
-            return dict(offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True)
-        return dict(stride=stride, frame_len=60)
+            return dict(offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True, **extra)
+        return dict(stride=stride, frame_len=60, **extra)
 
     variants = {
         "copy(read+write all bytes)": lambda i: dst.copy_(bufs[i % 8]),
         "classify noswap nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, swap_macs=False,
                                                          backend=backend, **kw(i)),
-        "classify noswap nogroup ldslut": lambda i: mg.group_by(bufs[i % 8], n, group=False, swap_macs=False,
-                                                                lut_lds=True, backend=backend, **kw(i)),
         "classify inplace nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, backend=backend, **kw(i)),
         "classify inplace-wb16 nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, wb_partial=True,
                                                                backend=backend, **kw(i)),
@@ -74,7 +76,7 @@ def main():
     }
     # multi-stream: independent batches in flight on S streams, one handle (scratch) per stream
     extra = {}
-    for S in (2, 3, 4):
+    for S in (() if args.no_multistream else (2, 3, 4)):
         mgs = [nb.Maglev(names, args.m) for _ in range(S)]
         sts = [torch.cuda.Stream(dev) for _ in range(S)]
         outs = [(torch.empty(n, dtype=torch.uint16, device=dev), torch.empty(n, dtype=torch.uint32, device=dev),
@@ -91,6 +93,9 @@ def main():
         extra[f"full path l2 inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False))
         extra[f"_keep{S}"] = (mgs, sts, outs)
     variants.update({k: v for k, v in extra.items() if not k.startswith("_keep")})
+    if args.only:
+        keys = [k.strip() for k in args.only.split(",")]
+        variants = {k: v for k, v in variants.items() if any(q in k for q in keys)}
     res = {k: [] for k in variants}
     all_streams = [st for k, v in extra.items() if k.startswith("_keep") for st in v[1]]
     for r in range(args.rounds):
