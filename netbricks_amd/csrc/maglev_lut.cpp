@@ -112,7 +112,13 @@ int build_lut(const char* const* names, const uint32_t* lens, uint32_t n, uint64
   uint64_t filled = 0;
   while (filled < m) {
     for (uint32_t i = 0; i < n; ++i) {
-      while (entry[cur[i]] != kEmpty) advance(i);
+      while (entry[cur[i]] != kEmpty) {
+        advance(i);
+        // permutations[i][m] would be out of bounds: the reference panics (nf.rs:52-54)
+        if (next[i] >= m)
+          return set_error(NBG_EINVAL, "maglev: permutation of backend %u exhausted (table size %llu not coprime "
+                           "to its skip; use a prime table size)", i, (unsigned long long)m);
+      }
       if (entry[cur[i]] == kEmpty) {
         entry[cur[i]] = i;
         advance(i);

@@ -81,6 +81,12 @@ int orc_lut_build(const char *const *names, const uint32_t *lens, uint32_t n, ui
             uint64_t c = (off[i] + (unsigned __int128)next[i] * skip[i] % m) % m;
             while (entry[c] != ORC_EMPTY) {
                 next[i]++;
+                if (next[i] >= m) { /* permutations[i][m] is out of bounds: the reference panics */
+                    free(off);
+                    free(skip);
+                    free(next);
+                    return -34;
+                }
                 c = (off[i] + (unsigned __int128)next[i] * skip[i] % m) % m;
             }
             if (entry[c] == ORC_EMPTY) {

@@ -82,6 +82,8 @@ def generate_lut(names: list[str], lsize: int) -> list[int]:
             c = (off + nxt[i] * skip) % lsize
             while entry[c] != LUT_EMPTY:
                 nxt[i] += 1
+                if nxt[i] >= lsize:  # permutations[i][lsize] is out of bounds: the reference panics
+                    raise IndexError("maglev: permutation exhausted (table size not coprime to skip)")
                 c = (off + nxt[i] * skip) % lsize
             if entry[c] == LUT_EMPTY:
                 entry[c] = i

@@ -271,3 +271,45 @@ def test_defer_group_split(torch_cuda, mg65):
            r.perm.view(torch_cuda.int32).cpu().numpy().view(np.uint32),
            r.counts.view(torch_cuda.int32).cpu().numpy().view(np.uint32))
     _assert_same(got, exp)
+
+
+def test_golden_packets_fixture(torch_cuda, mg65):
+    """The committed golden vectors (tests/golden/packets.npz, made by the Python oracle)."""
+    import os
+
+    pk = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "packets.npz")))
+    n = pk["off"].size
+    buf = pk["buf"].copy()
+    got = _run(torch_cuda, mg65, buf, n, offs=pk["off"], lens=pk["len"])
+    np.testing.assert_array_equal(got[1], pk["backend65"])
+    np.testing.assert_array_equal(got[2], pk["perm65"])
+    np.testing.assert_array_equal(got[3], pk["counts65"])
+    for i in range(n):
+        ln = min(12, int(pk["len"][i]))
+        o = int(pk["off"][i])
+        assert got[0][o:o + ln].tobytes() == pk["mac12"][i, :ln].tobytes(), i
+
+
+def test_golden_lemmy_pcap_host_path(torch_cuda):
+    """The reference's macswap fixture (http_lemmy.pcap) through nbg_maglev_classify_host."""
+    import json
+    import os
+    import struct
+
+    from netbricks_amd import Maglev
+
+    gold_dir = os.path.join(os.path.dirname(__file__), "golden")
+    data = open(os.path.join(gold_dir, "http_lemmy.pcap"), "rb").read()
+    pos, frames = 24, []
+    while pos + 16 <= len(data):
+        incl = struct.unpack("<IIII", data[pos:pos + 16])[2]
+        frames.append(bytearray(data[pos + 16:pos + 16 + incl]))
+        pos += 16 + incl
+    gold = json.load(open(os.path.join(gold_dir, "lemmy.json")))
+    mg = Maglev(["Larry", "Curly", "Moe"], 65537)
+    be, perm, counts = mg.group_by_host(frames)
+    assert be.tolist() == [g["backend3"] for g in gold]
+    assert [f[:12].hex() for f in frames] == [g["swapped_head12"] for g in gold]
+    assert counts.tolist() == [8, 7, 0, 0]
+    assert perm.tolist() == [0, 2, 3, 6, 8, 10, 11, 14, 1, 4, 5, 7, 9, 12, 13]
+    mg.close()
