@@ -1,0 +1,309 @@
+// Host-side mirror of the NetBricks batch-operator surface for the Maglev path, backed by
+// the MI355X C-ABI (include/nbgpu.h).  Same names and meaning as the reference:
+//
+//   ReceiveBatch::new(port)          framework/src/operators/receive_batch.rs:9-98
+//   .parse::<MacHeader>()            framework/src/operators/mod.rs:59-64, parsed_batch.rs
+//   .transform(swap_addresses)       framework/src/operators/transform_batch.rs:11-118
+//   .group_by(ct, group_fn, sched)   framework/src/operators/group_by.rs:13-113
+//   GroupBy::get_group(i)            group_by.rs:102-112 (+ RestoreHeader, restore_header.rs)
+//   merge(batches)                   framework/src/operators/merge_batch.rs:10-111
+//   .compose() / .send(port)         composition_batch.rs:13-60, send_batch.rs:10-125
+//   MpscQueue (1024 slots)           framework/src/queues/mpsc_mbuf_queue.rs:22-265
+//   StandaloneScheduler              framework/src/scheduler/standalone_scheduler.rs:127-158
+//
+// The per-packet closures of test/maglev (nf.rs:94-106) cannot cross an FFI boundary per
+// packet, so the transform and group functions of this path are *descriptors* (MacSwap,
+// MaglevGroup) that the GPU group_by recognises: its producer task accumulates received
+// bursts into one batch, runs parse + swap + flow hash + LUT lookup + stable grouping in one
+// nbg_maglev_classify_host call, and enqueues the mbufs into the per-group FIFOs in arrival
+// order — exactly what GroupByProducer::execute (group_by.rs:43-55) does packet by packet.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/nbgpu.h"
+
+namespace nb {
+
+// ---- packets ----------------------------------------------------------------------------
+// Stand-in for rte_mbuf: data pointer + data_len + the two metadata slots NetBricks uses to
+// save the parsed header and offset (interface/packet.rs:55-64, 217-221).
+struct MBuf {
+  std::vector<uint8_t> storage;  // data room (DPDK: >= 2 KiB, so 64-B windows are owned)
+  uint16_t data_len = 0;
+  uintptr_t meta[2] = {0, 0};    // HEADER_SLOT, OFFSET_SLOT
+  uint64_t port_seq = 0;         // position in the receiving port's stream (bookkeeping)
+  uint8_t* data() { return storage.data(); }
+};
+
+struct PacketRx {  // interface/mod.rs:11-13
+  virtual ~PacketRx() = default;
+  virtual uint32_t recv(MBuf** pkts, uint32_t cap) = 0;
+};
+struct PacketTx {  // interface/mod.rs:15-17
+  virtual ~PacketTx() = default;
+  virtual uint32_t send(MBuf** pkts, uint32_t n) = 0;
+};
+
+class NbError : public std::runtime_error {
+ public:
+  NbError(int code, const std::string& what) : std::runtime_error(what), code(code) {}
+  int code;
+};
+
+inline void check(int rc, const char* where) {
+  if (rc != NBG_OK) throw NbError(rc, std::string(where) + ": " + nbg_last_error());
+}
+
+// ---- queues -------------------------------------------------------------------------------
+// Single-producer ring of mbuf pointers with the reference's capacity rule (mask + tail - head,
+// mpsc_mbuf_queue.rs:91-115): a full queue refuses the packet and the producer drops it.
+class MpscQueue {
+ public:
+  explicit MpscQueue(uint32_t size = 1024) : ring_(size), mask_(size - 1) {
+    if (size & (size - 1)) throw std::invalid_argument("queue size must be a power of two");
+  }
+  bool enqueue_one(MBuf* m) {
+    if (mask_ + tail_ - head_ == 0) return false;  // free slots = mask + consumer_tail - producer_head
+    ring_[head_++ & mask_] = m;
+    return true;
+  }
+  uint32_t dequeue(MBuf** out, uint32_t cap) {  // mpsc_mbuf_queue.rs:197-212
+    uint32_t n = 0;
+    while (n < cap && tail_ != head_) out[n++] = ring_[tail_++ & mask_];
+    return n;
+  }
+  uint64_t size() const { return head_ - tail_; }
+  uint64_t free_slots() const { return mask_ + tail_ - head_; }
+
+ private:
+  std::vector<MBuf*> ring_;
+  uint64_t mask_, head_ = 0, tail_ = 0;
+};
+
+// ---- scheduler ----------------------------------------------------------------------------
+struct Executable {  // scheduler/mod.rs: trait Executable
+  virtual ~Executable() = default;
+  virtual void execute() = 0;
+};
+
+// Run-to-completion round robin over tasks (standalone_scheduler.rs:127-158).
+class StandaloneScheduler {
+ public:
+  size_t add_task(std::shared_ptr<Executable> t) {
+    tasks_.push_back(std::move(t));
+    return tasks_.size() - 1;
+  }
+  void execute_round() {
+    for (auto& t : tasks_) t->execute();
+  }
+
+ private:
+  std::vector<std::shared_ptr<Executable>> tasks_;
+};
+
+// ---- batches ------------------------------------------------------------------------------
+constexpr uint32_t kBurst = 32;  // ReceiveBatch::new -> PacketBatch::new(32), receive_batch.rs:26
+
+// A batch source: act() fills `pkts`, done() releases them (the Act trait, operators/act.rs).
+struct Batch {
+  virtual ~Batch() = default;
+  virtual void act() = 0;
+  virtual void done() = 0;
+  std::vector<MBuf*> pkts;
+};
+
+struct ReceiveBatch : Batch {  // receive_batch.rs:9-98
+  explicit ReceiveBatch(std::shared_ptr<PacketRx> q) : queue(std::move(q)) {}
+  void act() override {
+    pkts.resize(kBurst);
+    pkts.resize(queue->recv(pkts.data(), kBurst));
+    received += pkts.size();
+  }
+  void done() override { pkts.clear(); }
+  std::shared_ptr<PacketRx> queue;
+  uint64_t received = 0;
+};
+
+struct MacHeader {};  // headers/mac.rs:69-75; offset() == 14 under feature "performance"
+struct MacSwap {};    // MacHeader::swap_addresses (mac.rs:140-145) as a transform descriptor
+
+// ParsedBatch<MacHeader> (parsed_batch.rs) + TransformBatch(MacSwap): on this path both are
+// folded into the group_by kernel, so the chain only records what to apply.
+struct ParsedMacBatch {
+  std::shared_ptr<Batch> parent;
+  bool swap = false;
+};
+
+inline ParsedMacBatch parse_mac(std::shared_ptr<Batch> parent) { return ParsedMacBatch{std::move(parent), false}; }
+inline ParsedMacBatch transform(ParsedMacBatch p, MacSwap) {
+  p.swap = true;
+  return p;
+}
+
+// The Maglev group function of test/maglev (nf.rs:101-106): lut[flow_hash % M].
+class MaglevGroup {
+ public:
+  MaglevGroup(const std::vector<std::string>& backends, uint64_t lut_size, int device = 0) {
+    std::vector<const char*> names;
+    std::vector<uint32_t> lens;
+    for (auto& b : backends) {
+      names.push_back(b.data());
+      lens.push_back(static_cast<uint32_t>(b.size()));
+    }
+    nbg_maglev* h = nullptr;
+    check(nbg_maglev_create(names.data(), lens.data(), static_cast<uint32_t>(names.size()), lut_size, device, &h),
+          "nbg_maglev_create");
+    h_.reset(h, nbg_maglev_destroy);
+  }
+  nbg_maglev* handle() const { return h_.get(); }
+  uint32_t backends() const { return nbg_maglev_backends(h_.get()); }
+
+ private:
+  std::shared_ptr<nbg_maglev> h_;
+};
+
+// GroupBy (group_by.rs:15-113) with the GPU producer.  Packets whose group index would be
+// out of range in the reference (the would-panic sentinel) go to group `ct` (an extra
+// queue, get_group(ct)); everything else keeps the reference semantics.
+class GroupBy {
+ public:
+  GroupBy(ParsedMacBatch parent, uint32_t groups, MaglevGroup fn, StandaloneScheduler& sched,
+          uint32_t max_batch = 4096)
+      : groups_(groups) {
+    if (groups != fn.backends()) throw std::invalid_argument("group_by: groups != Maglev backends");
+    // the reference's queues hold 1024 mbufs (mpsc_mbuf_queue.rs:261); a GPU batch of
+    // max_batch packets needs room for a whole batch in one group
+    uint32_t qsize = 1024;
+    while (qsize < 2 * max_batch) qsize <<= 1;
+    for (uint32_t i = 0; i <= groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(qsize));
+    producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch);
+    task_ = sched.add_task(producer_);
+  }
+  uint32_t len() const { return groups_; }
+
+  // get_group(i): a ReceiveBatch over the group's MPSC consumer (+ RestoreHeader: the saved
+  // header/offset are in the mbuf metadata slots).
+  std::shared_ptr<ReceiveBatch> get_group(uint32_t i) {
+    if (i > groups_) return nullptr;
+    struct Consumer : PacketRx {
+      std::shared_ptr<MpscQueue> q;
+      uint32_t recv(MBuf** p, uint32_t cap) override { return q->dequeue(p, cap); }
+    };
+    auto c = std::make_shared<Consumer>();
+    c->q = queues_[i];
+    return std::make_shared<ReceiveBatch>(c);
+  }
+  uint64_t dropped() const { return producer_->dropped; }
+  uint64_t processed() const { return producer_->processed; }
+
+ private:
+  struct Producer : Executable {
+    Producer(ParsedMacBatch p, MaglevGroup f, std::vector<std::shared_ptr<MpscQueue>> q, uint32_t max_batch)
+        : parent(std::move(p)), fn(std::move(f)), queues(std::move(q)), max_batch(max_batch) {}
+    // GroupByProducer::execute (group_by.rs:43-55) for a whole batch: pull bursts until the
+    // batch is full or the port is idle, classify on the GPU, enqueue in per-group FIFO order.
+    void execute() override {
+      // backpressure: leave packets in the port (NIC ring) while a group could not absorb a
+      // whole batch, instead of pulling them and dropping on a full queue
+      for (auto& q : queues)
+        if (q->free_slots() < max_batch) return;
+      std::vector<MBuf*> batch;
+      for (;;) {
+        parent.parent->act();
+        auto& b = parent.parent->pkts;
+        batch.insert(batch.end(), b.begin(), b.end());
+        const bool idle = b.size() < kBurst;
+        parent.parent->done();
+        if (idle || batch.size() >= max_batch) break;
+      }
+      if (batch.empty()) return;
+      const size_t n = batch.size();
+      ptrs.resize(n);
+      lens.resize(n);
+      backend.resize(n);
+      perm.resize(n);
+      counts.resize(queues.size());
+      for (size_t i = 0; i < n; ++i) {
+        ptrs[i] = batch[i]->data();
+        lens[i] = batch[i]->data_len;
+      }
+      check(nbg_maglev_classify_host(fn.handle(), ptrs.data(), lens.data(), n, parent.swap ? NBG_SWAP_MACS : 0u,
+                                     backend.data(), perm.data(), counts.data()),
+            "nbg_maglev_classify_host");
+      size_t k = 0;
+      for (size_t g = 0; g < queues.size(); ++g) {
+        for (uint32_t j = 0; j < counts[g]; ++j, ++k) {
+          MBuf* m = batch[perm[k]];
+          m->meta[0] = reinterpret_cast<uintptr_t>(m->data());  // save_header_and_offset
+          m->meta[1] = 14;
+          if (!queues[g]->enqueue_one(m)) ++dropped;           // full queue: packet lost
+        }
+      }
+      processed += n;
+    }
+    ParsedMacBatch parent;
+    MaglevGroup fn;
+    std::vector<std::shared_ptr<MpscQueue>> queues;
+    uint32_t max_batch;
+    std::vector<uint8_t*> ptrs;
+    std::vector<uint16_t> lens, backend;
+    std::vector<uint32_t> perm, counts;
+    uint64_t dropped = 0, processed = 0;
+  };
+
+  uint32_t groups_;
+  std::vector<std::shared_ptr<MpscQueue>> queues_;
+  std::shared_ptr<Producer> producer_;
+  size_t task_ = 0;
+};
+
+// MergeBatch + CompositionBatch + SendBatch (merge_batch.rs:44-57, send_batch.rs:66-78): each
+// execution receives one burst from the current group, sends it, and rotates the group.
+class MergeSend : public Executable {
+ public:
+  MergeSend(std::vector<std::shared_ptr<ReceiveBatch>> parents, std::shared_ptr<PacketTx> port)
+      : parents_(std::move(parents)), port_(std::move(port)) {}
+  void execute() override {
+    auto& b = *parents_[which_];
+    b.act();
+    if (!b.pkts.empty()) sent += port_->send(b.pkts.data(), static_cast<uint32_t>(b.pkts.size()));
+    b.done();
+    which_ = (which_ + 1) % parents_.size();
+  }
+  uint64_t sent = 0;
+
+ private:
+  std::vector<std::shared_ptr<ReceiveBatch>> parents_;
+  std::shared_ptr<PacketTx> port_;
+  size_t which_ = 0;
+};
+
+// test/maglev/src/nf.rs:84-111 with the GPU group_by: returns the merged, composed
+// pipeline of all groups, ready to be sent (main.rs:33-37 `.send(port)`).
+struct MaglevPipeline {
+  std::shared_ptr<GroupBy> groups;
+  std::shared_ptr<MergeSend> tx;
+};
+
+inline MaglevPipeline maglev(std::shared_ptr<Batch> parent, StandaloneScheduler& s,
+                             const std::vector<std::string>& backends, std::shared_ptr<PacketTx> port,
+                             uint64_t lut_size = 65537, uint32_t max_batch = 4096) {
+  const uint32_t ct = static_cast<uint32_t>(backends.size());
+  MaglevGroup lut(backends, lut_size);  // Maglev::new(backends, 65537), nf.rs:90
+  auto groups = std::make_shared<GroupBy>(transform(parse_mac(std::move(parent)), MacSwap{}), ct, lut, s,
+                                          max_batch);
+  std::vector<std::shared_ptr<ReceiveBatch>> outs;
+  for (uint32_t i = 0; i <= ct; ++i) outs.push_back(groups->get_group(i));  // + sentinel group
+  auto tx = std::make_shared<MergeSend>(outs, std::move(port));
+  s.add_task(tx);
+  return {groups, tx};
+}
+
+}  // namespace nb

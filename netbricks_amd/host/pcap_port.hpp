@@ -1,0 +1,98 @@
+// A pcap-file port: the `dpdk:eth_pcap0,rx_pcap=...,tx_pcap=...` PMD that the reference's
+// example NFs use for testing (test/macswap/check.sh:3, README "Example NFs").  recv() hands
+// out the capture's frames in bursts; send() appends frames to the output capture.
+#pragma once
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "operators.hpp"
+
+namespace nb {
+
+struct PcapRecord {
+  uint32_t ts_sec = 0, ts_usec = 0;
+  std::vector<uint8_t> data;
+};
+
+inline std::vector<PcapRecord> read_pcap(const std::string& path) {
+  std::vector<PcapRecord> out;
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw std::runtime_error("cannot open " + path);
+  uint32_t gh[6];
+  if (std::fread(gh, 4, 6, f) != 6 || (gh[0] != 0xA1B2C3D4u && gh[0] != 0xA1B23C4Du)) {
+    std::fclose(f);
+    throw std::runtime_error("not a little-endian pcap: " + path);
+  }
+  uint32_t rh[4];
+  while (std::fread(rh, 4, 4, f) == 4) {
+    PcapRecord r;
+    r.ts_sec = rh[0];
+    r.ts_usec = rh[1];
+    r.data.resize(rh[2]);
+    if (rh[2] && std::fread(r.data.data(), 1, rh[2], f) != rh[2]) break;
+    out.push_back(std::move(r));
+  }
+  std::fclose(f);
+  return out;
+}
+
+inline void write_pcap(const std::string& path, const std::vector<PcapRecord>& recs) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot create " + path);
+  const uint32_t gh[6] = {0xA1B2C3D4u, 0x00040002u, 0, 0, 65535, 1 /* LINKTYPE_ETHERNET */};
+  std::fwrite(gh, 4, 6, f);
+  for (auto& r : recs) {
+    const uint32_t rh[4] = {r.ts_sec, r.ts_usec, static_cast<uint32_t>(r.data.size()),
+                            static_cast<uint32_t>(r.data.size())};
+    std::fwrite(rh, 4, 4, f);
+    std::fwrite(r.data.data(), 1, r.data.size(), f);
+  }
+  std::fclose(f);
+}
+
+// One port with an rx capture (consumed once) and a tx capture (collected in send order).
+class PcapPort : public PacketRx, public PacketTx {
+ public:
+  explicit PcapPort(const std::string& rx_path, uint32_t data_room = 2048) {
+    for (auto& r : read_pcap(rx_path)) {
+      auto m = std::make_unique<MBuf>();
+      m->storage.assign(std::max<size_t>(data_room, r.data.size()), 0);
+      std::memcpy(m->storage.data(), r.data.data(), r.data.size());
+      m->data_len = static_cast<uint16_t>(r.data.size());
+      m->port_seq = pool_.size();
+      ts_.push_back({r.ts_sec, r.ts_usec});
+      pool_.push_back(std::move(m));
+    }
+  }
+  uint32_t recv(MBuf** pkts, uint32_t cap) override {
+    uint32_t n = 0;
+    while (n < cap && next_ < pool_.size()) pkts[n++] = pool_[next_++].get();
+    return n;
+  }
+  uint32_t send(MBuf** pkts, uint32_t n) override {
+    for (uint32_t i = 0; i < n; ++i) {
+      PcapRecord r;
+      r.data.assign(pkts[i]->data(), pkts[i]->data() + pkts[i]->data_len);
+      tx_.push_back(std::move(r));
+      tx_index_.push_back(pkts[i]->port_seq);
+    }
+    return n;
+  }
+  bool rx_done() const { return next_ >= pool_.size(); }
+  size_t rx_total() const { return pool_.size(); }
+  const std::vector<PcapRecord>& tx() const { return tx_; }
+  const std::vector<size_t>& tx_index() const { return tx_index_; }  // rx position of each sent frame
+
+ private:
+  std::vector<std::unique_ptr<MBuf>> pool_;
+  std::vector<std::pair<uint32_t, uint32_t>> ts_;
+  size_t next_ = 0;
+  std::vector<PcapRecord> tx_;
+  std::vector<size_t> tx_index_;
+};
+
+}  // namespace nb

@@ -271,3 +271,15 @@ def test_oracle_is_test_infrastructure_only():
             if f.endswith((".py", ".hip", ".cpp", ".h", ".hpp", "Makefile")):
                 txt = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "maglev_ref" not in txt and "liborc" not in txt and "orc_" not in txt, f
+
+
+def test_host_operator_selftest():
+    """C++ operator mirror pieces that need no GPU: MPSC ring semantics and the pcap port."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "netbricks_amd", "host", "nb_host_selftest")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.dirname(exe)], check=True, capture_output=True)
+    r = subprocess.run([exe, os.path.join(GOLD, "http_lemmy.pcap"), "/tmp/nb_selftest_out.pcap"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
