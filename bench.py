@@ -82,6 +82,27 @@ def cpu_baseline(batch_host, lut, target_cpu_s=12.0):
                       f"{threads} pinned threads, {total_s * threads:.1f} CPU-s; host CPU: {model}"}
 
 
+def shard_seed(rank: int, batch: int) -> int:
+    """Seed of rank `rank`'s batch `batch`: every rank owns distinct packets (weak scaling)."""
+    return SEED + 1000003 * rank + batch
+
+
+def shared_lut(names, table, rank, world, device):
+    """Rank 0 builds the Maglev LUT (Maglev::new, nf.rs:70-76) and broadcasts it once (RCCL over
+    xGMI on GPUs, gloo in the CPU tests); every rank returns the same u16 table."""
+    import torch
+    import torch.distributed as dist
+
+    import netbricks_amd as nb
+
+    lut_t = torch.empty(table, dtype=torch.int32, device=device)
+    if rank == 0:
+        lut_t.copy_(torch.from_numpy(nb.build_lut(names, table).astype(np.int32)))
+    if world > 1:
+        dist.broadcast(lut_t, 0)
+    return lut_t.cpu().numpy().astype(np.uint16)
+
+
 def read_traffic():
     """HBM bytes per classify launch from the committed PMC profile (profiles/pmc_*.json), if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
@@ -119,11 +140,7 @@ def main():
 
     names = [f"backend-{i}" for i in range(N_BACKENDS)]
     if world > 1:
-        lut_t = torch.empty(TABLE, dtype=torch.int32, device=dev)
-        if rank == 0:
-            lut_t.copy_(torch.from_numpy(nb.build_lut(names, TABLE).astype(np.int32)))
-        dist.broadcast(lut_t, 0)  # RCCL over xGMI, once per backend set
-        lut = lut_t.cpu().numpy().astype(np.uint16)
+        lut = shared_lut(names, TABLE, rank, world, dev)  # RCCL broadcast, once per backend set
         mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(args.streams)]
     else:
         mgs = [nb.Maglev(names, TABLE, device=local) for _ in range(args.streams)]
@@ -133,7 +150,7 @@ def main():
     host0 = None
     dbufs = []
     for b in range(N_BATCHES):
-        buf, _, _ = nb.make_trace(BATCH, 0, seed=SEED + 1000003 * rank + b)
+        buf, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(rank, b))
         if b == 0:
             host0 = buf.copy()
         dbufs.append(torch.from_numpy(buf).to(dev))
