@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""End-to-end (host memory in, host memory out) Maglev throughput over PCIe.
+
+(a) pipelined: 64-B header windows of 1M-packet batches in pinned host memory; per batch on
+    one of S streams: H2D windows -> classify (+ grouping, MAC swap as 12-B records) -> D2H
+    backend + perm + MAC records.  Reports Mpps and PCIe GB/s per direction.
+(b) nbg_maglev_classify_host: scattered "mbufs" (2 KiB data rooms) -> gather into pinned
+    staging -> H2D -> kernels -> D2H -> MAC rewrite into the mbufs; synchronous, one call per
+    batch, as a GpuGroupBy producer would issue it.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--batches", type=int, default=24)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--host-n", type=int, default=1 << 18)
+    args = ap.parse_args()
+    import torch
+
+    import netbricks_amd as nb
+    from netbricks_amd import _lib
+
+    dev = torch.device("cuda:0")
+    names = [f"backend-{i}" for i in range(65)]
+    n = args.n
+    buf, _, _ = nb.make_trace(n, 0, seed=77)
+    S = args.streams
+    mgs = [nb.Maglev(names, 65537) for _ in range(S)]
+    sts = [torch.cuda.Stream(dev) for _ in range(S)]
+    h_win = [torch.from_numpy(buf.copy()).pin_memory() for _ in range(S)]
+    d_win = [torch.empty(n * 64, dtype=torch.uint8, device=dev) for _ in range(S)]
+    d_be = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(S)]
+    d_pm = [torch.empty(n, dtype=torch.uint32, device=dev) for _ in range(S)]
+    d_ct = [torch.empty(66, dtype=torch.uint32, device=dev) for _ in range(S)]
+    d_mac = [torch.empty(n * 12, dtype=torch.uint8, device=dev) for _ in range(S)]
+    h_be = [torch.empty(n, dtype=torch.int16).pin_memory() for _ in range(S)]
+    h_pm = [torch.empty(n, dtype=torch.int32).pin_memory() for _ in range(S)]
+    h_mac = [torch.empty(n * 12, dtype=torch.uint8).pin_memory() for _ in range(S)]
+
+    def batch(i):
+        j = i % S
+        with torch.cuda.stream(sts[j]):
+            d_win[j].copy_(h_win[j], non_blocking=True)
+            mgs[j].group_by(d_win[j], n, backend=d_be[j], perm=d_pm[j], counts=d_ct[j], mac_out=d_mac[j],
+                            stream=sts[j].cuda_stream)
+            h_be[j].copy_(d_be[j].view(torch.int16), non_blocking=True)
+            h_pm[j].copy_(d_pm[j].view(torch.int32), non_blocking=True)
+            h_mac[j].copy_(d_mac[j], non_blocking=True)
+
+    for i in range(S):
+        batch(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.batches):
+        batch(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    pk = args.batches * n
+    res = {"pipelined": {"mpps": round(pk / dt / 1e6, 1), "h2d_gbps": round(pk * 64 / dt / 1e9, 1),
+                         "d2h_gbps": round(pk * (2 + 4 + 12) / dt / 1e9, 1), "streams": S, "batch_pkts": n,
+                         "h2d_bytes_per_pkt": 64, "d2h_bytes_per_pkt": 18}}
+    # H2D alone for reference
+    t0 = time.perf_counter()
+    for i in range(args.batches):
+        with torch.cuda.stream(sts[i % S]):
+            d_win[i % S].copy_(h_win[i % S], non_blocking=True)
+    torch.cuda.synchronize()
+    res["h2d_only_gbps"] = round(args.batches * n * 64 / (time.perf_counter() - t0) / 1e9, 1)
+
+    # (b) the synchronous host-mbuf entry point
+    hn = args.host_n
+    room = 2048
+    mbufs = np.zeros(hn * room, dtype=np.uint8)
+    for i in range(hn):
+        mbufs[i * room:i * room + 60] = buf[(i % n) * 64:(i % n) * 64 + 60]
+    ptrs = (np.arange(hn, dtype=np.uint64) * room + mbufs.ctypes.data).astype(np.uint64)
+    lens = np.full(hn, 60, dtype=np.uint16)
+    be = np.empty(hn, dtype=np.uint16)
+    pm = np.empty(hn, dtype=np.uint32)
+    ct = np.empty(66, dtype=np.uint32)
+    h = mgs[0]._h
+    for it in range(2):
+        rc = _lib.lib.nbg_maglev_classify_host(h, ptrs.ctypes.data, lens.ctypes.data, hn, _lib.NBG_SWAP_MACS,
+                                               be.ctypes.data, pm.ctypes.data, ct.ctypes.data)
+        _lib.check(rc, "classify_host")
+    reps = 5
+    t0 = time.perf_counter()
+    for it in range(reps):
+        _lib.lib.nbg_maglev_classify_host(h, ptrs.ctypes.data, lens.ctypes.data, hn, _lib.NBG_SWAP_MACS,
+                                          be.ctypes.data, pm.ctypes.data, ct.ctypes.data)
+    dt = (time.perf_counter() - t0) / reps
+    res["classify_host"] = {"mpps": round(hn / dt / 1e6, 1), "batch_pkts": hn, "ms_per_batch": round(dt * 1e3, 3),
+                            "mbuf_data_room": room}
+    print(json.dumps(res))
+    _ = C
+
+
+if __name__ == "__main__":
+    main()
