@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnbgpu.so")
+# NBG_LIB_OVERRIDE: diagnostic builds of the same library (tools/); never set by the product
+LIB_PATH = os.environ.get("NBG_LIB_OVERRIDE") or os.path.join(_HERE, "libnbgpu.so")
 
 NBG_OK = 0
 NBG_SENTINEL = 0xFFFF

@@ -11,10 +11,11 @@
 //   (4 lanes per window, contiguous 1 KiB per instruction for the 64-B slot layout),
 //   transposes them through LDS to one packet per lane, and the lane holding chunk 0
 //   applies the MAC swap in registers and writes the window back with full-line stores.
-// scan_kernel — per backend bin, exclusive scan of the tile histograms over tiles; the
-//   last block to arrive scans the group totals into group bases.
-// scatter_kernel — per tile, wave ballot multisplit ranks (stable), a local counting sort
-//   in LDS, and coalesced stores of perm[] = packet indices grouped by backend.
+// scan_kernel — (many backends only) per backend bin, exclusive scan of the partition
+//   histograms over partitions, and the bin totals.
+// group_kernel — per partition: the per-bin prefix over earlier partitions and the group
+//   bases, then per 4096-packet chunk wave ballot multisplit ranks (stable), a local counting
+//   sort in LDS, and coalesced stores of perm[] = packet indices grouped by backend.
 //
 // Integer/byte work only; no MFMA.  HBM-bound.
 #include <hip/hip_runtime.h>
@@ -375,21 +376,31 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 // reduced here from the partition histograms staged in LDS, or read from scan_kernel's
 // output.  Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local
 // counting sort in LDS and coalesced perm stores.
-template <bool LDS_SCAN>
+#ifdef NBG_GPROBE  // diagnostic build: phase timestamps of three blocks, printed at exit
+#define GPROBE(k)                                                                          \
+  if (tid == 0 && (c == 0 || c == gridDim.x / 2 || c == gridDim.x - 1)) gpt[k] = wall_clock64();
+#else
+#define GPROBE(k)
+#endif
+template <int SCAN>
 __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
+#ifdef NBG_GPROBE
+  uint64_t gpt[10] = {};
+#endif
   extern __shared__ __align__(16) uint32_t gs[];
   __shared__ uint32_t s_wave[kGBlock / 64];
   constexpr uint32_t kW = kGBlock / 64;  // waves
   const uint32_t nbins = a.nb + 1;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   const uint32_t c = blockIdx.x;
+  GPROBE(0)
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbins;        // [nbins]
   uint32_t* cnt = tot + nbins;         // [kW][nbins]
   uint32_t* sub = cnt + kW * nbins;    // [nbins] per-chunk bin sizes, then chunk-local starts
   uint32_t* sidx = sub + nbins;        // [kChunk]
   uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
-  uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (LDS_SCAN)
+  uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (kScanLds)
 
   // ---- the first chunk's backends are loaded up front: their latency overlaps the prologue
   const uint32_t pbeg = c * a.part_pkts;
@@ -403,15 +414,42 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       pre_bin[r] = (a.perm && i < pend) ? a.backend[i] : 0u;
     }
   }
+  GPROBE(1)
   // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
   for (uint32_t b = tid; b < nbins; b += kGBlock) {
     base[b] = 0;
     tot[b] = 0;
   }
-  if constexpr (LDS_SCAN) {
+  if constexpr (SCAN == kScanDirect) {
+    __syncthreads();
+    // L threads per bin, each summing a strided subset of the partition rows straight from L2
+    // (consecutive threads read consecutive bins of one row: coalesced)
+    const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
+    for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
+      const uint32_t b = t % nbins, j = t / nbins;
+      uint32_t pre = 0, all = 0;
+      // kU loads in flight per thread: one L2 round trip per kU rows (n_parts <= 256, L >= 1)
+      constexpr uint32_t kU = 16;
+      for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
+        uint32_t h[kU];
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+          const uint32_t q = q0 + k * L;
+          h[k] = q < a.n_parts ? a.part_hist[q * nbins + b] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+          pre += q0 + k * L < c ? h[k] : 0u;
+          all += h[k];
+        }
+      }
+      if (pre) atomicAdd(&base[b], pre);
+      if (all) atomicAdd(&tot[b], all);
+    }
+  } else if constexpr (SCAN == kScanLds) {
     // stage the partition histograms: every load issued before any LDS store (one round trip)
     const uint32_t words = a.n_parts * nbins;
-    constexpr int kStage = 8;  // 8 x 1024 x 16 B = 128 KiB >= the LDS_SCAN limit
+    constexpr int kStage = 8;  // 8 x 1024 x 16 B = 128 KiB >= the kScanLds limit
     const uint32_t nvec = words / 4;
     const uint4* src = reinterpret_cast<const uint4*>(a.part_hist);
     uint4 tmp[kStage];
@@ -447,6 +485,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       tot[b] = a.totals[b];
     }
   }
+  GPROBE(2)
   // the next call accumulates into the other buffer: zero it (every block a slice)
   for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
   __syncthreads();
@@ -465,6 +504,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     }
   }
   __syncthreads();
+  GPROBE(3)
   if (!a.perm) return;
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -499,6 +539,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       ranks[r] = rank;
     }
     __syncthreads();
+    GPROBE(4)
     // per bin: offsets of each wave inside the bin (16-lane segmented scan over waves) ...
     for (uint32_t t = tid; t < nbins * kW; t += kGBlock) {
       const uint32_t b = t / kW, w = t % kW;
@@ -513,6 +554,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       if (w == kW - 1) sub[b] = x;  // the bin's packets in this chunk
     }
     __syncthreads();
+    GPROBE(5)
     // ... and the chunk-local start of each bin (scan over bins)
     const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
     const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
@@ -528,6 +570,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       lstart += n;
     }
     __syncthreads();
+    GPROBE(6)
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       if (bins[r] != 0xffffffffu) {
@@ -537,10 +580,20 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       }
     }
     __syncthreads();
+    GPROBE(7)
     // coalesced output: consecutive sorted slots of one bin are consecutive perm entries
     for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
     __syncthreads();
   }
+  GPROBE(8)
+#ifdef NBG_GPROBE
+  if (tid == 0 && (c == 0 || c == gridDim.x / 2 || c == gridDim.x - 1))
+    printf("GPROBE blk %u t0 %llu d: %llu %llu %llu %llu %llu %llu %llu %llu\n", c, (unsigned long long)gpt[0],
+           (unsigned long long)(gpt[1] - gpt[0]), (unsigned long long)(gpt[2] - gpt[1]),
+           (unsigned long long)(gpt[3] - gpt[2]), (unsigned long long)(gpt[4] - gpt[3]),
+           (unsigned long long)(gpt[5] - gpt[4]), (unsigned long long)(gpt[6] - gpt[5]),
+           (unsigned long long)(gpt[7] - gpt[6]), (unsigned long long)(gpt[8] - gpt[7]));
+#endif
 }
 
 template <int LUTM, bool F4, bool HIST, int R>
@@ -614,15 +667,29 @@ int launch_scan(const ScanArgs& a, void* stream) {
   return NBG_OK;
 }
 
-size_t group_lds(uint32_t nbins, uint32_t n_parts, bool lds_scan) {
+size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
   size_t w = static_cast<size_t>(nbins) * (3 + kGBlock / 64) + kChunk + kChunk / 2;
-  if (lds_scan) w += static_cast<size_t>(n_parts) * nbins;
+  if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }
 
-int launch_group(const GroupArgs& a, bool lds_scan, void* stream) {
-  const size_t lds = group_lds(a.nb + 1, a.n_parts, lds_scan);
-  auto fn = lds_scan ? group_kernel<true> : group_kernel<false>;
+// Default: sum the partition histograms from L2 inside the group kernel while the rows are
+// small (every block reads all of them), else a separate scan kernel.  NBG_GSCAN=0/1/2 forces
+// a mode (diagnostics; 1 falls back when the rows do not fit in LDS).
+int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
+  static const int forced = [] {
+    const char* e = std::getenv("NBG_GSCAN");
+    return e ? std::atoi(e) : -1;
+  }();
+  if (forced == kScanKernel || forced == kScanDirect) return forced;
+  if (forced == kScanLds && group_lds(nbins, n_parts, kScanLds) <= 100 * 1024) return kScanLds;
+  return static_cast<size_t>(nbins) * n_parts <= 32 * 1024 ? kScanDirect : kScanKernel;
+}
+
+int launch_group(const GroupArgs& a, int scan, void* stream) {
+  const size_t lds = group_lds(a.nb + 1, a.n_parts, scan);
+  auto fn = scan == kScanDirect ? group_kernel<kScanDirect>
+                                : (scan == kScanLds ? group_kernel<kScanLds> : group_kernel<kScanKernel>);
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess)

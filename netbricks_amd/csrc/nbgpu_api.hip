@@ -56,7 +56,7 @@ struct nbg_maglev {
   int rounds = 1;                     // classify rounds of 64 packets per wave per tile
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
   bool pending = false;
-  bool pending_lds_scan = false;
+  int pending_scan_mode = 0;
   GroupArgs pending_args{};
   ScanArgs pending_scan{};
   hipStream_t last_stream = nullptr;
@@ -302,8 +302,7 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   int rc = launch_classify(a, h->wide, lds, h->rounds, grid, stream);
   if (rc) return rc;
   if (group) {
-    // partition prefixes reduced inside the group kernel when the histograms fit in LDS
-    const bool lds_scan = group_lds(nbins, n_parts, true) <= 100 * 1024;
+    const int scan = pick_group_scan(nbins, n_parts);
     ScanArgs sa{};
     sa.part_hist = part_cur;
     sa.part_prefix = h->d_part_prefix;
@@ -329,12 +328,12 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
     h->parity ^= 1u;
     if (flags & NBG_DEFER_GROUP) {
       h->pending = true;
-      h->pending_lds_scan = lds_scan;
+      h->pending_scan_mode = scan;
       h->pending_args = ga;
       h->pending_scan = sa;
     } else {
-      if (!lds_scan && (rc = launch_scan(sa, stream))) return rc;
-      if ((rc = launch_group(ga, lds_scan, stream))) return rc;
+      if (scan == kScanKernel && (rc = launch_scan(sa, stream))) return rc;
+      if ((rc = launch_group(ga, scan, stream))) return rc;
     }
   }
   h->last_stream = static_cast<hipStream_t>(stream);
@@ -347,8 +346,8 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   DeviceGuard g(h->device);
   h->pending = false;
   int rc;
-  if (!h->pending_lds_scan && (rc = launch_scan(h->pending_scan, stream))) return rc;
-  if ((rc = launch_group(h->pending_args, h->pending_lds_scan, stream))) return rc;
+  if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
+  if ((rc = launch_group(h->pending_args, h->pending_scan_mode, stream))) return rc;
   h->last_stream = static_cast<hipStream_t>(stream);
   return NBG_OK;
 }

@@ -63,7 +63,7 @@ struct GroupArgs {
   uint32_t bits;              // ceil(log2(nb+1))
   uint32_t n_parts;
   uint32_t part_pkts;
-  const uint32_t* part_hist;  // [n_parts][nb+1]      (LDS_SCAN)
+  const uint32_t* part_hist;  // [n_parts][nb+1]      (kScanLds / kScanDirect)
   const uint32_t* part_prefix;// [n_parts][nb+1]      (scan_kernel path)
   const uint32_t* totals;     // [nb+1]               (scan_kernel path)
   uint32_t* part_hist_next;   // zeroed for the next call
@@ -72,11 +72,16 @@ struct GroupArgs {
   uint32_t* perm;             // nullable (counts only)
 };
 
+// How the group kernel gets each partition's per-bin prefix: from scan_kernel's output, by
+// summing the partition histograms staged in LDS, or by summing them straight from L2.
+enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
+
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int rounds, int grid, void* stream);
 int launch_scan(const ScanArgs& a, void* stream);
-int launch_group(const GroupArgs& a, bool lds_scan, void* stream);
-size_t group_lds(uint32_t nbins, uint32_t n_parts, bool lds_scan);
+int launch_group(const GroupArgs& a, int scan, void* stream);
+size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan);
+int pick_group_scan(uint32_t nbins, uint32_t n_parts);
 int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid);
 
 }  // namespace nbg

@@ -45,7 +45,7 @@ def main():
     backend = torch.empty(n, dtype=torch.uint16, device=dev)
     perm = torch.empty(n, dtype=torch.uint32, device=dev)
     counts = torch.empty(args.nb + 1, dtype=torch.uint32, device=dev)
-    dst = torch.empty_like(bufs[0])
+    dst = torch.empty(max(int(b.numel()) for b in bufs), dtype=torch.uint8, device=dev)
     mac = torch.empty(n * 12, dtype=torch.uint8, device=dev)
     desc = args.mode != 0
 
@@ -56,7 +56,7 @@ def main():
         return dict(stride=stride, frame_len=60, **extra)
 
     variants = {
-        "copy(read+write all bytes)": lambda i: dst.copy_(bufs[i % 8]),
+        "copy(read+write all bytes)": lambda i: dst[:bufs[i % 8].numel()].copy_(bufs[i % 8]),
         "classify noswap nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, swap_macs=False,
                                                          backend=backend, **kw(i)),
         "classify inplace nogroup": lambda i: mg.group_by(bufs[i % 8], n, group=False, backend=backend, **kw(i)),

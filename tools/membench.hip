@@ -69,6 +69,35 @@ __global__ __launch_bounds__(256) void pattern_p(uint4* __restrict__ buf, uint4*
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+
+// IMIX descriptor windows: 4 lanes per packet read its 64-B window at off[p] (64-B aligned,
+// scattered over ~375 MB); MODE 0 read, 1 in-place full-window nt rewrite, 2 + dense 12 B/pkt out
+template <int MODE>
+__global__ __launch_bounds__(256) void windows(uint8_t* __restrict__ buf, const uint32_t* __restrict__ off,
+                                               uint8_t* __restrict__ dst, uint32_t* sink, uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, part = lane & 3u, quad = lane >> 2;
+  const uint32_t wbase = blockIdx.x * 256u + wave * 64u;
+  const uint32_t own = wbase + lane < n ? off[wbase + lane] : 0u;
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t o = static_cast<uint32_t>(__shfl(static_cast<int>(own), k * 16 + quad));
+    v[k] = *reinterpret_cast<const uint4*>(buf + o + part * 16u);
+  }
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    const uint32_t o = static_cast<uint32_t>(__shfl(static_cast<int>(own), k * 16 + quad));
+    if (MODE == 1) nt_store(reinterpret_cast<uint4*>(buf + o + part * 16u), make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+    if (MODE == 2 && part == 0u) {
+      uint32_t* m = reinterpret_cast<uint32_t*>(dst + static_cast<size_t>(wbase + k * 16 + quad) * 12u);
+      m[0] = v[k].y; m[1] = v[k].x; m[2] = v[k].z;
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 template <typename F>
 float time_it(F f, int iters) {
   hipEvent_t a, b;
@@ -134,6 +163,38 @@ int main() {
     RUN(4, 3, "copy U4", B, B);
     RUN(8, 3, "copy U8", B, B);
     std::printf("--\n");
+  }
+  {
+    // IMIX 7:4:1 of 60/572/1496-B frames at 64-B aligned offsets (tools/ mirror of tracegen mode 1)
+    const uint32_t n = 1u << 20;
+    std::vector<uint32_t> off(n);
+    uint64_t x = 0x1234567ull, pos = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      x = x * 6364136223846793005ull + 1442695040888963407ull;
+      const uint32_t r = static_cast<uint32_t>(x >> 33) % 12u;
+      const uint32_t len = r < 7 ? 60 : (r < 11 ? 572 : 1496);
+      off[i] = static_cast<uint32_t>(pos);
+      pos += (len + 63) & ~63u;
+    }
+    std::vector<uint8_t*> ib(kBufs);
+    for (auto& p : ib) {
+      CK(hipMalloc(&p, pos + 64));
+      CK(hipMemset(p, 1, pos + 64));
+    }
+    uint32_t* d_off;
+    CK(hipMalloc(&d_off, n * 4ull));
+    CK(hipMemcpy(d_off, off.data(), n * 4ull, hipMemcpyHostToDevice));
+    uint8_t* mo;
+    CK(hipMalloc(&mo, n * 12ull));
+    const int grid = static_cast<int>(n / 256);
+    const double W = 64.0 * n, D = 4.0 * n;
+    std::printf("IMIX buffer %.1f MB, 1M windows\n", pos / 1e6);
+    float us = time_it([&](int i) { windows<0><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    report("imix windows read", us, W + D, 0);
+    us = time_it([&](int i) { windows<1><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    report("imix windows rw nt (in place)", us, W + D, W);
+    us = time_it([&](int i) { windows<2><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    report("imix windows read + 12B/pkt out", us, W + D, 12.0 * n);
   }
   return 0;
 }
