@@ -135,9 +135,54 @@ int nbg_maglev_check(nbg_maglev* h);
 int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                              uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out);
 
+
+/* ---- chained NF: test/lpm -> test/maglev (BASELINE config C5) ------------- */
+
+typedef struct nbg_lpm nbg_lpm;
+
+#define NBG_LPM_TBL24_SIZE ((1u << 24) + 1u) /* TBL24_SIZE, test/lpm/src/nf.rs:19 */
+
+/* IPLookup::new + insert(prefix, len, gate) per route + construct_table
+ * (test/lpm/src/nf.rs:24-86), uploaded to `device` (tbl24: 32 MiB; tbl_long: the used blocks).
+ * prefixes are host-order u32 (u32::from(Ipv4Addr), nf.rs:41); lens in [0, 32].  A later route
+ * with the same (prefix, len) replaces an earlier one (HashMap::insert, nf.rs:46).  Routes of
+ * one length are applied in ascending prefix order (the reference iterates a HashMap: see
+ * DESIGN.md).  NBG_EINVAL where the reference would panic (a fill past the end of a table). */
+int nbg_lpm_create(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gates, uint64_t n, int device,
+                   nbg_lpm** out);
+void nbg_lpm_destroy(nbg_lpm* t);
+
+/* IPLookup::lookup_entry (nf.rs:88-98) for n host-order IPv4 addresses in HBM -> u16 gates. */
+int nbg_lpm_lookup_device(nbg_lpm* t, const uint32_t* d_ips, uint64_t n, uint16_t* d_gate, void* stream);
+
+/*
+ * The chain `lpm(ReceiveBatch) -> maglev(...)`: per packet, test/lpm's pipeline
+ * (parse::<MacHeader> -> transform(swap_addresses) -> parse::<IpHeader> ->
+ * group_by(lpm_groups, lookup_entry(src)), test/lpm/src/nf.rs:212-228) and then test/maglev's
+ * (nf.rs:92-106), fused in one kernel pass.  The two MAC swaps cancel, so packet bytes are
+ * only read.  Outputs:
+ *   d_gate     n_pkts u16: lookup_entry(ip.src), or NBG_SENTINEL when lpm cannot parse the
+ *              packet (data_len < 14 + 20: the parse_header asserts, interface/packet.rs:392-399)
+ *   d_backend  n_pkts u16: the Maglev backend, or NBG_SENTINEL when either NF would panic
+ *              (lpm: unparseable or gate >= lpm_groups, the group index panic of
+ *              operators/group_by.rs:48; maglev: as nbg_maglev_classify_device)
+ *   d_perm / d_counts  grouped by backend as nbg_maglev_classify_device (input order inside a
+ *              group; the reference's cross-group merge order after lpm is scheduler-defined)
+ * flags: NBG_OWNED_WINDOWS | NBG_DEFER_GROUP (NBG_SWAP_MACS is ignored: the swaps cancel).
+ */
+int nbg_chain_lpm_maglev_device(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_groups, uint8_t* d_pkts,
+                                const uint32_t* d_off, const uint16_t* d_len, uint32_t stride, uint16_t fixed_len,
+                                uint64_t n_pkts, uint32_t flags, uint16_t* d_gate, uint16_t* d_backend,
+                                uint32_t* d_perm, uint32_t* d_counts, void* stream);
+
 const char* nbg_last_error(void);
 
 /* ---- host-only helpers (no GPU needed) ---------------------------------- */
+
+/* The product's own LPM builder (what nbg_lpm_create uploads), for tests: tbl24 has
+ * NBG_LPM_TBL24_SIZE entries; tbl_long receives *long_used (<= long_cap) entries. */
+int nbg_lpm_build_host(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gates, uint64_t n,
+                       uint16_t* tbl24, uint16_t* tbl_long, uint64_t long_cap, uint64_t* long_used);
 
 /* The product's own LUT builder (what nbg_maglev_create uploads), for tests. */
 int nbg_lut_build_host(const char* const* names, const uint32_t* name_lens, uint32_t n_backends,

@@ -20,6 +20,7 @@ NBG_OWNED_WINDOWS = 0x4
 NBG_WB_PARTIAL = 0x8
 NBG_DEFER_GROUP = 0x10
 NBG_TRACE_UNIQUE = 0x1
+NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
 # every symbol include/nbgpu.h declares: name -> (restype, argtypes)
 _P = C.c_void_p
@@ -39,7 +40,13 @@ SIGNATURES = {
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
+    "nbg_lpm_create": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P)]),
+    "nbg_lpm_destroy": (None, [_P]),
+    "nbg_lpm_lookup_device": (C.c_int, [_P, _P, C.c_uint64, _P, _P]),
+    "nbg_chain_lpm_maglev_device": (C.c_int, [_P, _P, C.c_uint32, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64,
+                                              C.c_uint32, _P, _P, _P, _P, _P]),
     "nbg_last_error": (C.c_char_p, []),
+    "nbg_lpm_build_host": (C.c_int, [_P, _P, _P, C.c_uint64, _P, _P, C.c_uint64, C.POINTER(C.c_uint64)]),
     "nbg_lut_build_host": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_uint64, _P]),
     "nbg_trace_layout": (C.c_uint64, [C.c_uint64, C.c_int, C.c_uint64, _P, _P]),
     "nbg_trace_fill": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32]),

@@ -95,12 +95,29 @@ __device__ __forceinline__ uint32_t lookup(const ClassifyArgs& a, const uint8_t*
   return lut_get<LUTM>(a, lut_lds, idx);
 }
 
-// Byte-wise path: any alignment, any length, any IHL.  Returns the bin (nb = sentinel).
-template <int LUTM, bool F4>
+// DIR-24-8 lookup_entry (test/lpm/src/nf.rs:88-98) of a host-order IPv4 address.
+__device__ __forceinline__ uint32_t lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, uint32_t ip) {
+  const uint32_t t = tbl24[ip >> 8];
+  return (t & 0x8000u) ? tbl_long[((t & 0x7fffu) << 8) + (ip & 0xffu)] : t;
+}
+
+// Byte-wise path: any alignment, any length, any IHL.  Returns the bin (nb = sentinel);
+// CHAIN also sets the lpm gate (sentinel when test/lpm cannot parse the packet).
+template <int LUTM, bool F4, bool CHAIN>
 __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const uint8_t* lut_lds, uint8_t* p,
-                                                  uint32_t len, uint32_t pkt) {
+                                                  uint32_t len, uint32_t pkt, uint32_t& gate) {
+  gate = kSentinel;
   if (len < kEth) return a.nb;  // Packet::parse_header assert (interface/packet.rs:392-399)
-  if (a.swap) {                 // transform runs before group_by over the batch
+  const uint8_t* q = p + kEth;
+  const uint32_t plen = len - kEth;
+  if constexpr (CHAIN) {
+    // test/lpm: parse::<IpHeader> asserts payload_size >= 20 (packet.rs:392-399, ip.rs:53-56);
+    // the gate is the group index of its group_by(lpm_groups) (test/lpm/src/nf.rs:216-221)
+    if (plen < 20) return a.nb;
+    const uint32_t ip = (static_cast<uint32_t>(q[12]) << 24) | (q[13] << 16) | (q[14] << 8) | q[15];
+    gate = lpm_lookup(a.tbl24, a.tbl_long, ip);
+    if (gate >= a.lpm_groups) return a.nb;
+  } else if (a.swap) {  // transform runs before group_by over the batch (chain: two swaps cancel)
     uint8_t* o = a.mac_out ? a.mac_out + static_cast<size_t>(pkt) * 12u : p;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -109,8 +126,6 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
       o[k + 6] = d;
     }
   }
-  const uint8_t* q = p + kEth;
-  const uint32_t plen = len - kEth;
   if (plen < 20) return a.nb;  // slice OOB in ipv4_extract_flow
   const uint32_t ps = (q[0] & 0xfu) * 4u;
   if (plen < ps + 4) return a.nb;
@@ -133,7 +148,7 @@ __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
 
 // ABL (diagnostic builds only, selected by NBG_ABL): 0 = full kernel; 1 = no hash/LUT (bin from a
 // header byte); 2 = also no LDS transpose (loads + backend store only).
-template <int LUTM, bool F4, bool HIST, int R, int ABL = 0, int NT = kBlock>
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int R, int ABL = 0, int NT = kBlock>
 __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr uint32_t kT = NT * R;  // packets per tile
@@ -207,9 +222,13 @@ __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
     }
 
     // ---- phase B: per round, transpose + swap + hash, and ISSUE the LUT gather (consumed in C)
-    uint32_t bin[R];
+    uint32_t bin[R], gate[R], iplo[R];
+    bool resolve[R];  // CHAIN fast path: gate[] holds the raw tbl24 entry until phase C
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+      gate[r] = kSentinel;
+      iplo[r] = 0;
+      resolve[r] = false;
       const uint32_t rbase = wbase + r * 64u;
       const uint32_t p_own = rbase + lane;
       if constexpr (ABL == 2) {
@@ -279,11 +298,17 @@ __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
             bin[r] = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
           } else {
             uint32_t lo, hi;
+            if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
+              const uint32_t ip = __builtin_bswap32(src);
+              gate[r] = a.tbl24[ip >> 8];
+              iplo[r] = ip & 0xffu;
+              resolve[r] = true;
+            }
             fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-            bin[r] = lookup<LUTM, F4>(a, lut_lds, lo, hi);  // gather issued; first use in phase C
+            bin[r] = lookup<LUTM, F4>(a, lut_lds, lo, hi);  // gathers issued; first use in phase C
           }
         } else {
-          bin[r] = classify_slow<LUTM, F4>(a, lut_lds, pown, len_own[r], p_own);
+          bin[r] = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, len_own[r], p_own, gate[r]);
         }
       }
     }
@@ -293,6 +318,11 @@ __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
     for (int r = 0; r < R; ++r) {
       const uint32_t p_own = wbase + r * 64u + lane;
       if (p_own < a.n_pkts) {
+        if constexpr (CHAIN) {
+          if (resolve[r] && (gate[r] & 0x8000u)) gate[r] = a.tbl_long[((gate[r] & 0x7fffu) << 8) + iplo[r]];
+          a.gate[p_own] = static_cast<uint16_t>(gate[r]);
+          if (gate[r] >= a.lpm_groups) bin[r] = a.nb;  // test/lpm would panic: never reaches maglev
+        }
         a.backend[p_own] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
         if constexpr (HIST) atomicAdd(&hist[bin[r]], 1u);
       }
@@ -596,50 +626,45 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 #endif
 }
 
-template <int LUTM, bool F4, bool HIST, int R>
+template <int LUTM, bool F4, bool HIST, bool CHAIN>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   constexpr int NT = (LUTM == kLdsU8 || LUTM == kLdsU16) ? kLdsBlock : kBlock;
-  auto fn = classify_kernel<LUTM, F4, HIST, R, 0, NT>;
+  auto fn = classify_kernel<LUTM, F4, HIST, CHAIN, 1, 0, NT>;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 
-template <int LUTM, bool F4, bool HIST, int R, int ABL>
+template <int LUTM, bool F4, bool HIST, int ABL>
 int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, R, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, 1, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 
 template <int LUTM, bool F4, bool HIST>
-int launch_r(const ClassifyArgs& a, int rounds, int grid, size_t lds, hipStream_t s) {
+int launch_v(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
+  if (a.tbl24) return launch_one<LUTM, F4, HIST, true>(a, grid, lds, s);
   if constexpr (LUTM == kGlobalU8 && F4 && !HIST) {
     static const int abl = [] {
       const char* e = std::getenv("NBG_ABL");
       return e ? std::atoi(e) : 0;
     }();
-    if (abl == 1) return launch_abl<LUTM, F4, HIST, 1, 1>(a, grid, lds, s);
-    if (abl == 2) return launch_abl<LUTM, F4, HIST, 1, 2>(a, grid, lds, s);
-    if (abl == 3) return launch_abl<LUTM, F4, HIST, 1, 3>(a, grid, lds, s);
-    if (abl == 4) return launch_abl<LUTM, F4, HIST, 1, 4>(a, grid, lds, s);
+    if (abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
+    if (abl == 2) return launch_abl<LUTM, F4, HIST, 2>(a, grid, lds, s);
+    if (abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
+    if (abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
   }
-  switch (rounds) {
-    case 1: return launch_one<LUTM, F4, HIST, 1>(a, grid, lds, s);
-    case 2: return launch_one<LUTM, F4, HIST, 2>(a, grid, lds, s);
-    default: return launch_one<LUTM, F4, HIST, 4>(a, grid, lds, s);
-  }
+  return launch_one<LUTM, F4, HIST, false>(a, grid, lds, s);
 }
 
 template <int LUTM>
-int launch_mode(const ClassifyArgs& a, bool hist, int rounds, int grid, size_t lds, hipStream_t s) {
+int launch_mode(const ClassifyArgs& a, bool hist, int grid, size_t lds, hipStream_t s) {
   if (a.m == 65537u)
-    return hist ? launch_r<LUTM, true, true>(a, rounds, grid, lds, s)
-                : launch_r<LUTM, true, false>(a, rounds, grid, lds, s);
-  return hist ? launch_r<LUTM, false, true>(a, rounds, grid, lds, s)
-              : launch_r<LUTM, false, false>(a, rounds, grid, lds, s);
+    return hist ? launch_v<LUTM, true, true>(a, grid, lds, s) : launch_v<LUTM, true, false>(a, grid, lds, s);
+  return hist ? launch_v<LUTM, false, true>(a, grid, lds, s) : launch_v<LUTM, false, false>(a, grid, lds, s);
 }
 
 size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
@@ -649,15 +674,31 @@ size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
 
 }  // namespace
 
-int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int rounds, int grid, void* stream) {
+int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;
   const size_t lds = classify_lds(a.nb, lds_lut ? a.lut_lds_bytes : 0);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (lds_lut)
-    return wide_lut ? launch_mode<kLdsU16>(a, hist, rounds, grid, lds, s)
-                    : launch_mode<kLdsU8>(a, hist, rounds, grid, lds, s);
-  return wide_lut ? launch_mode<kGlobalU16>(a, hist, rounds, grid, lds, s)
-                  : launch_mode<kGlobalU8>(a, hist, rounds, grid, lds, s);
+    return wide_lut ? launch_mode<kLdsU16>(a, hist, grid, lds, s) : launch_mode<kLdsU8>(a, hist, grid, lds, s);
+  return wide_lut ? launch_mode<kGlobalU16>(a, hist, grid, lds, s) : launch_mode<kGlobalU8>(a, hist, grid, lds, s);
+}
+
+__global__ __launch_bounds__(kBlock) void lpm_lookup_kernel(const uint16_t* __restrict__ tbl24,
+                                                            const uint16_t* __restrict__ tbl_long,
+                                                            const uint32_t* __restrict__ ips, uint32_t n,
+                                                            uint16_t* __restrict__ gate) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) gate[i] = static_cast<uint16_t>(lpm_lookup(tbl24, tbl_long, ips[i]));
+}
+
+int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
+                      uint16_t* gate, void* stream) {
+  const uint32_t grid = static_cast<uint32_t>((n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(lpm_lookup_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), tbl24,
+                     tbl_long, ips, static_cast<uint32_t>(n), gate);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "lpm lookup launch: %s", hipGetErrorString(e));
+  return NBG_OK;
 }
 
 int launch_scan(const ScanArgs& a, void* stream) {

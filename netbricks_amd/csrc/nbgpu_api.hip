@@ -39,6 +39,13 @@ using namespace nbg;
     if (e_ != hipSuccess) return set_error(NBG_EIO, "%s: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
+struct nbg_lpm {
+  int device = 0;
+  uint16_t* d_tbl24 = nullptr;     // NBG_LPM_TBL24_SIZE entries
+  uint16_t* d_tbl_long = nullptr;  // the used 256-entry blocks (at least one entry)
+  uint64_t long_used = 0;
+};
+
 struct nbg_maglev {
   int device = 0;
   uint32_t nb = 0;
@@ -53,7 +60,6 @@ struct nbg_maglev {
   uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
   uint32_t parity = 0;
   uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
-  int rounds = 1;                     // classify rounds of 64 packets per wave per tile
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
   bool pending = false;
   int pending_scan_mode = 0;
@@ -139,7 +145,6 @@ int upload(nbg_maglev* h) {
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
-  if (const char* e = std::getenv("NBG_ROUNDS")) h->rounds = std::atoi(e) >= 4 ? 4 : (std::atoi(e) >= 2 ? 2 : 1);
   int rc = classify_grid(true, h->lut_bytes, h->nb, h->device, &h->grid_lds);
   if (rc) return rc;
   return classify_grid(false, 0, h->nb, h->device, &h->grid_global);
@@ -247,10 +252,15 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
                                        d_counts, nullptr, stream);
 }
 
-int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
-                                  uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
-                                  uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
-                                  void* stream) {
+}  // extern "C"
+
+namespace {
+
+// One classify (+ grouping) launch; `lpm` non-null runs the chained test/lpm stage first.
+int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len, uint32_t stride,
+                    uint16_t fixed_len, uint64_t n_pkts, uint32_t flags, uint16_t* d_backend, uint32_t* d_perm,
+                    uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
+                    uint16_t* d_gate, void* stream) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
   if (h->pending) return set_error(NBG_EINVAL, "classify: a deferred group is pending (nbg_maglev_finish_group)");
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify: n_pkts must be < 2^30");
@@ -259,6 +269,8 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
     return NBG_OK;
   }
   if (!d_pkts || !d_backend) return set_error(NBG_EINVAL, "classify: null packet or backend buffer");
+  if (lpm && (!d_gate || lpm->device != h->device))
+    return set_error(NBG_EINVAL, "chain: null gate buffer, or lpm and maglev handles on different devices");
   if (!d_off && stride == 0) return set_error(NBG_EINVAL, "classify: stride 0 without offsets");
   if (!d_off && static_cast<unsigned __int128>(n_pkts) * stride > (1ull << 40))
     return set_error(NBG_EINVAL, "classify: batch too large");
@@ -268,7 +280,7 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   if (group && nbins > kMaxGroupBins)
     return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
   const bool lds = use_lds_lut(h, flags);
-  const uint32_t hist_tile = (lds ? kLdsBlock : kBlock) * h->rounds;
+  const uint32_t hist_tile = lds ? kLdsBlock : kBlock;
   const uint32_t n_tiles = static_cast<uint32_t>((n_pkts + hist_tile - 1) / hist_tile);
   // LDS-staged LUT: persistent resident grid; L2 LUT: one tile per block
   const int grid = lds ? std::min<int>(h->grid_lds, static_cast<int>(n_tiles)) : static_cast<int>(n_tiles);
@@ -291,7 +303,7 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   a.lut_lds_bytes = lds ? h->lut_bytes : 0;
   a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
   a.nb = h->nb;
-  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  a.swap = (flags & NBG_SWAP_MACS) && !lpm ? 1u : 0u;  // chain: lpm's and maglev's swaps cancel
   // a 64-B window per packet start is owned: fixed slots of >= 64 B, or the caller says so
   a.win_owned = (!d_off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
   a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
@@ -299,7 +311,14 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   a.mac_out = d_mac_out;
   a.part_hist = group ? part_cur : nullptr;
   a.part_pkts = part_pkts;
-  int rc = launch_classify(a, h->wide, lds, h->rounds, grid, stream);
+  if (lpm) {
+    a.tbl24 = lpm->d_tbl24;
+    a.tbl_long = lpm->d_tbl_long;
+    a.lpm_groups = lpm_groups;
+    a.gate = d_gate;
+    a.mac_out = nullptr;
+  }
+  int rc = launch_classify(a, h->wide, lds, grid, stream);
   if (rc) return rc;
   if (group) {
     const int scan = pick_group_scan(nbins, n_parts);
@@ -338,6 +357,74 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
   }
   h->last_stream = static_cast<hipStream_t>(stream);
   return NBG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
+                                  uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
+                                  uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
+                                  void* stream) {
+  return classify_common(h, d_pkts, d_off, d_len, stride, fixed_len, n_pkts, flags, d_backend, d_perm, d_counts,
+                         d_mac_out, nullptr, 0, nullptr, stream);
+}
+
+int nbg_chain_lpm_maglev_device(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_groups, uint8_t* d_pkts,
+                                const uint32_t* d_off, const uint16_t* d_len, uint32_t stride, uint16_t fixed_len,
+                                uint64_t n_pkts, uint32_t flags, uint16_t* d_gate, uint16_t* d_backend,
+                                uint32_t* d_perm, uint32_t* d_counts, void* stream) {
+  if (!lpm) return set_error(NBG_EINVAL, "chain: null lpm handle");
+  return classify_common(mg, d_pkts, d_off, d_len, stride, fixed_len, n_pkts, flags & ~NBG_SWAP_MACS, d_backend,
+                         d_perm, d_counts, nullptr, lpm, lpm_groups, d_gate, stream);
+}
+
+int nbg_lpm_create(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gates, uint64_t n, int device,
+                   nbg_lpm** out) {
+  if (!out || ((!prefixes || !lens || !gates) && n)) return set_error(NBG_EINVAL, "nbg_lpm_create: null argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_error(NBG_ENODEV, "no HIP device available (the LPM path has no CPU fallback)");
+  if (device < 0 || device >= ndev) return set_error(NBG_ENODEV, "device %d out of range (%d devices)", device, ndev);
+  std::vector<uint16_t> t24, tl;
+  uint64_t used = 0;
+  int rc = build_lpm(prefixes, lens, gates, n, t24, tl, used);
+  if (rc) return rc;
+  nbg_lpm* t = new (std::nothrow) nbg_lpm();
+  if (!t) return set_error(NBG_ENOMEM, "out of host memory");
+  t->device = device;
+  t->long_used = used;
+  DeviceGuard g(device);
+  const uint64_t nl = used ? used : 1;
+  if (hipMalloc(&t->d_tbl24, t24.size() * 2) != hipSuccess || hipMalloc(&t->d_tbl_long, nl * 2) != hipSuccess ||
+      hipMemcpy(t->d_tbl24, t24.data(), t24.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(t->d_tbl_long, tl.data(), nl * 2, hipMemcpyHostToDevice) != hipSuccess) {
+    nbg_lpm_destroy(t);
+    return set_error(NBG_ENOMEM, "nbg_lpm_create: device allocation/upload failed");
+  }
+  *out = t;
+  return NBG_OK;
+}
+
+void nbg_lpm_destroy(nbg_lpm* t) {
+  if (!t) return;
+  {
+    DeviceGuard g(t->device);
+    (void)hipFree(t->d_tbl24);
+    (void)hipFree(t->d_tbl_long);
+  }
+  delete t;
+}
+
+int nbg_lpm_lookup_device(nbg_lpm* t, const uint32_t* d_ips, uint64_t n, uint16_t* d_gate, void* stream) {
+  if (!t) return set_error(NBG_EINVAL, "lpm lookup: null handle");
+  if (n == 0) return NBG_OK;
+  if (!d_ips || !d_gate) return set_error(NBG_EINVAL, "lpm lookup: null buffer");
+  if (n >= (1ull << 32)) return set_error(NBG_EINVAL, "lpm lookup: n must be < 2^32");
+  DeviceGuard g(t->device);
+  return launch_lpm_lookup(t->d_tbl24, t->d_tbl_long, d_ips, n, d_gate, stream);
 }
 
 int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {

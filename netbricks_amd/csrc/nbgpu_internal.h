@@ -15,6 +15,8 @@ int set_error(int code, const char* fmt, ...);
 uint64_t fnv1a64(const uint8_t* p, size_t n);
 uint64_t xxh64(const uint8_t* p, size_t n, uint64_t seed);
 int build_lut(const char* const* names, const uint32_t* lens, uint32_t n, uint64_t m, std::vector<uint32_t>& entry);
+int build_lpm(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gates, uint64_t n,
+              std::vector<uint16_t>& tbl24, std::vector<uint16_t>& tbl_long, uint64_t& long_used);
 
 // Kernel geometry.
 constexpr int kBlock = 256;          // classify threads per workgroup (4 waves), L2-gather LUT
@@ -46,6 +48,11 @@ struct ClassifyArgs {
   uint8_t* mac_out;         // nullable: dense 12-B swapped-MAC records instead of in-place swap
   uint32_t* part_hist;      // nullable: [n_parts][nb+1] partition histograms (pre-zeroed)
   uint32_t part_pkts;       // packets per partition
+  // chained test/lpm stage (nbg_chain_lpm_maglev_device); tbl24 == nullptr: Maglev alone
+  const uint16_t* tbl24;
+  const uint16_t* tbl_long;
+  uint32_t lpm_groups;
+  uint16_t* gate;
 };
 
 struct ScanArgs {
@@ -77,8 +84,10 @@ struct GroupArgs {
 enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
 
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
-int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int rounds, int grid, void* stream);
+int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
 int launch_scan(const ScanArgs& a, void* stream);
+int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
+                      uint16_t* gate, void* stream);
 int launch_group(const GroupArgs& a, int scan, void* stream);
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan);
 int pick_group_scan(uint32_t nbins, uint32_t n_parts);

@@ -354,3 +354,94 @@ double orc_cpu_baseline(uint8_t *buf, const uint64_t *offs, uint64_t stride, con
     free(tid);
     return worst;
 }
+
+
+/* ---- test/lpm (chained before test/maglev, config C5) ------------------------------
+ * IPLookup::construct_table (test/lpm/src/nf.rs:49-86) over routes given as arrays;
+ * one length's routes are applied in ascending prefix order (see maglev_ref.IPLookup).
+ * tbl24 and tbl_long have ORC_TBL24 entries each.  Returns 0, or -34 where the reference
+ * panics (a fill past a table's end, prefix length > 32). */
+#define ORC_TBL24 ((1u << 24) + 1u)
+
+typedef struct { uint32_t k; uint16_t v; uint64_t seq; } orc_route;
+
+static int route_cmp(const void *a, const void *b) {
+    const orc_route *x = (const orc_route *)a, *y = (const orc_route *)b;
+    if (x->k != y->k) return x->k < y->k ? -1 : 1;
+    return x->seq < y->seq ? -1 : (x->seq > y->seq);
+}
+
+int orc_lpm_build(const uint32_t *prefixes, const uint8_t *lens, const uint16_t *gates, uint64_t n,
+                  uint16_t *tbl24, uint16_t *tbl_long, uint64_t *long_used) {
+    memset(tbl24, 0, ORC_TBL24 * sizeof(uint16_t));
+    memset(tbl_long, 0, ORC_TBL24 * sizeof(uint16_t));
+    uint64_t cur = 0;
+    for (uint32_t len = 0; len <= 32; len++) {
+        uint64_t cnt = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            if (lens[i] > 32) return -34;
+            cnt += lens[i] == len;
+        }
+        if (!cnt) continue;
+        orc_route *r = (orc_route *)malloc(cnt * sizeof(orc_route));
+        uint64_t c = 0;
+        for (uint64_t i = 0; i < n; i++)
+            if (lens[i] == len) { r[c].k = prefixes[i]; r[c].v = gates[i]; r[c].seq = i; c++; }
+        qsort(r, cnt, sizeof(orc_route), route_cmp);
+        for (uint64_t i = 0; i < cnt; i++) {
+            if (i + 1 < cnt && r[i + 1].k == r[i].k) continue; /* HashMap::insert: the last one wins */
+            const uint32_t k = r[i].k;
+            const uint16_t v = r[i].v;
+            if (len <= 24) {
+                uint64_t start = k >> 8, end = start + (1ull << (24 - len));
+                if (end > ORC_TBL24) { free(r); return -34; }
+                for (uint64_t p = start; p < end; p++) tbl24[p] = v;
+            } else {
+                uint16_t t24 = tbl24[k >> 8];
+                if (!(t24 & 0x8000)) {
+                    if (cur + 256 > ORC_TBL24) { free(r); return -34; }
+                    uint64_t start = cur + (k & 0xff), end = start + (1ull << (32 - len));
+                    for (uint64_t j = cur; j < cur + 256; j++) tbl_long[j] = (j < start || j >= end) ? t24 : v;
+                    tbl24[k >> 8] = (uint16_t)((uint16_t)(cur >> 8) | 0x8000);
+                    cur += 256;
+                } else {
+                    uint64_t start = ((uint64_t)(t24 & 0x7fff) << 8) + (k & 0xff), end = start + (1ull << (32 - len));
+                    if (end > ORC_TBL24) { free(r); return -34; }
+                    for (uint64_t j = start; j < end; j++) tbl_long[j] = v;
+                }
+            }
+        }
+        free(r);
+    }
+    *long_used = cur;
+    return 0;
+}
+
+static inline uint16_t lpm_lookup(const uint16_t *tbl24, const uint16_t *tbl_long, uint32_t ip) {
+    uint16_t t = tbl24[ip >> 8];
+    return (t & 0x8000) ? tbl_long[((uint32_t)(t & 0x7fff) << 8) + (ip & 0xff)] : t;
+}
+
+void orc_lpm_lookup(const uint16_t *tbl24, const uint16_t *tbl_long, const uint32_t *ips, uint64_t n, uint16_t *gate) {
+    for (uint64_t i = 0; i < n; i++) gate[i] = lpm_lookup(tbl24, tbl_long, ips[i]);
+}
+
+/* lpm() -> maglev() per packet (test/lpm/src/nf.rs:212-228, test/maglev/src/nf.rs:92-106);
+ * the two MAC swaps cancel, so `buf` is only read. */
+void orc_chain_classify(const uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
+                        uint32_t fixed_len, uint64_t n, const uint16_t *tbl24, const uint16_t *tbl_long,
+                        uint32_t lpm_groups, const uint32_t *lut, uint64_t m, uint16_t *gate, uint16_t *backend) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint8_t *f = buf + pkt_off(offs, stride, i);
+        uint32_t len = pkt_len(lens, fixed_len, i);
+        gate[i] = ORC_SENTINEL;
+        backend[i] = ORC_SENTINEL;
+        if (len < ORC_ETH + 20) continue; /* parse::<MacHeader>, parse::<IpHeader> asserts */
+        const uint8_t *ip = f + ORC_ETH;
+        uint32_t src = (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15];
+        gate[i] = lpm_lookup(tbl24, tbl_long, src);
+        if (gate[i] >= lpm_groups) continue; /* group index out of range: the reference panics */
+        uint64_t h;
+        if (flow_hash_of(f, len, &h)) backend[i] = (uint16_t)lut[h % m];
+    }
+}

@@ -20,6 +20,10 @@ Restated reference items (paths relative to the NetBricks repo root):
 * `Packet::parse_header` / `get_payload` / `payload_size`
                                   framework/src/interface/packet.rs:258-260,392-399,467-472
 * GroupBy producer FIFO semantics framework/src/operators/group_by.rs:43-55
+* `IPLookup` (DIR-24-8) insert / construct_table / lookup_entry
+                                  test/lpm/src/nf.rs:12-99
+* `lpm()` pipeline (parse, swap, parse::<IpHeader>, group_by(3, lookup(src)))
+                                  test/lpm/src/nf.rs:212-228; IpHeader size 20 headers/ip.rs:53-56
 
 Third-party arithmetic (un-vendored crates, unpinned `"*"` in the reference):
 * `fnv` crate `FnvHasher`: FNV-1a 64, offset 0xcbf29ce484222325, prime 0x100000001b3.
@@ -150,3 +154,86 @@ def group_perm(backends: list[int], n_backends: int):
         counts[b] += 1
     perm = sorted(range(len(bins)), key=lambda i: (bins[i], i))
     return perm, counts
+
+
+# ---- test/lpm (chained before test/maglev in BASELINE config C5) -------------------------
+
+TBL24_SIZE = (1 << 24) + 1   # nf.rs:19
+RAW_SIZE = 33                # nf.rs:20
+OVERFLOW_MASK = 0x8000       # nf.rs:21
+IP_HDR = 20                  # IpHeader::size() (headers/ip.rs:53-56)
+
+
+class IPLookup:
+    """test/lpm/src/nf.rs:12-99.  raw_entries[len] maps prefix -> gate (HashMap::insert
+    replaces).  construct_table visits one length's routes in ascending prefix order: the
+    reference iterates a HashMap, whose order only matters when routes of one length overlap
+    with different gates (never for masked prefixes) — the product uses the same rule."""
+
+    def __init__(self):
+        import numpy as np
+        self.tbl24 = np.zeros(TBL24_SIZE, dtype=np.uint16)
+        self.tbl_long = np.zeros(TBL24_SIZE, dtype=np.uint16)
+        self.current_tbl_long = 0
+        self.raw_entries = [dict() for _ in range(RAW_SIZE)]
+
+    def insert(self, ip: int, plen: int, gate: int) -> None:
+        if plen >= RAW_SIZE:
+            raise IndexError("prefix length > 32 (the reference panics)")
+        self.raw_entries[plen][ip & 0xFFFFFFFF] = gate & 0xFFFF
+
+    def construct_table(self) -> None:
+        for i in range(25):
+            for k in sorted(self.raw_entries[i]):
+                v = self.raw_entries[i][k]
+                start = k >> 8
+                end = start + (1 << (24 - i))
+                if end > TBL24_SIZE:
+                    raise IndexError("tbl24 fill past its end (the reference panics)")
+                self.tbl24[start:end] = v
+        for i in range(25, RAW_SIZE):
+            for k in sorted(self.raw_entries[i]):
+                v = self.raw_entries[i][k]
+                addr = k
+                t24entry = int(self.tbl24[addr >> 8])
+                if t24entry & OVERFLOW_MASK == 0:
+                    ctlb = self.current_tbl_long
+                    if ctlb + 256 > TBL24_SIZE:
+                        raise IndexError("tbl_long exhausted (the reference panics)")
+                    start = ctlb + (addr & 0xFF)
+                    end = start + (1 << (32 - i))
+                    for j in range(ctlb, ctlb + 256):
+                        self.tbl_long[j] = t24entry if (j < start or j >= end) else v
+                    self.tbl24[addr >> 8] = ((ctlb >> 8) & 0xFFFF) | OVERFLOW_MASK   # `as u16`
+                    self.current_tbl_long += 256
+                else:
+                    start = ((t24entry & ~OVERFLOW_MASK & 0xFFFF) << 8) + (addr & 0xFF)
+                    end = start + (1 << (32 - i))
+                    if end > TBL24_SIZE:
+                        raise IndexError("tbl_long fill past its end (the reference panics)")
+                    self.tbl_long[start:end] = v
+
+    def lookup_entry(self, ip: int) -> int:
+        t24entry = int(self.tbl24[ip >> 8])
+        if t24entry & OVERFLOW_MASK:
+            return int(self.tbl_long[((t24entry & ~OVERFLOW_MASK & 0xFFFF) << 8) + (ip & 0xFF)])
+        return t24entry
+
+
+def process_chain(frame: bytes, table: IPLookup, lut: list[int], lpm_groups: int = 3):
+    """One packet through lpm() then maglev() (frames are not modified: the swaps cancel).
+
+    Returns (gate, backend): gate = SENTINEL where lpm cannot parse the packet (data_len <
+    14 + 20: parse::<MacHeader>/parse::<IpHeader> asserts); backend = SENTINEL where either
+    NF would panic (also gate >= lpm_groups: group index out of range in group_by.rs:48).
+    """
+    if len(frame) < ETH_HDR + IP_HDR:
+        return SENTINEL, SENTINEL
+    src = struct.unpack(">I", bytes(frame[ETH_HDR + 12:ETH_HDR + 16]))[0]   # IpHeader::src (ip.rs:101-103)
+    gate = table.lookup_entry(src)
+    if gate >= lpm_groups:
+        return gate, SENTINEL
+    flow = extract_flow(bytes(frame[ETH_HDR:]))
+    if flow is None:
+        return gate, SENTINEL
+    return gate, lut[flow_hash(flow) % len(lut)]

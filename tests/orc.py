@@ -41,6 +41,13 @@ def lib():
         L.orc_cpu_baseline.restype = C.c_double
         L.orc_cpu_baseline.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, C.c_uint64, C.c_uint32,
                                        C.c_int, C.c_int, _P]
+        L.orc_lpm_build.restype = C.c_int
+        L.orc_lpm_build.argtypes = [_P, _P, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64)]
+        L.orc_lpm_lookup.restype = None
+        L.orc_lpm_lookup.argtypes = [_P, _P, _P, C.c_uint64, _P]
+        L.orc_chain_classify.restype = None
+        L.orc_chain_classify.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, _P, C.c_uint32, _P,
+                                         C.c_uint64, _P, _P]
         _lib = L
     return _lib
 
@@ -80,3 +87,52 @@ def flow_hash(frame: bytes):
     ok = C.c_int(0)
     h = lib().orc_flow_hash(b, len(frame), C.byref(ok))
     return h if ok.value else None
+
+
+TBL24 = (1 << 24) + 1
+
+
+def routes_arrays(routes):
+    """[(dotted-quad | int, len, gate)] -> (u32 prefixes, u8 lens, u16 gates)."""
+    pf, ln, gt = [], [], []
+    for ip, plen, gate in routes:
+        if isinstance(ip, str):
+            a = [int(x) for x in ip.split(".")]
+            ip = (a[0] << 24) | (a[1] << 16) | (a[2] << 8) | a[3]
+        pf.append(ip)
+        ln.append(plen)
+        gt.append(gate)
+    return (np.asarray(pf, dtype=np.uint32), np.asarray(ln, dtype=np.uint8), np.asarray(gt, dtype=np.uint16))
+
+
+def lpm_build(routes):
+    """-> (rc, tbl24 u16[2^24+1], tbl_long u16[used])"""
+    pf, ln, gt = routes_arrays(routes)
+    t24 = np.empty(TBL24, dtype=np.uint16)
+    tl = np.empty(TBL24, dtype=np.uint16)
+    used = C.c_uint64(0)
+    rc = lib().orc_lpm_build(pf.ctypes.data, ln.ctypes.data, gt.ctypes.data, pf.size, t24.ctypes.data,
+                             tl.ctypes.data, C.byref(used))
+    return rc, t24, tl[:used.value].copy()
+
+
+def lpm_lookup(t24, tl, ips):
+    ips = np.ascontiguousarray(ips, dtype=np.uint32)
+    tl = tl if tl.size else np.zeros(1, dtype=np.uint16)
+    out = np.empty(max(ips.size, 1), dtype=np.uint16)
+    lib().orc_lpm_lookup(t24.ctypes.data, tl.ctypes.data, ips.ctypes.data, ips.size, out.ctypes.data)
+    return out[:ips.size]
+
+
+def chain_classify(buf, n, t24, tl, lut, *, offs=None, stride=64, lens=None, fixed_len=60, lpm_groups=3):
+    """lpm() -> maglev(): (gate u16[n], backend u16[n]); `buf` is not modified."""
+    lut = np.ascontiguousarray(lut, dtype=np.uint32)
+    tl = tl if tl.size else np.zeros(1, dtype=np.uint16)
+    offs64 = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+    lens16 = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    gate = np.empty(max(n, 1), dtype=np.uint16)
+    be = np.empty(max(n, 1), dtype=np.uint16)
+    lib().orc_chain_classify(buf.ctypes.data, None if offs64 is None else offs64.ctypes.data, stride,
+                             None if lens16 is None else lens16.ctypes.data, fixed_len, n, t24.ctypes.data,
+                             tl.ctypes.data, lpm_groups, lut.ctypes.data, lut.size, gate.ctypes.data, be.ctypes.data)
+    return gate[:n], be[:n]
