@@ -103,6 +103,18 @@ def shared_lut(names, table, rank, world, device):
     return lut_t.cpu().numpy().astype(np.uint16)
 
 
+def scatter_shard(global_buf, out, rank: int, world: int) -> None:
+    """Config C4's data-path collective: rank 0 holds the whole batch (world contiguous shards)
+    and scatters shard r to rank r (RCCL ncclScatter over xGMI on GPUs; gloo in the CPU tests).
+    Shard-major order == global packet order, so per-shard grouping composes."""
+    import torch.distributed as dist
+
+    if rank == 0:
+        dist.scatter(out, list(global_buf.chunk(world)), src=0)
+    else:
+        dist.scatter(out, None, src=0)
+
+
 def read_traffic():
     """HBM bytes per classify launch from the committed PMC profile (profiles/pmc_*.json), if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
@@ -123,6 +135,8 @@ def main():
     ap.add_argument("--mac-record", action="store_true",
                     help="write the swapped MACs as dense 12-B egress records instead of in place")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--scatter-steps", type=int, default=50,
+                    help="N>1: steps of the scatter-inclusive pass (RCCL scatter from rank 0 + classify); 0 = skip")
     args = ap.parse_args()
 
     import torch
@@ -198,6 +212,45 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
 
+    # ---- C4 scatter-inclusive pass (N > 1): every step rank 0 scatters world x 1M packets over
+    #      xGMI and each rank classifies its shard; reported beside the device-resident value
+    scatter = None
+    if world > 1 and args.scatter_steps > 0:
+        try:
+            recv = torch.empty(BATCH * SLOT, dtype=torch.uint8, device=dev)
+            glob = torch.cat([dbufs[0]] + [torch.empty_like(dbufs[0]) for _ in range(world - 1)]) if rank == 0 else None
+            if rank == 0:
+                for r in range(1, world):  # rank 0 holds every rank's first shard (same seeds as the ranks own)
+                    buf_r, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(r, 0))
+                    glob[r * BATCH * SLOT:(r + 1) * BATCH * SLOT].copy_(torch.from_numpy(buf_r))
+            cur = torch.cuda.current_stream(dev).cuda_stream
+
+            def sstep():
+                scatter_shard(glob, recv, rank, world)
+                mgs[0].group_by(recv, BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True, stream=cur, **outs[0])
+
+            for _ in range(3):
+                sstep()
+            sync_all()
+            dist.barrier()
+            sync_all()
+            t1 = time.perf_counter()
+            for _ in range(args.scatter_steps):
+                sstep()
+            sync_all()
+            st_el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+            dist.all_reduce(st_el, op=dist.ReduceOp.MAX)
+            st_s = float(st_el[0])
+            scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
+                       "ms_per_step": round(st_s / args.scatter_steps * 1e3, 4), "steps": args.scatter_steps,
+                       "root_egress_GBps": round(BATCH * SLOT * (world - 1) * args.scatter_steps / st_s / 1e9, 1),
+                       "what": "rank 0 scatters world x 1M 64-B packets (ncclScatter over xGMI), each rank classifies "
+                               "its shard (MAC swap + grouping); single stream per rank"}
+            del recv, glob
+        except Exception as e:  # informational; the device-resident value above stands on its own
+            log(f"[rank {rank}] scatter-inclusive pass failed: {e}")
+            scatter = {"error": str(e)[:200]}
+
     # ---- roofline pass: classify kernel timed alone (single stream, events around each launch)
     st = streams[0]
     kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -258,6 +311,8 @@ def main():
                          "group_kernel_avg_us": round(group_ms.mean() * 1e3, 2)},
             "cpu_baseline": cpu,
         }
+        if scatter is not None:
+            line["scatter_inclusive"] = scatter
         print(json.dumps(line), flush=True)
     for m in mgs:
         m.close()

@@ -49,7 +49,13 @@ def _worker(rank, world, port, out):
     digest = torch.tensor([int(np.uint64(lut.astype(np.uint64).sum()))], dtype=torch.int64)
     all_d = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(all_d, digest)
-    out[rank] = {"lut_ok": np.array_equal(lut, nb.build_lut(names, bench.TABLE)),
+    # C4's scatter from rank 0: rank r receives exactly shard r of the global batch
+    glob = torch.from_numpy(np.concatenate([nb.make_trace(n, 0, seed=bench.shard_seed(r, 0))[0]
+                                            for r in range(world)])) if rank == 0 else None
+    recv = torch.empty(n * 64, dtype=torch.uint8)
+    bench.scatter_shard(glob, recv, rank, world)
+    scatter_ok = np.array_equal(recv.numpy(), buf)
+    out[rank] = {"lut_ok": np.array_equal(lut, nb.build_lut(names, bench.TABLE)), "scatter_ok": scatter_ok,
                  "same_lut": len({int(d) for d in all_d}) == 1, "counts": c.numpy().tolist(),
                  "first": buf[:64].tobytes()}
     dist.destroy_process_group()
@@ -67,7 +73,7 @@ def test_two_rank_shards_gloo():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    assert all(out[r]["lut_ok"] and out[r]["same_lut"] for r in range(world))
+    assert all(out[r]["lut_ok"] and out[r]["same_lut"] and out[r]["scatter_ok"] for r in range(world))
     assert out[0]["first"] != out[1]["first"]  # distinct shards
     # global reference: concatenate the shards and group once
     lut = nb.build_lut([f"backend-{i}" for i in range(bench.N_BACKENDS)], bench.TABLE)

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Throughput of the secondary BASELINE configs on one GPU (bench.py measures C2).
+
+  c3  Maglev 1000 backends / 655373-slot LUT (u16), IMIX 7:4:1 descriptors (u32 off + u16 len),
+      MAC swap in place (owned 64-B windows), per-backend grouping.
+      Algorithmic bytes/pkt: 64 window + 6 descriptor + 12 MAC + 2 backend + 4 perm = 88.
+  c5  chained test/lpm -> test/maglev (65 backends / 65537), IMIX descriptors, DIR-24-8 table of the
+      reference's 105 routes + the mixed route set (tests/golden/lpm_routes.json); the two MAC swaps
+      cancel, so packets are only read.  Bytes/pkt: 64 + 6 + 2 gate + 2 backend + 4 perm + 4 LPM = 82.
+
+Steps rotate over 8 distinct 1M-packet batches on --streams streams (one handle per stream), timed
+with events like bench.py; a single-stream pass times the classify kernel alone per launch.
+Prints one JSON line per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BATCH = 1 << 20
+N_BATCHES = 8
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3,c5")
+    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+
+    import netbricks_amd as nb
+
+    dev = torch.device("cuda:0")
+    routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
+    for cfg in args.config.split(","):
+        if cfg == "c3":
+            names, m, nbk = [f"be{i}" for i in range(1000)], 655373, 1000
+            bytes_pkt, classify_bytes = 88, 84
+        elif cfg == "c5":
+            names, m, nbk = [f"backend-{i}" for i in range(65)], 65537, 65
+            bytes_pkt, classify_bytes = 82, 78
+        else:
+            raise SystemExit(f"unknown config {cfg}")
+        t0 = time.time()
+        bufs, offs, lens = [], [], []
+        for b in range(N_BATCHES):
+            buf, off, ln = nb.make_trace(BATCH, 1, seed=1000 + b)
+            bufs.append(torch.from_numpy(buf).to(dev))
+            offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
+            lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
+        print(f"[{cfg}] traces in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        S = args.streams
+        mgs = [nb.Maglev(names, m) for _ in range(S)]
+        lpm = nb.Lpm(routes["reference"] + routes["mixed"]) if cfg == "c5" else None
+        sts = [torch.cuda.Stream(dev) for _ in range(S)]
+        outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                     perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                     counts=torch.empty(nbk + 1, dtype=torch.uint32, device=dev)) for _ in range(S)]
+        gates = [torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(S)]
+
+        def step(i, j=None, defer=False):
+            j = i % S if j is None else j
+            k = i % N_BATCHES
+            if cfg == "c5":
+                nb.chain_lpm_maglev(mgs[j], lpm, bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
+                                    defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream, **outs[j])
+            else:
+                mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, swap_macs=True,
+                                defer_group=defer, stream=sts[j].cuda_stream, **outs[j])
+
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(torch.cuda.current_stream(dev))
+        for st in sts:
+            st.wait_event(ev0)
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t_start
+        # classify kernel alone (single stream, events around each launch)
+        st = sts[0]
+        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for i in range(args.steps):
+            kev[i][0].record(st)
+            step(i, 0, defer=True)
+            kev[i][1].record(st)
+            mgs[0].finish_group(st.cuda_stream)
+        torch.cuda.synchronize()
+        for mg in mgs:
+            mg.check()
+        kus = float(np.mean([a.elapsed_time(b) for a, b in kev])) * 1e3
+        mpps = BATCH * args.steps / elapsed / 1e6
+        line = {"config": cfg, "mpps": round(mpps, 1), "us_per_batch": round(elapsed / args.steps * 1e6, 2),
+                "streams": S, "batch_pkts": BATCH, "backends": nbk, "table_size": m,
+                "path_bytes_per_pkt": bytes_pkt, "path_gbps": round(mpps * bytes_pkt / 1e3, 1),
+                "classify_us": round(kus, 2), "classify_bytes_per_pkt": classify_bytes,
+                "classify_gbps": round(BATCH * classify_bytes / kus / 1e3, 1),
+                "classify_frac_of_8TBps": round(BATCH * classify_bytes / kus / 1e3 / 8000.0, 4)}
+        if cfg == "c5":
+            g = gates[0].view(torch.int16).cpu().numpy().view(np.uint16)
+            line["gate_hist"] = {str(k): int(v) for k, v in zip(*np.unique(g, return_counts=True))}
+        print(json.dumps(line), flush=True)
+        for mg in mgs:
+            mg.close()
+        if lpm is not None:
+            lpm.close()
+        del bufs, offs, lens
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
