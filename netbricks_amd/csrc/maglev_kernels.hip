@@ -35,12 +35,13 @@ constexpr uint32_t kEth = 14;
 enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3 };
 
 // h = h ^ b; h *= 0x100000001b3 on (lo, hi) 32-bit halves:
-// h * (2^40 + 0x1b3) = lo*0x1b3 + 2^32 * (mulhi(lo,0x1b3) + hi*0x1b3 + (lo << 8))  (mod 2^64)
+// h * (2^40 + 0x1b3) = lo*0x1b3 + 2^32 * ((hi*0x1b3 mod 2^32) + (lo << 8))  (mod 2^64)
+// -> one v_mad_u64_u32 (lo*0x1b3 + (hi*0x1b3) << 32), one v_mul_lo_u32, one shift-add.
 __device__ __forceinline__ void fnv_step(uint32_t& lo, uint32_t& hi, uint32_t b) {
   lo ^= b;
-  const uint32_t nhi = __umulhi(lo, 0x1b3u) + hi * 0x1b3u + (lo << 8);
-  lo = lo * 0x1b3u;
-  hi = nhi;
+  const uint64_t t = static_cast<uint64_t>(lo) * 0x1b3u + (static_cast<uint64_t>(hi * 0x1b3u) << 32);
+  hi = static_cast<uint32_t>(t >> 32) + (lo << 8);
+  lo = static_cast<uint32_t>(t);
 }
 
 // x mod 65537 with 2^16 == -1 (mod 65537): alternating 16-bit digit sum.
@@ -146,12 +147,94 @@ __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
 }
 
-// ABL (diagnostic builds only, selected by NBG_ABL): 0 = full kernel; 1 = no hash/LUT (bin from a
-// header byte); 2 = also no LDS transpose (loads + backend store only).
-template <int LUTM, bool F4, bool HIST, bool CHAIN, int R, int ABL = 0, int NT = kBlock>
-__global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
+// Workgroup barrier for LDS-only hand-offs: wait for this wave's LDS operations, then s_barrier.
+// Unlike __syncthreads() it does not wait for outstanding global stores (the release fence drains
+// vmcnt), which would put HBM write latency on the group kernel's critical path.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One wave's 64-packet tile in registers: lane = (quad, part) holds 16-B chunk `part` of
+// packet k*16+quad (k = 0..3) — for 64-B slots each wave-instruction reads 1 KiB contiguous.
+// Every load is issued unconditionally (a lane with nothing to read loads 16 B at the batch
+// base) and nothing selects on its value: a predicated load merged with a default forces the
+// compiler to wait for it inside the branch, serialising the four loads.  The chunk of a lane
+// whose cflag bit is clear is never used.
+struct TileRegs {
+  uint4 ch[4];
+  uint32_t cflag;  // bit k: chunk k was really read and the packet is long enough for the fast path
+};
+
+// Per-lane metadata of its own packet (descriptor mode: offset + length; else fixed).
+struct TileMeta {
+  uint32_t off, len;
+};
+
+// DESC (descriptor mode): off[] and len[] are both present and read unconditionally (clamped
+// index), so the loads can stay in flight; otherwise only len[] may be present.
+template <bool DESC>
+__device__ __forceinline__ TileMeta load_meta(const ClassifyArgs& a, uint32_t wbase, uint32_t lane) {
+  const uint32_t p = min(wbase + lane, a.n_pkts - 1u);  // clamped: the value of a lane past the end is unused
+  TileMeta m;
+  if constexpr (DESC) {
+    m.off = a.off[p];
+    m.len = a.len[p];
+  } else {
+    m.off = 0u;
+    m.len = a.len ? a.len[p] : a.fixed_len;
+  }
+  return m;
+}
+
+// Fixed slots: the wave's tile base is wave-uniform (scalar 64-bit math) and lane offsets are
+// 32-bit (stride < 2^24 is checked on the host), keeping 64-bit multiplies out of the VALU path.
+template <bool DESC>
+__device__ __forceinline__ const uint8_t* pkt_addr(const ClassifyArgs& a, uint32_t wbase, uint32_t idx_in_tile,
+                                                   uint32_t off) {
+  if constexpr (DESC) return a.pkts + off;
+  return a.pkts + static_cast<size_t>(wbase) * a.stride + __umul24(idx_in_tile, a.stride);
+}
+
+template <bool DESC>
+__device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase, const TileMeta& m, uint32_t part,
+                                          uint32_t quad, TileRegs& t) {
+  const uint8_t* addr[4];
+  t.cflag = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t src = k * 16u + quad;
+    const uint32_t p = wbase + src;
+    const bool pv = p < a.n_pkts;
+    const uint32_t o = DESC ? static_cast<uint32_t>(__shfl(static_cast<int>(m.off), src)) : 0u;
+    const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(m.len), src)) : a.fixed_len;
+    const uint8_t* base = pkt_addr<DESC>(a, wbase, src, o);
+    const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
+    // chunk readable/writable: inside the frame, or the window is owned by this packet
+    const bool inwin = a.win_owned || (part * 16u + 16u <= l);
+    const bool rd = pv && aligned && inwin;
+    addr[k] = rd ? base + part * 16u : a.pkts;
+    if (rd && l >= 48u) t.cflag |= 1u << k;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t.ch[k] = ldg16(addr[k]);
+}
+
+// classify_kernel: each wave walks `tiles_per_wave` consecutive 64-packet tiles (1 with the L2
+// LUT: occupancy hides the latency; more with the LDS-staged LUT, to amortise the staging).  Per
+// tile: loads, LDS transpose, hash + gathers, then the write-back stores (vmcnt retires in issue
+// order: stores issued before the gathers would delay their use), then the slow-path packets.
+// One LDS histogram per block (two barriers per launch) is flushed once into the block's partition
+// row (the block's 64 * waves * tiles_per_wave packets divide part_pkts).  A software-pipelined variant (next tile's loads issued
+// behind the gathers) measured no faster at high occupancy and cost 18 VGPRs.
+// ABL (diagnostic builds only, selected by NBG_ABL): 1 = no hash/LUT (bin from header bytes);
+// 3 = FNV without the LUT gather; 4 = LUT gather of a trivial hash.
+template <int LUTM, bool F4, bool HIST, bool CHAIN, bool DESC, int ABL = 0, int NT = kBlock>
+__global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
-  constexpr uint32_t kT = NT * R;  // packets per tile
+  constexpr uint32_t kW = NT / 64u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint32_t part = lane & 3u, quad = lane >> 2;
   const uint32_t nbins = a.nb + 1;
@@ -159,8 +242,8 @@ __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
   const uint32_t lut_bytes = kLdsLut ? a.lut_lds_bytes : 0u;
   uint8_t* lut_lds = smem;
   uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + (NT / 64u) * 64u * kXStride);
-  const bool desc = a.off != nullptr;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + kW * 64u * kXStride);  // per block
+  constexpr bool desc = DESC;
 
   if constexpr (kLdsLut) {
     // stage the LUT: all loads issued before the LDS stores (one round trip)
@@ -181,163 +264,121 @@ __global__ __launch_bounds__(NT) void classify_kernel(ClassifyArgs a) {
         if (k < nvec) dst[k] = t[j];
       }
     }
+    __syncthreads();
+  }
+  if constexpr (HIST) {
+    for (uint32_t b = tid; b < nbins; b += NT) hist[b] = 0;
+    lds_sync();
   }
 
-  for (uint32_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
-    if constexpr (HIST) {
-      for (uint32_t b = tid; b < nbins; b += NT) hist[b] = 0;
+  const uint32_t tpw = a.tiles_per_wave;
+  const uint32_t t0 = (blockIdx.x * kW + wave) * tpw;  // first 64-packet tile of this wave
+  for (uint32_t i = 0; i < tpw; ++i) {
+    const uint32_t wbase = (t0 + i) * 64u;
+    if (wbase >= a.n_pkts) break;  // wave-uniform
+    const uint32_t p_own = wbase + lane;
+    const TileMeta meta = load_meta<DESC>(a, wbase, lane);
+    TileRegs cur;
+    load_tile<DESC>(a, wbase, meta, part, quad, cur);
+    // transpose: chunks 0..2 -> LDS [packet][80 B]
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = cur.ch[k];
     }
-    __syncthreads();
-    const uint32_t wbase = tile * kT + wave * (64u * R);
-
-    // ---- phase A: metadata and every round's window loads (R x 4 x 16 B in flight per lane);
-    //      lane = (quad, part) holds chunk `part` of packet k*16+quad of each round
-    uint32_t off_own[R], len_own[R], cflag[R];
-    uint4 ch[R][4];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t p_own = wbase + r * 64u + lane;
-      const bool v_own = p_own < a.n_pkts;
-      off_own[r] = desc ? (v_own ? a.off[p_own] : 0u) : 0u;
-      len_own[r] = a.len ? (v_own ? a.len[p_own] : 0u) : a.fixed_len;
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      cflag[r] = 0;  // bit k: chunk k may be written back if the packet is fast-path
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t src = k * 16u + quad;
-        const uint32_t p = wbase + r * 64u + src;
-        const bool pv = p < a.n_pkts;
-        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own[r]), src)) : 0u;
-        const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(len_own[r]), src)) : a.fixed_len;
-        const uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(p) * a.stride);
-        const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
-        // chunk readable/writable: inside the frame, or the window is owned by this packet
-        const bool inwin = a.win_owned || (part * 16u + 16u <= l);
-        const bool rd = pv && aligned && inwin;
-        ch[r][k] = rd ? ldg16(base + part * 16u) : make_uint4(0, 0, 0, 0);
-        if (rd && l >= 48u) cflag[r] |= 1u << k;
-      }
-    }
-
-    // ---- phase B: per round, transpose + swap + hash, and ISSUE the LUT gather (consumed in C)
-    uint32_t bin[R], gate[R], iplo[R];
-    bool resolve[R];  // CHAIN fast path: gate[] holds the raw tbl24 entry until phase C
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      gate[r] = kSentinel;
-      iplo[r] = 0;
-      resolve[r] = false;
-      const uint32_t rbase = wbase + r * 64u;
-      const uint32_t p_own = rbase + lane;
-      if constexpr (ABL == 2) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc ^= ch[r][k].x ^ ch[r][k].y ^ ch[r][k].z ^ ch[r][k].w;
-        bin[r] = acc & 63u;
-        continue;
-      }
-      // transpose: chunks 0..2 -> LDS [packet][80 B] (region reused per round, in wave order)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = ch[r][k];
-      }
-      // MAC swap in the loader lanes + window write-back (fast-path packets only)
-      if (a.swap) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
-          const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(ch[r][k].w), lane & ~3u));
-          const bool fast = ((cflag[r] >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
-          const uint32_t src = k * 16u + quad;
-          const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(off_own[r]), src)) : 0u;
-          if (!fast) continue;
-          uint8_t* base = a.pkts + (desc ? static_cast<size_t>(o) : static_cast<size_t>(rbase + src) * a.stride);
-          uint4 v = ch[r][k];
-          if (part == 0u) {
-            const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
-            // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
-            v = make_uint4((w1 >> 16) | (w2 << 16), (w2 >> 16) | (w0 << 16), (w0 >> 16) | (w1 << 16), v.w);
-          }
-          if (a.mac_out) {
-            // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
-            if (part == 0u) {
-              uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(rbase + src) * 12u);
-              mo[0] = v.x;
-              mo[1] = v.y;
-              mo[2] = v.z;
-            }
-          } else if (part == 0u || a.wb_full) {
-            stg16_nt(base + part * 16u, v);  // chunks 1..3 unchanged: makes the write whole lines
-          }
-        }
-      }
-      // compute lane: one packet
-      bin[r] = a.nb;
-      if (p_own < a.n_pkts) {
-        const uint8_t* x = xp + lane * kXStride;
-        const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
-        uint8_t* pown = a.pkts + (desc ? static_cast<size_t>(off_own[r]) : static_cast<size_t>(p_own) * a.stride);
-        const bool aligned = (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
-        // same decision as the loader lanes: chunks 0..2 were loaded and (if swapping) written
-        if (aligned && len_own[r] >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
-          const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
-          const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
-          // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
-          const uint32_t src = (c1.z >> 16) | (c1.w << 16);
-          const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
-          const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
-          if constexpr (ABL == 1) {
-            bin[r] = (src ^ dst ^ ports) % a.nb;
-          } else if constexpr (ABL == 3) {  // FNV, no LUT gather
-            uint32_t lo, hi;
-            fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-            bin[r] = mod_f4(lo, hi) % a.nb;
-          } else if constexpr (ABL == 4) {  // LUT gather of a trivial hash
-            bin[r] = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
-          } else {
-            uint32_t lo, hi;
-            if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
-              const uint32_t ip = __builtin_bswap32(src);
-              gate[r] = a.tbl24[ip >> 8];
-              iplo[r] = ip & 0xffu;
-              resolve[r] = true;
-            }
-            fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-            bin[r] = lookup<LUTM, F4>(a, lut_lds, lo, hi);  // gathers issued; first use in phase C
-          }
+    // compute lane: one packet (issues the LUT / LPM gathers).  Packets off the fast path are
+    // classified after this tile's loads, stores and gathers are all issued (`slow` below): their
+    // byte-wise loads would otherwise make the compiler wait for every outstanding load here.
+    uint32_t bin = a.nb, gate = kSentinel, iplo = 0;
+    bool resolve = false;  // CHAIN fast path: `gate` holds the raw tbl24 entry until consumed
+    bool slow = false;
+    uint8_t* pown = const_cast<uint8_t*>(pkt_addr<DESC>(a, wbase, lane, meta.off));
+    if (p_own < a.n_pkts) {
+      const uint8_t* x = xp + lane * kXStride;
+      const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
+      const bool aligned = (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
+      // same decision as the loader lanes: chunks 0..2 were loaded (and, if swapping, get written)
+      if (aligned && meta.len >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
+        const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
+        const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
+        // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
+        const uint32_t src = (c1.z >> 16) | (c1.w << 16);
+        const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
+        const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
+        if constexpr (ABL == 1) {
+          bin = (src ^ dst ^ ports) % a.nb;
+        } else if constexpr (ABL == 3) {
+          uint32_t lo, hi;
+          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+          bin = mod_f4(lo, hi) % a.nb;
+        } else if constexpr (ABL == 4) {
+          bin = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
         } else {
-          bin[r] = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, len_own[r], p_own, gate[r]);
+          uint32_t lo, hi;
+          if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
+            const uint32_t ip = __builtin_bswap32(src);
+            gate = a.tbl24[ip >> 8];
+            iplo = ip & 0xffu;
+            resolve = true;
+          }
+          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+          bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
         }
+      } else {
+        slow = true;
       }
     }
-
-    // ---- phase C: consume the gathers
+    // MAC swap in the loader lanes + window write-back (fast-path packets only)
+    if (a.swap) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const uint32_t p_own = wbase + r * 64u + lane;
-      if (p_own < a.n_pkts) {
-        if constexpr (CHAIN) {
-          if (resolve[r] && (gate[r] & 0x8000u)) gate[r] = a.tbl_long[((gate[r] & 0x7fffu) << 8) + iplo[r]];
-          a.gate[p_own] = static_cast<uint16_t>(gate[r]);
-          if (gate[r] >= a.lpm_groups) bin[r] = a.nb;  // test/lpm would panic: never reaches maglev
+      for (int k = 0; k < 4; ++k) {
+        // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
+        const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(cur.ch[k].w), lane & ~3u));
+        const bool fast = ((cur.cflag >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
+        const uint32_t src = k * 16u + quad;
+        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(meta.off), src)) : 0u;
+        if (!fast) continue;
+        uint8_t* base = const_cast<uint8_t*>(pkt_addr<DESC>(a, wbase, src, o));
+        uint4 v = cur.ch[k];
+        if (part == 0u) {
+          const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
+          // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
+          v = make_uint4((w1 >> 16) | (w2 << 16), (w2 >> 16) | (w0 << 16), (w0 >> 16) | (w1 << 16), v.w);
         }
-        a.backend[p_own] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
-        if constexpr (HIST) atomicAdd(&hist[bin[r]], 1u);
+        if (a.mac_out) {
+          // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
+          if (part == 0u) {
+            uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(wbase + src) * 12u);
+            mo[0] = v.x;
+            mo[1] = v.y;
+            mo[2] = v.z;
+          }
+        } else if (part == 0u || a.wb_full) {
+          stg16_nt(base + part * 16u, v);  // chunks 1..3 unchanged: makes the write whole lines
+        }
       }
     }
+    // consume the gathers
+    if (p_own < a.n_pkts) {
+      if (slow) bin = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, meta.len, p_own, gate);
+      if constexpr (CHAIN) {
+        if (resolve && (gate & 0x8000u)) gate = a.tbl_long[((gate & 0x7fffu) << 8) + iplo];
+        a.gate[p_own] = static_cast<uint16_t>(gate);
+        if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
+      }
+      a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+      if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+    }
+  }
 
-    if constexpr (HIST) {
-      __syncthreads();
-      // partition histogram: few tiles share a partition row, so the adds rarely contend
-      uint32_t* row = a.part_hist + static_cast<size_t>(tile * kT / a.part_pkts) * nbins;
-      for (uint32_t b = tid; b < nbins; b += NT) {
-        const uint32_t h = hist[b];
-        if (h) atomicAdd(&row[b], h);
-      }
+  if constexpr (HIST) {
+    // one flush per block into its partition row (the block's packets never straddle two):
+    // 4096-packet rows take ~16 blocks' adds, so they rarely contend
+    lds_sync();
+    uint32_t* row = a.part_hist + static_cast<size_t>(blockIdx.x * kW * tpw * 64u / a.part_pkts) * nbins;
+    for (uint32_t b = tid; b < nbins; b += NT) {
+      const uint32_t h = hist[b];
+      if (h) atomicAdd(&row[b], h);
     }
-    __syncthreads();
   }
 }
 
@@ -353,7 +394,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wa
     if (lane >= static_cast<uint32_t>(d)) x += y;
   }
   if (lane == 63u) s_wave[wave] = x;
-  __syncthreads();
+  lds_sync();
   uint32_t wpre = 0, tot = 0;
 #pragma unroll
   for (uint32_t w = 0; w < NT / 64; ++w) {
@@ -361,7 +402,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wa
     if (w < wave) wpre += t;
     tot += t;
   }
-  __syncthreads();
+  lds_sync();
   total = tot;
   return wpre + x - v;
 }
@@ -451,7 +492,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     tot[b] = 0;
   }
   if constexpr (SCAN == kScanDirect) {
-    __syncthreads();
+    lds_sync();
     // L threads per bin, each summing a strided subset of the partition rows straight from L2
     // (consecutive threads read consecutive bins of one row: coalesced)
     const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
@@ -494,7 +535,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       if (v < nvec) reinterpret_cast<uint4*>(ph)[v] = tmp[k];
     }
     for (uint32_t i = nvec * 4 + tid; i < words; i += kGBlock) ph[i] = a.part_hist[i];
-    __syncthreads();
+    lds_sync();
     // L threads per bin, each summing a strided subset of the partitions
     const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
     for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
@@ -509,16 +550,14 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       if (all) atomicAdd(&tot[b], all);
     }
   } else {
-    __syncthreads();
+    lds_sync();
     for (uint32_t b = tid; b < nbins; b += kGBlock) {
       base[b] = a.part_prefix[static_cast<size_t>(c) * nbins + b];
       tot[b] = a.totals[b];
     }
   }
   GPROBE(2)
-  // the next call accumulates into the other buffer: zero it (every block a slice)
-  for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
-  __syncthreads();
+  lds_sync();
   {
     const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
     const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
@@ -533,15 +572,18 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       gb += t;
     }
   }
-  __syncthreads();
+  lds_sync();
   GPROBE(3)
+  // the next call accumulates into the other buffer: zero it (every block a slice; nothing in
+  // this kernel waits for these stores)
+  for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
   if (!a.perm) return;
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t* mycnt = cnt + wave * nbins;
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
     for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
-    __syncthreads();
+    lds_sync();
     uint32_t bins[kGRounds], ranks[kGRounds];
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
@@ -568,7 +610,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       bins[r] = valid ? bin : 0xffffffffu;
       ranks[r] = rank;
     }
-    __syncthreads();
+    lds_sync();
     GPROBE(4)
     // per bin: offsets of each wave inside the bin (16-lane segmented scan over waves) ...
     for (uint32_t t = tid; t < nbins * kW; t += kGBlock) {
@@ -583,7 +625,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       cnt[w * nbins + b] = x - v;
       if (w == kW - 1) sub[b] = x;  // the bin's packets in this chunk
     }
-    __syncthreads();
+    lds_sync();
     GPROBE(5)
     // ... and the chunk-local start of each bin (scan over bins)
     const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
@@ -599,7 +641,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       base[b] += n;               // advance past this chunk's packets of bin b
       lstart += n;
     }
-    __syncthreads();
+    lds_sync();
     GPROBE(6)
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
@@ -609,11 +651,11 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
         sbin[j] = static_cast<uint16_t>(bins[r]);
       }
     }
-    __syncthreads();
+    lds_sync();
     GPROBE(7)
     // coalesced output: consecutive sorted slots of one bin are consecutive perm entries
     for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
-    __syncthreads();
+    lds_sync();
   }
   GPROBE(8)
 #ifdef NBG_GPROBE
@@ -629,7 +671,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 template <int LUTM, bool F4, bool HIST, bool CHAIN>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   constexpr int NT = (LUTM == kLdsU8 || LUTM == kLdsU16) ? kLdsBlock : kBlock;
-  auto fn = classify_kernel<LUTM, F4, HIST, CHAIN, 1, 0, NT>;
+  auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, true, 0, NT> : classify_kernel<LUTM, F4, HIST, CHAIN, false, 0, NT>;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
@@ -638,7 +680,7 @@ int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
 
 template <int LUTM, bool F4, bool HIST, int ABL>
 int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, 1, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, false, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -652,10 +694,9 @@ int launch_v(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
       const char* e = std::getenv("NBG_ABL");
       return e ? std::atoi(e) : 0;
     }();
-    if (abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
-    if (abl == 2) return launch_abl<LUTM, F4, HIST, 2>(a, grid, lds, s);
-    if (abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
-    if (abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
+    if (!a.off && abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
+    if (!a.off && abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
+    if (!a.off && abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
   }
   return launch_one<LUTM, F4, HIST, false>(a, grid, lds, s);
 }

@@ -6,11 +6,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "nbgpu_internal.h"
@@ -67,6 +69,11 @@ struct nbg_maglev {
   ScanArgs pending_scan{};
   hipStream_t last_stream = nullptr;
   int grid_lds = 0, grid_global = 0;
+  uint32_t tiles_per_wave = 1;        // L2-LUT classify: 64-packet tiles per wave (NBG_TPW)
+  // descriptor mode without lengths: a fixed_len-filled u16[] (the kernel reads off[] and len[])
+  uint16_t* d_fixed_len = nullptr;
+  uint64_t fixed_len_cap = 0;
+  uint16_t fixed_len_val = 0;
   // host-path staging (pinned host + device)
   uint64_t host_cap = 0;
   uint32_t host_win = 0;
@@ -95,6 +102,9 @@ struct DeviceGuard {
 };
 
 void free_scratch(nbg_maglev* h) {
+  (void)hipFree(h->d_fixed_len);
+  h->d_fixed_len = nullptr;
+  h->fixed_len_cap = 0;
   (void)hipFree(h->d_part_hist);
   (void)hipFree(h->d_part_prefix);
   (void)hipFree(h->d_totals);
@@ -145,6 +155,11 @@ int upload(nbg_maglev* h) {
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
+  if (const char* e = std::getenv("NBG_TPW")) {
+    const int v = std::atoi(e);
+    h->tiles_per_wave = 1;
+    while (static_cast<int>(h->tiles_per_wave) < v && h->tiles_per_wave < 64) h->tiles_per_wave <<= 1;
+  }
   int rc = classify_grid(true, h->lut_bytes, h->nb, h->device, &h->grid_lds);
   if (rc) return rc;
   return classify_grid(false, 0, h->nb, h->device, &h->grid_global);
@@ -154,6 +169,27 @@ int upload(nbg_maglev* h) {
 // occupancy); NBG_LUT_LDS stages it in LDS when it fits.
 bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
   return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024;
+}
+
+// Run fn(begin, end) over [0, n) on up to 8 host threads (large batches only: the gather of
+// scattered mbuf windows is bound by host memory latency, not bandwidth).
+template <typename F>
+void parallel_for(uint64_t n, F fn) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  unsigned t = hw ? std::min(hw, 8u) : 1u;
+  if (n < 32768) t = 1;
+  if (t <= 1) {
+    fn(uint64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  const uint64_t per = (n + t - 1) / t;
+  for (unsigned k = 1; k < t; ++k) {
+    const uint64_t b = k * per, e = std::min(n, b + per);
+    if (b < e) pool.emplace_back([=] { fn(b, e); });
+  }
+  fn(uint64_t(0), std::min(n, per));
+  for (auto& th : pool) th.join();
 }
 
 int finish_create(nbg_maglev* h, int device, nbg_maglev** out) {
@@ -272,6 +308,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   if (lpm && (!d_gate || lpm->device != h->device))
     return set_error(NBG_EINVAL, "chain: null gate buffer, or lpm and maglev handles on different devices");
   if (!d_off && stride == 0) return set_error(NBG_EINVAL, "classify: stride 0 without offsets");
+  if (!d_off && stride >= (1u << 24)) return set_error(NBG_EINVAL, "classify: stride must be < 2^24 (use offsets)");
   if (!d_off && static_cast<unsigned __int128>(n_pkts) * stride > (1ull << 40))
     return set_error(NBG_EINVAL, "classify: batch too large");
   DeviceGuard g(h->device);
@@ -280,16 +317,41 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   if (group && nbins > kMaxGroupBins)
     return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
   const bool lds = use_lds_lut(h, flags);
-  const uint32_t hist_tile = lds ? kLdsBlock : kBlock;
-  const uint32_t n_tiles = static_cast<uint32_t>((n_pkts + hist_tile - 1) / hist_tile);
-  // LDS-staged LUT: persistent resident grid; L2 LUT: one tile per block
-  const int grid = lds ? std::min<int>(h->grid_lds, static_cast<int>(n_tiles)) : static_cast<int>(n_tiles);
+  // each wave walks tpw consecutive 64-packet tiles (software-pipelined); the LDS-LUT variant
+  // runs a resident grid of 1024-thread blocks so that the LUT staging is amortised
+  const uint32_t waves_per_block = (lds ? kLdsBlock : kBlock) / 64;
+  const uint64_t n_tiles64 = (n_pkts + 63) / 64;
+  // a block's packets (64 * waves * tpw, a power of two <= kChunk) must not straddle a partition
+  const uint32_t tpw_max = kChunk / (64u * waves_per_block);
+  uint32_t tpw = std::min(h->tiles_per_wave, tpw_max);
+  if (lds) {
+    const uint64_t want = (n_tiles64 + uint64_t(h->grid_lds) * waves_per_block - 1) / (uint64_t(h->grid_lds) * waves_per_block);
+    tpw = 1;
+    while (tpw < want && tpw < tpw_max) tpw <<= 1;
+  }
+  const int grid = static_cast<int>((n_tiles64 + uint64_t(tpw) * waves_per_block - 1) / (uint64_t(tpw) * waves_per_block));
   const uint64_t per = (n_pkts + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
   const uint32_t part_pkts = static_cast<uint32_t>(per * kChunk);
   const uint32_t n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
   uint32_t* part_cur = h->d_part_hist + static_cast<size_t>(h->parity) * kMaxParts * nbins;
   uint32_t* part_next = h->d_part_hist + static_cast<size_t>(h->parity ^ 1u) * kMaxParts * nbins;
 
+  if (d_off && !d_len) {
+    if (h->fixed_len_cap < n_pkts) {
+      (void)hipFree(h->d_fixed_len);
+      h->d_fixed_len = nullptr;
+      h->fixed_len_cap = 0;
+      NBG_HIP(hipMalloc(&h->d_fixed_len, n_pkts * sizeof(uint16_t)));
+      h->fixed_len_cap = n_pkts;
+      h->fixed_len_val = static_cast<uint16_t>(~fixed_len);  // force the fill below
+    }
+    if (h->fixed_len_val != fixed_len) {
+      NBG_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(h->d_fixed_len), fixed_len, h->fixed_len_cap,
+                                static_cast<hipStream_t>(stream)));
+      h->fixed_len_val = fixed_len;
+    }
+    d_len = h->d_fixed_len;
+  }
   ClassifyArgs a{};
   a.pkts = d_pkts;
   a.off = d_off;
@@ -297,7 +359,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   a.stride = stride;
   a.fixed_len = fixed_len;
   a.n_pkts = static_cast<uint32_t>(n_pkts);
-  a.n_tiles = n_tiles;
+  a.tiles_per_wave = tpw;
   a.lut = h->d_lut;
   a.m = static_cast<uint32_t>(h->m);
   a.lut_lds_bytes = lds ? h->lut_bytes : 0;
@@ -459,13 +521,16 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
     return NBG_OK;
   }
   // Header window per packet: bytes the path can read = 14 + max(20, 4*IHL + 4) <= 78.
-  uint32_t need = 64;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (lens[i] > 64 && lens[i] >= 15) {
-      const uint32_t w = 14 + std::max<uint32_t>(20, (pkt_ptrs[i][14] & 0xfu) * 4 + 4);
-      if (w > need) need = w;
+  std::atomic<uint32_t> need{64};
+  parallel_for(n, [&](uint64_t b, uint64_t e) {
+    uint32_t m = 64;
+    for (uint64_t i = b; i < e; ++i) {
+      if (lens[i] > 64) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (pkt_ptrs[i][14] & 0xfu) * 4 + 4));
     }
-  }
+    uint32_t cur = need.load();
+    while (m > cur && !need.compare_exchange_weak(cur, m)) {
+    }
+  });
   const uint32_t win = need <= 64 ? 64 : 80;
   if (n > h->host_cap || win != h->host_win) {
     free_host_path(h);
@@ -481,11 +546,15 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
     h->host_cap = cap;
     h->host_win = win;
   }
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint32_t c = std::min<uint32_t>(lens[i], win);
-    std::memcpy(h->h_win + i * win, pkt_ptrs[i], c);
-    h->h_len[i] = lens[i];
-  }
+  uint8_t* h_win = h->h_win;
+  uint16_t* h_len = h->h_len;
+  parallel_for(n, [=](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint32_t c = std::min<uint32_t>(lens[i], win);
+      std::memcpy(h_win + i * win, pkt_ptrs[i], c);
+      h_len[i] = lens[i];
+    }
+  });
   hipStream_t s = h->host_stream;
   NBG_HIP(hipMemcpyAsync(h->d_win, h->h_win, n * win, hipMemcpyHostToDevice, s));
   NBG_HIP(hipMemcpyAsync(h->d_len, h->h_len, n * 2, hipMemcpyHostToDevice, s));
@@ -502,8 +571,11 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
   if (swap) NBG_HIP(hipMemcpyAsync(h->h_mac, h->d_mac, n * 12, hipMemcpyDeviceToHost, s));
   NBG_HIP(hipStreamSynchronize(s));
   if (swap) {
-    for (uint64_t i = 0; i < n; ++i)
-      if (lens[i] >= 14) std::memcpy(pkt_ptrs[i], h->h_mac + i * 12, 12);
+    const uint8_t* h_mac = h->h_mac;
+    parallel_for(n, [=](uint64_t b, uint64_t e) {
+      for (uint64_t i = b; i < e; ++i)
+        if (lens[i] >= 14) std::memcpy(pkt_ptrs[i], h_mac + i * 12, 12);
+    });
   }
   return NBG_OK;
 }

@@ -35,7 +35,7 @@ struct ClassifyArgs {
   uint32_t stride;
   uint32_t fixed_len;
   uint32_t n_pkts;
-  uint32_t n_tiles;
+  uint32_t tiles_per_wave;  // consecutive 64-packet tiles per wave (power of 2, <= 64)
   const void* lut;          // u8 or u16 entries
   uint32_t m;               // table size
   uint32_t lut_lds_bytes;   // bytes of LUT staged in LDS (0 = global gather)

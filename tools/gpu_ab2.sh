@@ -4,7 +4,7 @@ mkdir -p gpurun_out
 NBG_LIB_OVERRIDE=$PWD/tools/ab/lib_new.so timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest(new) rc=$rc"; tail -3 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 for pass in 1 2; do
-  for cfg in old:1 new:1 new:2 new:4; do
+  for cfg in ${CFGS:-old:1 new:1}; do
     L=${cfg%%:*}; T=${cfg##*:}
     echo "== lib_$L TPW=$T (pass $pass)"
     NBG_TPW=$T NBG_LIB_OVERRIDE=$PWD/tools/ab/lib_$L.so timeout -k 10 300 python tools/kbench.py "$@" > gpurun_out/ab.log 2>&1
