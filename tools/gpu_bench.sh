@@ -17,4 +17,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace -d "$R0/gpurun_out/prof/pmc_$C" -o run --output-format csv -- python "$R0/bench.py" --streams 1 --steps 50 --warmup 10 --no-cpu-baseline > "$R0/gpurun_out/prof/pmc_$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-exit 0
+cd "$R0" && python tools/pmc_to_json.py gpurun_out/prof/pmc_FETCH_SIZE gpurun_out/prof/pmc_WRITE_SIZE ${ROUND:-1} > gpurun_out/prof/pmc.json
+rc=$?; cat gpurun_out/prof/pmc.json; exit $rc
