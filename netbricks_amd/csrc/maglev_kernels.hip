@@ -34,6 +34,11 @@ constexpr uint32_t kEth = 14;
 // LUT placement / width variants.
 enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3 };
 
+// Packet layouts: fixed slots (general), fixed slots known by the host to be 16-B aligned with
+// owned windows, no length array and frames >= 48 B (every chunk readable, no per-lane
+// predicates), and descriptors (offset + length arrays).
+enum Layout { kFixed = 0, kLean = 1, kDesc = 2 };
+
 // h = h ^ b; h *= 0x100000001b3 on (lo, hi) 32-bit halves:
 // h * (2^40 + 0x1b3) = lo*0x1b3 + 2^32 * ((hi*0x1b3 mod 2^32) + (lo << 8))  (mod 2^64)
 // -> one v_mad_u64_u32 (lo*0x1b3 + (hi*0x1b3) << 32), one v_mul_lo_u32, one shift-add.
@@ -175,11 +180,14 @@ struct TileMeta {
 
 // DESC (descriptor mode): off[] and len[] are both present and read unconditionally (clamped
 // index), so the loads can stay in flight; otherwise only len[] may be present.
-template <bool DESC>
+template <int LAYOUT>
 __device__ __forceinline__ TileMeta load_meta(const ClassifyArgs& a, uint32_t wbase, uint32_t lane) {
   const uint32_t p = min(wbase + lane, a.n_pkts - 1u);  // clamped: the value of a lane past the end is unused
   TileMeta m;
-  if constexpr (DESC) {
+  if constexpr (LAYOUT == kLean) {
+    m.off = 0u;
+    m.len = a.fixed_len;
+  } else if constexpr (LAYOUT == kDesc) {
     m.off = a.off[p];
     m.len = a.len[p];
   } else {
@@ -191,18 +199,32 @@ __device__ __forceinline__ TileMeta load_meta(const ClassifyArgs& a, uint32_t wb
 
 // Fixed slots: the wave's tile base is wave-uniform (scalar 64-bit math) and lane offsets are
 // 32-bit (stride < 2^24 is checked on the host), keeping 64-bit multiplies out of the VALU path.
-template <bool DESC>
+template <int LAYOUT>
 __device__ __forceinline__ const uint8_t* pkt_addr(const ClassifyArgs& a, uint32_t wbase, uint32_t idx_in_tile,
                                                    uint32_t off) {
-  if constexpr (DESC) return a.pkts + off;
+  if constexpr (LAYOUT == kDesc) return a.pkts + off;
   return a.pkts + static_cast<size_t>(wbase) * a.stride + __umul24(idx_in_tile, a.stride);
 }
 
-template <bool DESC>
+template <int LAYOUT>
 __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase, const TileMeta& m, uint32_t part,
                                           uint32_t quad, TileRegs& t) {
+  constexpr bool DESC = LAYOUT == kDesc;
   const uint8_t* addr[4];
   t.cflag = 0;
+  if constexpr (LAYOUT == kLean) {
+    // every chunk of every packet is readable; only the batch tail is masked
+    const uint8_t* tb = a.pkts + static_cast<size_t>(wbase) * a.stride + __umul24(quad, a.stride) + part * 16u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool pv = wbase + k * 16u + quad < a.n_pkts;
+      addr[k] = pv ? tb + k * 16u * a.stride : a.pkts;
+      t.cflag |= static_cast<uint32_t>(pv) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t.ch[k] = ldg16(addr[k]);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t src = k * 16u + quad;
@@ -210,7 +232,7 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
     const bool pv = p < a.n_pkts;
     const uint32_t o = DESC ? static_cast<uint32_t>(__shfl(static_cast<int>(m.off), src)) : 0u;
     const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(m.len), src)) : a.fixed_len;
-    const uint8_t* base = pkt_addr<DESC>(a, wbase, src, o);
+    const uint8_t* base = pkt_addr<LAYOUT>(a, wbase, src, o);
     const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
     // chunk readable/writable: inside the frame, or the window is owned by this packet
     const bool inwin = a.win_owned || (part * 16u + 16u <= l);
@@ -231,7 +253,7 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
 // behind the gathers) measured no faster at high occupancy and cost 18 VGPRs.
 // ABL (diagnostic builds only, selected by NBG_ABL): 1 = no hash/LUT (bin from header bytes);
 // 3 = FNV without the LUT gather; 4 = LUT gather of a trivial hash.
-template <int LUTM, bool F4, bool HIST, bool CHAIN, bool DESC, int ABL = 0, int NT = kBlock>
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL = 0, int NT = kBlock>
 __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(ClassifyArgs a) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr uint32_t kW = NT / 64u;
@@ -243,7 +265,7 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
   uint8_t* lut_lds = smem;
   uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + kW * 64u * kXStride);  // per block
-  constexpr bool desc = DESC;
+  constexpr bool desc = LAYOUT == kDesc;
 
   if constexpr (kLdsLut) {
     // stage the LUT: all loads issued before the LDS stores (one round trip)
@@ -277,9 +299,9 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     const uint32_t wbase = (t0 + i) * 64u;
     if (wbase >= a.n_pkts) break;  // wave-uniform
     const uint32_t p_own = wbase + lane;
-    const TileMeta meta = load_meta<DESC>(a, wbase, lane);
+    const TileMeta meta = load_meta<LAYOUT>(a, wbase, lane);
     TileRegs cur;
-    load_tile<DESC>(a, wbase, meta, part, quad, cur);
+    load_tile<LAYOUT>(a, wbase, meta, part, quad, cur);
     // transpose: chunks 0..2 -> LDS [packet][80 B]
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -291,13 +313,14 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     uint32_t bin = a.nb, gate = kSentinel, iplo = 0;
     bool resolve = false;  // CHAIN fast path: `gate` holds the raw tbl24 entry until consumed
     bool slow = false;
-    uint8_t* pown = const_cast<uint8_t*>(pkt_addr<DESC>(a, wbase, lane, meta.off));
+    uint8_t* pown = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, lane, meta.off));
     if (p_own < a.n_pkts) {
       const uint8_t* x = xp + lane * kXStride;
       const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
-      const bool aligned = (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
+      const bool aligned = LAYOUT == kLean || (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
+      const bool longf = LAYOUT == kLean || meta.len >= 48u;
       // same decision as the loader lanes: chunks 0..2 were loaded (and, if swapping, get written)
-      if (aligned && meta.len >= 48u && ((w3 >> 16) & 0xfu) == 5u) {
+      if (aligned && longf && ((w3 >> 16) & 0xfu) == 5u) {
         const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
         const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
         // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
@@ -337,7 +360,7 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
         const uint32_t src = k * 16u + quad;
         const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(meta.off), src)) : 0u;
         if (!fast) continue;
-        uint8_t* base = const_cast<uint8_t*>(pkt_addr<DESC>(a, wbase, src, o));
+        uint8_t* base = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, src, o));
         uint4 v = cur.ch[k];
         if (part == 0u) {
           const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
@@ -428,6 +451,32 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   __syncthreads();
   total = tot;
   return wpre + x - v;
+}
+
+// Many backends: the partition histograms come from this kernel instead of the classify kernel
+// (whose per-block flush would cost about one global atomic per packet at ~1000 bins).  One
+// 1024-thread block per partition counts its packets' backends in LDS and stores the whole row.
+__global__ __launch_bounds__(kGBlock) void hist_kernel(HistArgs a) {
+  extern __shared__ __align__(16) uint32_t hs[];
+  const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c = blockIdx.x;
+  const uint32_t pbeg = c * a.part_pkts, pend = min(pbeg + a.part_pkts, a.n_pkts);
+  for (uint32_t b = tid; b < nbins; b += kGBlock) hs[b] = 0;
+  lds_sync();
+  for (uint32_t i0 = pbeg; i0 < pend; i0 += 4 * kGBlock) {
+    uint32_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t i = i0 + k * kGBlock + tid;
+      v[k] = i < pend ? a.backend[i] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (v[k] != 0xffffffffu) atomicAdd(&hs[v[k] == NBG_SENTINEL ? a.nb : v[k]], 1u);
+    }
+  }
+  lds_sync();
+  uint32_t* row = a.part_hist + static_cast<size_t>(c) * nbins;
+  for (uint32_t b = tid; b < nbins; b += kGBlock) row[b] = hs[b];
 }
 
 // Fallback for many backends: one block per bin, exclusive scan of part_hist[.][bin] over
@@ -671,7 +720,9 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 template <int LUTM, bool F4, bool HIST, bool CHAIN>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   constexpr int NT = (LUTM == kLdsU8 || LUTM == kLdsU16) ? kLdsBlock : kBlock;
-  auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, true, 0, NT> : classify_kernel<LUTM, F4, HIST, CHAIN, false, 0, NT>;
+  auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, kDesc, 0, NT>
+                  : (a.lean ? classify_kernel<LUTM, F4, HIST, CHAIN, kLean, 0, NT>
+                            : classify_kernel<LUTM, F4, HIST, CHAIN, kFixed, 0, NT>);
   hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
@@ -680,7 +731,7 @@ int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
 
 template <int LUTM, bool F4, bool HIST, int ABL>
 int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, false, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, kLean, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -694,9 +745,9 @@ int launch_v(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
       const char* e = std::getenv("NBG_ABL");
       return e ? std::atoi(e) : 0;
     }();
-    if (!a.off && abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
-    if (!a.off && abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
-    if (!a.off && abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
+    if (a.lean && abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
+    if (a.lean && abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
+    if (a.lean && abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
   }
   return launch_one<LUTM, F4, HIST, false>(a, grid, lds, s);
 }
@@ -742,6 +793,14 @@ int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uin
   return NBG_OK;
 }
 
+int launch_hist(const HistArgs& a, void* stream) {
+  const size_t lds = static_cast<size_t>(a.nb + 1) * 4;
+  hipLaunchKernelGGL(hist_kernel, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "hist launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
 int launch_scan(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(scan_kernel, dim3(a.nbins), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
@@ -758,6 +817,16 @@ size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
 // Default: sum the partition histograms from L2 inside the group kernel while the rows are
 // small (every block reads all of them), else a separate scan kernel.  NBG_GSCAN=0/1/2 forces
 // a mode (diagnostics; 1 falls back when the rows do not fit in LDS).
+// Partition histograms from the classify kernel's per-block flush for few bins, from hist_kernel
+// for many (NBG_HIST_KERNEL_BINS overrides the threshold, for measurements).
+bool hist_in_classify(uint32_t nbins) {
+  static const uint32_t limit = [] {
+    const char* e = std::getenv("NBG_HIST_KERNEL_BINS");
+    return e ? static_cast<uint32_t>(std::atoi(e)) : 257u;
+  }();
+  return nbins < limit;
+}
+
 int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
   static const int forced = [] {
     const char* e = std::getenv("NBG_GSCAN");

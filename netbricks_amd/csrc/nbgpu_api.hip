@@ -65,6 +65,8 @@ struct nbg_maglev {
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
   bool pending = false;
   int pending_scan_mode = 0;
+  bool pending_hist = false;
+  HistArgs pending_hist_args{};
   GroupArgs pending_args{};
   ScanArgs pending_scan{};
   hipStream_t last_stream = nullptr;
@@ -369,9 +371,14 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   // a 64-B window per packet start is owned: fixed slots of >= 64 B, or the caller says so
   a.win_owned = (!d_off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
   a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
+  a.lean = (!d_off && !d_len && a.win_owned && stride % 16 == 0 && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
+            fixed_len >= 48)
+               ? 1u
+               : 0u;
   a.backend = d_backend;
   a.mac_out = d_mac_out;
-  a.part_hist = group ? part_cur : nullptr;
+  const bool hist_k = group && !hist_in_classify(nbins);  // histograms by hist_kernel instead
+  a.part_hist = group && !hist_k ? part_cur : nullptr;
   a.part_pkts = part_pkts;
   if (lpm) {
     a.tbl24 = lpm->d_tbl24;
@@ -390,6 +397,13 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     sa.totals = h->d_totals;
     sa.n_parts = n_parts;
     sa.nbins = nbins;
+    HistArgs ha{};
+    ha.backend = d_backend;
+    ha.n_pkts = static_cast<uint32_t>(n_pkts);
+    ha.nb = h->nb;
+    ha.part_pkts = part_pkts;
+    ha.n_parts = n_parts;
+    ha.part_hist = part_cur;
     GroupArgs ga{};
     ga.backend = d_backend;
     ga.n_pkts = static_cast<uint32_t>(n_pkts);
@@ -410,9 +424,12 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     if (flags & NBG_DEFER_GROUP) {
       h->pending = true;
       h->pending_scan_mode = scan;
+      h->pending_hist = hist_k;
+      h->pending_hist_args = ha;
       h->pending_args = ga;
       h->pending_scan = sa;
     } else {
+      if (hist_k && (rc = launch_hist(ha, stream))) return rc;
       if (scan == kScanKernel && (rc = launch_scan(sa, stream))) return rc;
       if ((rc = launch_group(ga, scan, stream))) return rc;
     }
@@ -495,6 +512,7 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   DeviceGuard g(h->device);
   h->pending = false;
   int rc;
+  if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;
   if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
   if ((rc = launch_group(h->pending_args, h->pending_scan_mode, stream))) return rc;
   h->last_stream = static_cast<hipStream_t>(stream);

@@ -44,6 +44,7 @@ struct ClassifyArgs {
   uint32_t swap;
   uint32_t win_owned;       // every packet start owns 64 readable/writable bytes
   uint32_t wb_full;         // write back the whole owned window (full lines) instead of 16 B
+  uint32_t lean;            // fixed slots, 16-B aligned, owned windows, no len[], fixed_len >= 48
   uint16_t* backend;
   uint8_t* mac_out;         // nullable: dense 12-B swapped-MAC records instead of in-place swap
   uint32_t* part_hist;      // nullable: [n_parts][nb+1] partition histograms (pre-zeroed)
@@ -53,6 +54,15 @@ struct ClassifyArgs {
   const uint16_t* tbl_long;
   uint32_t lpm_groups;
   uint16_t* gate;
+};
+
+struct HistArgs {
+  const uint16_t* backend;
+  uint32_t n_pkts;
+  uint32_t nb;
+  uint32_t part_pkts;
+  uint32_t n_parts;
+  uint32_t* part_hist;      // [n_parts][nb+1], every entry stored
 };
 
 struct ScanArgs {
@@ -86,6 +96,8 @@ enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
 int launch_scan(const ScanArgs& a, void* stream);
+int launch_hist(const HistArgs& a, void* stream);
+bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
                       uint16_t* gate, void* stream);
 int launch_group(const GroupArgs& a, int scan, void* stream);
