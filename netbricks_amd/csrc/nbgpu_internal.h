@@ -22,9 +22,12 @@ int build_lpm(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gat
 constexpr int kBlock = 256;          // classify threads per workgroup (4 waves), L2-gather LUT
 constexpr int kLdsBlock = 1024;      // classify threads per workgroup with the LDS-staged LUT (1 per CU)
 constexpr int kXStride = 80;         // LDS bytes per packet in the transpose (64 + 16: conflict-free b128)
-constexpr int kGBlock = 1024;        // group kernel threads per workgroup (16 waves)
-constexpr int kGRounds = 4;          // group kernel rounds of 64 packets per wave per chunk
-constexpr int kChunk = kGBlock * kGRounds;  // packets per group-kernel chunk (4096)
+#ifndef NBG_GBLOCK
+#define NBG_GBLOCK 512
+#endif
+constexpr int kGBlock = NBG_GBLOCK;  // group kernel threads per workgroup (8 waves: overlaps classify better)
+constexpr int kChunk = 4096;         // packets per group-kernel chunk
+constexpr int kGRounds = kChunk / kGBlock;  // group kernel rounds of 64 packets per wave per chunk
 constexpr uint32_t kMaxParts = 256;  // partitions per batch (part_pkts is a multiple of kChunk)
 constexpr uint32_t kMaxGroupBins = 1024;  // group output supports n_backends + 1 <= 1024
 

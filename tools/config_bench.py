@@ -30,7 +30,7 @@ N_BATCHES = 8
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3,c5")
-    ap.add_argument("--streams", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=4)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     args = ap.parse_args()
@@ -88,18 +88,21 @@ def main():
             step(i)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t_start
-        # classify kernel alone (single stream, events around each launch)
+        # classify kernel alone (single stream, fence-free HIP events around each launch)
+        from bench import KernelTimer
+
         st = sts[0]
-        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        kt = KernelTimer(args.steps)
         for i in range(args.steps):
-            kev[i][0].record(st)
+            kt.start(i, st.cuda_stream)
             step(i, 0, defer=True)
-            kev[i][1].record(st)
+            kt.stop(i, st.cuda_stream)
             mgs[0].finish_group(st.cuda_stream)
         torch.cuda.synchronize()
         for mg in mgs:
             mg.check()
-        kus = float(np.mean([a.elapsed_time(b) for a, b in kev])) * 1e3
+        kus = float(kt.ms().mean()) * 1e3
+        kt.close()
         mpps = BATCH * args.steps / elapsed / 1e6
         line = {"config": cfg, "mpps": round(mpps, 1), "us_per_batch": round(elapsed / args.steps * 1e6, 2),
                 "streams": S, "batch_pkts": BATCH, "backends": nbk, "table_size": m,

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--only", default="", help="comma-separated substrings of variant names to run")
     ap.add_argument("--no-multistream", action="store_true")
     ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS for every variant")
+    ap.add_argument("--streams", default="2,3,4", help="stream counts of the multi-stream variants")
     args = ap.parse_args()
     import torch
 
@@ -76,7 +77,7 @@ def main():
     }
     # multi-stream: independent batches in flight on S streams, one handle (scratch) per stream
     extra = {}
-    for S in (() if args.no_multistream else (2, 3, 4)):
+    for S in (() if args.no_multistream else tuple(int(x) for x in args.streams.split(","))):
         mgs = [nb.Maglev(names, args.m) for _ in range(S)]
         sts = [torch.cuda.Stream(dev) for _ in range(S)]
         outs = [(torch.empty(n, dtype=torch.uint16, device=dev), torch.empty(n, dtype=torch.uint32, device=dev),
