@@ -144,9 +144,16 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
   return lookup<LUTM, F4>(a, lut_lds, lo, hi);
 }
 
-__device__ __forceinline__ uint4 ldg16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
-// Non-temporal 16-B store: in-place window write-back streams ~10 % faster with nt (tools/membench).
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+#ifdef NBG_NT_LOADS  // measurement build: packet windows are read once, so try the streaming policy
+__device__ __forceinline__ uint4 ldg16(const uint8_t* p) {
+  const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(w.x, w.y, w.z, w.w);
+}
+#else
+__device__ __forceinline__ uint4 ldg16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+#endif
+// Non-temporal 16-B store: in-place window write-back streams ~10 % faster with nt (tools/membench).
 __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
   const u32x4_t w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
@@ -244,13 +251,117 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
   for (int k = 0; k < 4; ++k) t.ch[k] = ldg16(addr[k]);
 }
 
-// classify_kernel: each wave walks `tiles_per_wave` consecutive 64-packet tiles (1 with the L2
-// LUT: occupancy hides the latency; more with the LDS-staged LUT, to amortise the staging).  Per
+#ifdef NBG_CPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch
+constexpr uint32_t kProbeWaves = 1u << 15;
+__device__ unsigned long long g_cprobe[kProbeWaves * 4];
+#define CPROBE(k)                                                                      \
+  if (lane == 0 && gw < kProbeWaves) g_cprobe[gw * 4 + (k)] = wall_clock64();
+#else
+#define CPROBE(k)
+#endif
+
+// One transposed 64-packet tile of classify_kernel (its loads in `cur`, its chunks 0..2 in the
+// wave's LDS rows `xp`): classify each lane's packet, write back, count.  Packets off the fast
+// path are classified after this tile's loads, stores and gathers are all issued (`slow`): their
+// byte-wise loads would otherwise make the compiler wait for every outstanding load.
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL>
+__device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8_t* lut_lds, const uint8_t* xp,
+                                              uint32_t* hist, uint32_t lane, uint32_t part, uint32_t quad,
+                                              uint32_t wbase, const TileMeta& meta, const TileRegs& cur) {
+  constexpr bool desc = LAYOUT == kDesc;
+  const uint32_t p_own = wbase + lane;
+  // compute lane: one packet (issues the LUT / LPM gathers)
+  uint32_t bin = a.nb, gate = kSentinel, iplo = 0;
+  bool resolve = false;  // CHAIN fast path: `gate` holds the raw tbl24 entry until consumed
+  bool slow = false;
+  uint8_t* pown = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, lane, meta.off));
+  if (p_own < a.n_pkts) {
+    const uint8_t* x = xp + lane * kXStride;
+    const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
+    const bool aligned = LAYOUT == kLean || (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
+    const bool longf = LAYOUT == kLean || meta.len >= 48u;
+    // same decision as the loader lanes: chunks 0..2 were loaded (and, if swapping, get written)
+    if (aligned && longf && ((w3 >> 16) & 0xfu) == 5u) {
+      const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
+      const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
+      // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
+      const uint32_t src = (c1.z >> 16) | (c1.w << 16);
+      const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
+      const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
+      if constexpr (ABL == 1) {
+        bin = (src ^ dst ^ ports) % a.nb;
+      } else if constexpr (ABL == 3) {
+        uint32_t lo, hi;
+        fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+        bin = mod_f4(lo, hi) % a.nb;
+      } else if constexpr (ABL == 4) {
+        bin = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
+      } else {
+        uint32_t lo, hi;
+        if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
+          const uint32_t ip = __builtin_bswap32(src);
+          gate = a.tbl24[ip >> 8];
+          iplo = ip & 0xffu;
+          resolve = true;
+        }
+        fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+        bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
+      }
+    } else {
+      slow = true;
+    }
+  }
+  // MAC swap in the loader lanes + window write-back (fast-path packets only)
+  if (a.swap) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
+      const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(cur.ch[k].w), lane & ~3u));
+      const bool fast = ((cur.cflag >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
+      const uint32_t src = k * 16u + quad;
+      const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(meta.off), src)) : 0u;
+      if (!fast) continue;
+      uint8_t* base = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, src, o));
+      uint4 v = cur.ch[k];
+      if (part == 0u) {
+        const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
+        // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
+        v = make_uint4((w1 >> 16) | (w2 << 16), (w2 >> 16) | (w0 << 16), (w0 >> 16) | (w1 << 16), v.w);
+      }
+      if (a.mac_out) {
+        // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
+        if (part == 0u) {
+          uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(wbase + src) * 12u);
+          mo[0] = v.x;
+          mo[1] = v.y;
+          mo[2] = v.z;
+        }
+      } else if (part == 0u || a.wb_full) {
+        stg16_nt(base + part * 16u, v);  // chunks 1..3 unchanged: makes the write whole lines
+      }
+    }
+  }
+  // consume the gathers
+  if (p_own < a.n_pkts) {
+    if (slow) bin = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, meta.len, p_own, gate);
+    if constexpr (CHAIN) {
+      if (resolve && (gate & 0x8000u)) gate = a.tbl_long[((gate & 0x7fffu) << 8) + iplo];
+      a.gate[p_own] = static_cast<uint16_t>(gate);
+      if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
+    }
+    a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+    if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+  }
+}
+
+// classify_kernel: each wave walks `tiles_per_wave` consecutive 64-packet tiles.  L2-gathered LUT:
+// 256-thread blocks, one tile per wave, 8 blocks per CU (occupancy hides the latency; a software
+// pipeline measured no faster there and cost 18 VGPRs).  LDS-staged LUT: one
+// 1024-thread block per CU, up to 4 tiles per wave with two tiles' loads in flight (below).  Per
 // tile: loads, LDS transpose, hash + gathers, then the write-back stores (vmcnt retires in issue
 // order: stores issued before the gathers would delay their use), then the slow-path packets.
 // One LDS histogram per block (two barriers per launch) is flushed once into the block's partition
-// row (the block's 64 * waves * tiles_per_wave packets divide part_pkts).  A software-pipelined variant (next tile's loads issued
-// behind the gathers) measured no faster at high occupancy and cost 18 VGPRs.
+// row (the block's 64 * waves * tiles_per_wave packets divide part_pkts).
 // ABL (diagnostic builds only, selected by NBG_ABL): 1 = no hash/LUT (bin from header bytes);
 // 3 = FNV without the LUT gather; 4 = LUT gather of a trivial hash.
 template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL = 0, int NT = kBlock>
@@ -265,134 +376,100 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
   uint8_t* lut_lds = smem;
   uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + kW * 64u * kXStride);  // per block
-  constexpr bool desc = LAYOUT == kDesc;
+  const uint32_t tpw = a.tiles_per_wave;
+  const uint32_t t0 = (blockIdx.x * kW + wave) * tpw;  // first 64-packet tile of this wave
+#ifdef NBG_CPROBE
+  const uint32_t gw = blockIdx.x * kW + wave;
+  bool first = true;
+#endif
+  CPROBE(0)
 
+  // LDS-staged LUT: one 1024-thread block per CU (4 waves per SIMD) leaves VGPRs for kPf tiles'
+  // loads in flight beside the tile being classified (a ring of kPf + 1 register tiles; the tile
+  // loop is unrolled so that the ring stays in registers).  The first tiles' loads are issued
+  // before the LUT staging, so that its latency hides under theirs.
+  constexpr uint32_t kPf = kLdsLut ? 2u : 0u;
+  constexpr uint32_t kRing = kPf + 1u;
+  constexpr uint32_t kMaxTpw = kLdsLut ? kChunk / (64u * kW) : 1u;
+  TileMeta rm[kRing];
+  TileRegs rt[kRing];
   if constexpr (kLdsLut) {
-    // stage the LUT: all loads issued before the LDS stores (one round trip)
-    const uint4* src = static_cast<const uint4*>(a.lut);
-    uint4* dst = reinterpret_cast<uint4*>(lut_lds);
-    const uint32_t nvec = lut_bytes / 16u;
-    constexpr int kS = 8;
-    for (uint32_t k0 = 0; k0 < nvec; k0 += kS * NT) {
-      uint4 t[kS];
 #pragma unroll
-      for (int j = 0; j < kS; ++j) {
-        const uint32_t k = k0 + j * NT + tid;
-        t[j] = k < nvec ? src[k] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < kS; ++j) {
-        const uint32_t k = k0 + j * NT + tid;
-        if (k < nvec) dst[k] = t[j];
+    for (uint32_t j = 0; j < kPf; ++j) {
+      const uint32_t wb = (t0 + j) * 64u;
+      if (j < tpw && wb < a.n_pkts) {
+        rm[j] = load_meta<LAYOUT>(a, wb, lane);
+        load_tile<LAYOUT>(a, wb, rm[j], part, quad, rt[j]);
       }
     }
-    __syncthreads();
+    constexpr int kS = 8;  // 16 B per thread per slot: up to 128 KiB per 1024-thread block
+    const uint32_t nvec = lut_bytes / 16u;
+    const uint4* src = static_cast<const uint4*>(a.lut);
+    uint4 lt[kS];
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+      const uint32_t k = j * NT + tid;
+      lt[j] = k < nvec ? src[k] : make_uint4(0, 0, 0, 0);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(lut_lds);
+#pragma unroll
+    for (int j = 0; j < kS; ++j) {
+      const uint32_t k = j * NT + tid;
+      if (k < nvec) dst[k] = lt[j];
+    }
   }
   if constexpr (HIST) {
     for (uint32_t b = tid; b < nbins; b += NT) hist[b] = 0;
-    lds_sync();
   }
+  if constexpr (HIST || kLdsLut) lds_sync();
 
-  const uint32_t tpw = a.tiles_per_wave;
-  const uint32_t t0 = (blockIdx.x * kW + wave) * tpw;  // first 64-packet tile of this wave
-  for (uint32_t i = 0; i < tpw; ++i) {
-    const uint32_t wbase = (t0 + i) * 64u;
-    if (wbase >= a.n_pkts) break;  // wave-uniform
-    const uint32_t p_own = wbase + lane;
-    const TileMeta meta = load_meta<LAYOUT>(a, wbase, lane);
-    TileRegs cur;
-    load_tile<LAYOUT>(a, wbase, meta, part, quad, cur);
-    // transpose: chunks 0..2 -> LDS [packet][80 B]
+  // transpose: chunks 0..2 of each packet of a tile -> LDS [packet][kXStride B]
+  auto transpose = [&](const TileRegs& cur) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (part < 3u) *reinterpret_cast<uint4*>(xp + (k * 16u + quad) * kXStride + part * 16u) = cur.ch[k];
     }
-    // compute lane: one packet (issues the LUT / LPM gathers).  Packets off the fast path are
-    // classified after this tile's loads, stores and gathers are all issued (`slow` below): their
-    // byte-wise loads would otherwise make the compiler wait for every outstanding load here.
-    uint32_t bin = a.nb, gate = kSentinel, iplo = 0;
-    bool resolve = false;  // CHAIN fast path: `gate` holds the raw tbl24 entry until consumed
-    bool slow = false;
-    uint8_t* pown = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, lane, meta.off));
-    if (p_own < a.n_pkts) {
-      const uint8_t* x = xp + lane * kXStride;
-      const uint32_t w3 = *reinterpret_cast<const uint32_t*>(x + 12);
-      const bool aligned = LAYOUT == kLean || (reinterpret_cast<uintptr_t>(pown) & 15u) == 0;
-      const bool longf = LAYOUT == kLean || meta.len >= 48u;
-      // same decision as the loader lanes: chunks 0..2 were loaded (and, if swapping, get written)
-      if (aligned && longf && ((w3 >> 16) & 0xfu) == 5u) {
-        const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
-        const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
-        // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
-        const uint32_t src = (c1.z >> 16) | (c1.w << 16);
-        const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
-        const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
-        if constexpr (ABL == 1) {
-          bin = (src ^ dst ^ ports) % a.nb;
-        } else if constexpr (ABL == 3) {
-          uint32_t lo, hi;
-          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-          bin = mod_f4(lo, hi) % a.nb;
-        } else if constexpr (ABL == 4) {
-          bin = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
-        } else {
-          uint32_t lo, hi;
-          if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
-            const uint32_t ip = __builtin_bswap32(src);
-            gate = a.tbl24[ip >> 8];
-            iplo = ip & 0xffu;
-            resolve = true;
-          }
-          fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-          bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
-        }
-      } else {
-        slow = true;
-      }
-    }
-    // MAC swap in the loader lanes + window write-back (fast-path packets only)
-    if (a.swap) {
+  };
+
+
+  if constexpr (kPf > 0) {
+    // tile i sits in ring slot i % kRing; after its transpose, tile i + kPf is loaded into the
+    // slot tile i - 1 used
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
-        const uint32_t w3 = static_cast<uint32_t>(__shfl(static_cast<int>(cur.ch[k].w), lane & ~3u));
-        const bool fast = ((cur.cflag >> k) & 1u) && ((w3 >> 16) & 0xfu) == 5u;
-        const uint32_t src = k * 16u + quad;
-        const uint32_t o = desc ? static_cast<uint32_t>(__shfl(static_cast<int>(meta.off), src)) : 0u;
-        if (!fast) continue;
-        uint8_t* base = const_cast<uint8_t*>(pkt_addr<LAYOUT>(a, wbase, src, o));
-        uint4 v = cur.ch[k];
-        if (part == 0u) {
-          const uint32_t w0 = v.x, w1 = v.y, w2 = v.z;
-          // new bytes 0..5 = old 6..11, new 6..11 = old 0..5
-          v = make_uint4((w1 >> 16) | (w2 << 16), (w2 >> 16) | (w0 << 16), (w0 >> 16) | (w1 << 16), v.w);
-        }
-        if (a.mac_out) {
-          // egress rewrite record: the 12 swapped bytes, dense (packet bytes untouched)
-          if (part == 0u) {
-            uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(wbase + src) * 12u);
-            mo[0] = v.x;
-            mo[1] = v.y;
-            mo[2] = v.z;
-          }
-        } else if (part == 0u || a.wb_full) {
-          stg16_nt(base + part * 16u, v);  // chunks 1..3 unchanged: makes the write whole lines
-        }
+    for (uint32_t i = 0; i < kMaxTpw; ++i) {
+      const uint32_t wbase = (t0 + i) * 64u;
+      if (i >= tpw || wbase >= a.n_pkts) break;  // wave-uniform
+      transpose(rt[i % kRing]);
+#ifdef NBG_CPROBE
+      if (first) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); CPROBE(1) first = false; }
+#endif
+      const uint32_t j = i + kPf, wb = (t0 + j) * 64u;
+      if (j < tpw && wb < a.n_pkts) {
+        rm[j % kRing] = load_meta<LAYOUT>(a, wb, lane);
+        load_tile<LAYOUT>(a, wb, rm[j % kRing], part, quad, rt[j % kRing]);
       }
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, rm[i % kRing],
+                                                           rt[i % kRing]);
     }
-    // consume the gathers
-    if (p_own < a.n_pkts) {
-      if (slow) bin = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, meta.len, p_own, gate);
-      if constexpr (CHAIN) {
-        if (resolve && (gate & 0x8000u)) gate = a.tbl_long[((gate & 0x7fffu) << 8) + iplo];
-        a.gate[p_own] = static_cast<uint16_t>(gate);
-        if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
-      }
-      a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-      if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+  } else {
+    for (uint32_t i = 0; i < tpw; ++i) {
+      const uint32_t wbase = (t0 + i) * 64u;
+      if (wbase >= a.n_pkts) break;  // wave-uniform
+      const TileMeta meta = load_meta<LAYOUT>(a, wbase, lane);
+      TileRegs cur;
+      load_tile<LAYOUT>(a, wbase, meta, part, quad, cur);
+      transpose(cur);
+#ifdef NBG_CPROBE
+      if (first) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); CPROBE(1) first = false; }
+#endif
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, meta, cur);
     }
   }
 
+#ifdef NBG_CPROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gathers and stores are done
+#endif
+  CPROBE(2)
   if constexpr (HIST) {
     // one flush per block into its partition row (the block's packets never straddle two):
     // 4096-packet rows take ~16 blocks' adds, so they rarely contend
@@ -403,6 +480,7 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
       if (h) atomicAdd(&row[b], h);
     }
   }
+  CPROBE(3)
 }
 
 // Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
@@ -723,6 +801,7 @@ int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, kDesc, 0, NT>
                   : (a.lean ? classify_kernel<LUTM, F4, HIST, CHAIN, kLean, 0, NT>
                             : classify_kernel<LUTM, F4, HIST, CHAIN, kFixed, 0, NT>);
+
   hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
@@ -866,3 +945,11 @@ int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int
 }
 
 }  // namespace nbg
+
+#ifdef NBG_CPROBE
+// Diagnostic builds only (not part of include/nbgpu.h): the per-wave timestamps of the last launch.
+extern "C" int nbg_debug_cprobe(unsigned long long* out, uint64_t n) {
+  if (n > nbg::kProbeWaves * 4) n = nbg::kProbeWaves * 4;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_cprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
+}
+#endif

@@ -21,7 +21,8 @@ int build_lpm(const uint32_t* prefixes, const uint8_t* lens, const uint16_t* gat
 // Kernel geometry.
 constexpr int kBlock = 256;          // classify threads per workgroup (4 waves), L2-gather LUT
 constexpr int kLdsBlock = 1024;      // classify threads per workgroup with the LDS-staged LUT (1 per CU)
-constexpr int kXStride = 80;         // LDS bytes per packet in the transpose (64 + 16: conflict-free b128)
+constexpr int kXStride = 48;         // LDS bytes per packet in the transpose: chunks 0..2 (a 12-dword row
+                                     // stride keeps the b128 reads conflict-free; 8 blocks fit per CU)
 #ifndef NBG_GBLOCK
 #define NBG_GBLOCK 512
 #endif

@@ -100,9 +100,11 @@ def _mixed_sources(buf, off, n, seed):
         buf[off.astype(np.int64) + 26 + k] = b[:, k]
 
 
-@pytest.mark.parametrize("mode,n", [(0, 1 << 20), (1, 262144), (1, 1000)])
-def test_chain_vs_oracle_at_size(torch_cuda, tables, mode, n):
-    """C2 layout (fixed 64-B slots) at full size and the IMIX descriptor layout of config C5."""
+@pytest.mark.parametrize("mode,n,lut_lds", [(0, 1 << 20, False), (1, 262144, False), (1, 1000, False),
+                                            (0, 1 << 20, True), (1, 262144, True)])
+def test_chain_vs_oracle_at_size(torch_cuda, tables, mode, n, lut_lds):
+    """C2 layout (fixed 64-B slots) at full size and the IMIX descriptor layout of config C5
+    (L2-gathered and LDS-staged Maglev LUT)."""
     import netbricks_amd as nb
 
     torch = torch_cuda
@@ -110,7 +112,7 @@ def test_chain_vs_oracle_at_size(torch_cuda, tables, mode, n):
     buf, off, ln = nb.make_trace(n, mode, seed=99 + mode)
     _mixed_sources(buf, off, n, seed=n)
     kw = dict(stride=64, frame_len=60) if mode == 0 else dict(offsets=off, lens=ln, owned_windows=True)
-    got = _chain(torch, mg, t["mixed"], buf, n, **kw)
+    got = _chain(torch, mg, t["mixed"], buf, n, lut_lds=lut_lds, **kw)
     rc, t24, tl = orc.lpm_build(ROUTES["mixed"])
     assert rc == 0
     lut = orc.lut_build(NAMES65, 65537)

@@ -70,14 +70,16 @@ def test_c2_small(torch_cuda, mg65, n, lut_lds):
     _assert_same(got, _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
 
 
-def test_c2_full_1m(torch_cuda, mg65):
-    """BASELINE config C2 size: 1,048,576 x 64-B frames, 65 backends, M=65537."""
+@pytest.mark.parametrize("lut_lds", [False, True])
+def test_c2_full_1m(torch_cuda, mg65, lut_lds):
+    """BASELINE config C2 size: 1,048,576 x 64-B frames, 65 backends, M=65537 (L2-gathered LUT, and
+    the LDS-staged LUT whose waves keep two tiles' loads in flight)."""
     from netbricks_amd import make_trace
 
     n = 1 << 20
     buf, _, _ = make_trace(n, 0)
     lut = orc.lut_build(NAMES65, 65537)
-    got = _run(torch_cuda, mg65, buf, n)
+    got = _run(torch_cuda, mg65, buf, n, lut_lds=lut_lds)
     exp = _oracle(buf, n, lut, 65, stride=64, fixed_len=60)
     _assert_same(got, exp)
     # size-independent properties: perm is a permutation, groups sorted, counts sum to n
@@ -115,9 +117,11 @@ def test_reference_names_lut3(torch_cuda):
     mg.close()
 
 
-@pytest.mark.parametrize("nb,m", [(1000, 655373), (300, 65537), (2, 7), (257, 1009)])
-def test_imix_descriptors(torch_cuda, nb, m):
-    """C3-like: IMIX frames at 64-B aligned offsets with a length array; wide/global LUTs."""
+@pytest.mark.parametrize("lut_lds", [False, True])
+@pytest.mark.parametrize("nb,m", [(1000, 655373), (300, 65537), (2, 7), (257, 1009), (65, 65537)])
+def test_imix_descriptors(torch_cuda, nb, m, lut_lds):
+    """C3-like: IMIX frames at 64-B aligned offsets with a length array; wide/global LUTs (the LDS
+    flag stages the LUTs that fit: u8 65537, u16 1009, u8 7)."""
     from netbricks_amd import Maglev, make_trace
 
     names = [f"be{i}" for i in range(nb)]
@@ -125,7 +129,7 @@ def test_imix_descriptors(torch_cuda, nb, m):
     n = 20000
     buf, off, ln = make_trace(n, 1, seed=nb)
     lut = orc.lut_build(names, m)
-    got = _run(torch_cuda, mg, buf, n, offs=off, lens=ln)
+    got = _run(torch_cuda, mg, buf, n, offs=off, lens=ln, lut_lds=lut_lds)
     _assert_same(got, _oracle(buf, n, lut, nb, offs=off, lens=ln))
     mg.close()
 

@@ -2,7 +2,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 9
 R0="$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
