@@ -583,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 template <int SCAN>
 __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
 #ifdef NBG_GPROBE
-  uint64_t gpt[10] = {};
+  uint64_t gpt[12] = {};
 #endif
   extern __shared__ __align__(16) uint32_t gs[];
   __shared__ uint32_t s_wave[kGBlock / 64];
@@ -607,10 +607,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
   {
     const uint32_t wb = pbeg + wave * (64u * kGRounds);
 #pragma unroll
-    for (int r = 0; r < kGRounds; ++r) {
-      const uint32_t i = wb + r * 64u + lane;
-      pre_bin[r] = (a.perm && i < pend) ? a.backend[i] : 0u;
-    }
+    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = a.backend[min(wb + r * 64u + lane, a.n_pkts - 1u)];
   }
   GPROBE(1)
   // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
@@ -631,14 +628,11 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
         uint32_t h[kU];
 #pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) {
-          const uint32_t q = q0 + k * L;
-          h[k] = q < a.n_parts ? a.part_hist[q * nbins + b] : 0u;
-        }
+        for (uint32_t k = 0; k < kU; ++k) h[k] = a.part_hist[min(q0 + k * L, a.n_parts - 1u) * nbins + b];
 #pragma unroll
         for (uint32_t k = 0; k < kU; ++k) {
           pre += q0 + k * L < c ? h[k] : 0u;
-          all += h[k];
+          all += q0 + k * L < a.n_parts ? h[k] : 0u;
         }
       }
       if (pre) atomicAdd(&base[b], pre);
@@ -701,27 +695,30 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
   }
   lds_sync();
   GPROBE(3)
-  // the next call accumulates into the other buffer: zero it (every block a slice; nothing in
-  // this kernel waits for these stores)
-  for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
-  if (!a.perm) return;
+  // The next call accumulates into the other histogram buffer: every block zeroes a slice of it,
+  // last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the first wait
+  // for a backend load would also wait for them (the counter retires in issue order).
+  auto zero_next = [&] {
+    for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
+  };
+  if (!a.perm) {
+    zero_next();
+    return;
+  }
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   uint32_t* mycnt = cnt + wave * nbins;
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
     for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
     lds_sync();
+    GPROBE(9)
     uint32_t bins[kGRounds], ranks[kGRounds];
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
-      uint32_t bin = 0;
-      if (valid) {
-        const uint32_t v = cbase == pbeg ? pre_bin[r] : a.backend[i];
-        bin = v == NBG_SENTINEL ? a.nb : v;
-      }
+      const uint32_t bin = valid ? (pre_bin[r] == NBG_SENTINEL ? a.nb : pre_bin[r]) : 0u;
       unsigned long long eq = __ballot(valid);
       for (uint32_t bit = 0; bit < a.bits; ++bit) {
         const bool set = (bin >> bit) & 1u;
@@ -736,6 +733,14 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       }
       bins[r] = valid ? bin : 0xffffffffu;
       ranks[r] = rank;
+    }
+    GPROBE(10)
+    // the next chunk's backends (partitions of more than one chunk): loaded now, behind this
+    // chunk's scans and stores
+    if (cbase + kChunk < pend) {
+#pragma unroll
+      for (int r = 0; r < kGRounds; ++r)
+        pre_bin[r] = a.backend[min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u)];
     }
     lds_sync();
     GPROBE(4)
@@ -784,10 +789,13 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
     lds_sync();
   }
+  zero_next();
   GPROBE(8)
 #ifdef NBG_GPROBE
   if (tid == 0 && (c == 0 || c == gridDim.x / 2 || c == gridDim.x - 1))
-    printf("GPROBE blk %u t0 %llu d: %llu %llu %llu %llu %llu %llu %llu %llu\n", c, (unsigned long long)gpt[0],
+    printf("GPROBE blk %u split %llu %llu %llu t0 %llu d: %llu %llu %llu %llu %llu %llu %llu %llu\n", c,
+           (unsigned long long)(gpt[9] - gpt[3]), (unsigned long long)(gpt[10] - gpt[9]),
+           (unsigned long long)(gpt[4] - gpt[10]), (unsigned long long)gpt[0],
            (unsigned long long)(gpt[1] - gpt[0]), (unsigned long long)(gpt[2] - gpt[1]),
            (unsigned long long)(gpt[3] - gpt[2]), (unsigned long long)(gpt[4] - gpt[3]),
            (unsigned long long)(gpt[5] - gpt[4]), (unsigned long long)(gpt[6] - gpt[5]),
