@@ -135,6 +135,24 @@ int nbg_maglev_check(nbg_maglev* h);
 int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                              uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out);
 
+/*
+ * The same, pipelined: nbg_maglev_host_submit gathers the batch's header windows into one of the
+ * handle's NBG_HOST_SLOTS pinned staging slots (host worker threads), queues the H2D copy, the
+ * kernels and the D2H copy, and returns a ticket without waiting; nbg_maglev_host_wait(ticket)
+ * waits for that batch, stores its results in the buffers given to the submit and writes the
+ * swapped MACs into its mbufs.  So a producer gathers batch i+1 while batch i crosses PCIe and
+ * runs.  Windows are 48 B when every frame longer than 48 B has IHL <= 7 (64 or 80 B otherwise).
+ * Batches of one handle are classified in submit order.  A submit into a slot whose batch was
+ * not waited for completes that batch first.  Everything a submit names (mbufs, lens, outputs)
+ * must stay valid until its wait returns (or the slot is reused).  Replaces a sequence of
+ * GroupByProducer::execute calls over host mbufs (operators/group_by.rs:43-55).
+ */
+#define NBG_HOST_SLOTS 3
+int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
+                           uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out,
+                           uint64_t* ticket);
+int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket);
+
 
 /* ---- chained NF: test/lpm -> test/maglev (BASELINE config C5) ------------- */
 

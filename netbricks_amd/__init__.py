@@ -4,9 +4,9 @@ The hot path (parse + MAC swap + 5-tuple FNV-1a + Maglev LUT + per-backend FIFO
 grouping; optionally chained after test/lpm's DIR-24-8 gate) is hand-written HIP for gfx950 in `csrc/`, exported through the C-ABI in
 `include/nbgpu.h` (`libnbgpu.so`).  This package is a thin Python surface over it.
 """
-from ._lib import NBG_SENTINEL, NbgError, LIB_PATH  # noqa: F401  (raises ImportError if the .so is missing)
+from ._lib import NBG_HOST_SLOTS, NBG_SENTINEL, NbgError, LIB_PATH  # noqa: F401  (raises ImportError if the .so is missing)
 from .maglev import GroupedBatch, Maglev, build_lut, make_trace  # noqa: F401
 from .lpm import Lpm, LpmResult, build_lpm, chain_lpm_maglev  # noqa: F401
 
-__all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL", "NbgError", "LIB_PATH",
+__all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL", "NBG_HOST_SLOTS", "NbgError", "LIB_PATH",
            "Lpm", "LpmResult", "build_lpm", "chain_lpm_maglev"]

@@ -19,6 +19,7 @@ NBG_LUT_LDS = 0x2
 NBG_OWNED_WINDOWS = 0x4
 NBG_WB_PARTIAL = 0x8
 NBG_DEFER_GROUP = 0x10
+NBG_HOST_SLOTS = 3
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
@@ -40,6 +41,8 @@ SIGNATURES = {
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
+    "nbg_maglev_host_submit": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, C.POINTER(C.c_uint64)]),
+    "nbg_maglev_host_wait": (C.c_int, [_P, C.c_uint64]),
     "nbg_lpm_create": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P)]),
     "nbg_lpm_destroy": (None, [_P]),
     "nbg_lpm_lookup_device": (C.c_int, [_P, _P, C.c_uint64, _P, _P]),

@@ -7,6 +7,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -76,18 +79,37 @@ struct nbg_maglev {
   uint16_t* d_fixed_len = nullptr;
   uint64_t fixed_len_cap = 0;
   uint16_t fixed_len_val = 0;
-  // host-path staging (pinned host + device)
-  uint64_t host_cap = 0;
-  uint32_t host_win = 0;
-  uint8_t* h_win = nullptr;
-  uint16_t* h_len = nullptr;
-  uint8_t* h_mac = nullptr;
-  uint8_t* d_win = nullptr;
-  uint8_t* d_mac = nullptr;
-  uint16_t* d_len = nullptr;
-  uint16_t* d_backend = nullptr;
-  uint32_t* d_perm = nullptr;
-  hipStream_t host_stream = nullptr;
+  // host path (PCIe): NBG_HOST_SLOTS staging slots, one batch in flight per slot
+  struct HostSlot {
+    uint64_t cap = 0;          // packets the buffers hold
+    uint8_t* h_win = nullptr;  // pinned: windows (cap * 80 B + 64 B of slack for the last chunk load)
+    uint16_t* h_len = nullptr;
+    uint8_t* h_mac = nullptr;  // pinned: 12-B swapped-MAC records
+    uint16_t* h_backend = nullptr;
+    uint32_t* h_perm = nullptr;
+    uint32_t* h_counts = nullptr;
+    uint8_t* d_win = nullptr;
+    uint16_t* d_len = nullptr;
+    uint8_t* d_mac = nullptr;
+    uint16_t* d_backend = nullptr;
+    uint32_t* d_perm = nullptr;
+    uint32_t* d_counts = nullptr;
+    hipStream_t copy = nullptr;  // H2D and D2H of this slot
+    hipEvent_t staged = nullptr, classified = nullptr, done = nullptr;
+    bool busy = false;
+    uint64_t ticket = 0;
+    // the submitted batch (the caller keeps these valid until its wait)
+    uint8_t* const* pkt_ptrs = nullptr;
+    const uint16_t* lens = nullptr;
+    uint64_t n = 0;
+    bool swap = false;
+    uint16_t* backend_out = nullptr;
+    uint32_t* perm_out = nullptr;
+    uint32_t* counts_out = nullptr;
+  };
+  HostSlot slots[NBG_HOST_SLOTS];
+  hipStream_t host_compute = nullptr;  // the classify and group kernels of every slot, in submit order
+  uint64_t next_ticket = 1;
 };
 
 namespace {
@@ -117,25 +139,39 @@ void free_scratch(nbg_maglev* h) {
   h->d_counts = nullptr;
 }
 
+void free_slot_buffers(nbg_maglev::HostSlot& t) {
+  (void)hipHostFree(t.h_win);
+  (void)hipHostFree(t.h_len);
+  (void)hipHostFree(t.h_mac);
+  (void)hipHostFree(t.h_backend);
+  (void)hipHostFree(t.h_perm);
+  (void)hipHostFree(t.h_counts);
+  (void)hipFree(t.d_win);
+  (void)hipFree(t.d_len);
+  (void)hipFree(t.d_mac);
+  (void)hipFree(t.d_backend);
+  (void)hipFree(t.d_perm);
+  (void)hipFree(t.d_counts);
+  t.h_win = t.h_mac = t.d_win = t.d_mac = nullptr;
+  t.h_len = t.d_len = t.h_backend = t.d_backend = nullptr;
+  t.h_perm = t.h_counts = t.d_perm = t.d_counts = nullptr;
+  t.cap = 0;
+}
+
 void free_host_path(nbg_maglev* h) {
-  (void)hipHostFree(h->h_win);
-  (void)hipHostFree(h->h_len);
-  (void)hipHostFree(h->h_mac);
-  (void)hipFree(h->d_win);
-  (void)hipFree(h->d_mac);
-  (void)hipFree(h->d_len);
-  (void)hipFree(h->d_backend);
-  (void)hipFree(h->d_perm);
-  h->h_win = nullptr;
-  h->h_len = nullptr;
-  h->h_mac = nullptr;
-  h->d_win = nullptr;
-  h->d_mac = nullptr;
-  h->d_len = nullptr;
-  h->d_backend = nullptr;
-  h->d_perm = nullptr;
-  h->host_cap = 0;
-  h->host_win = 0;
+  for (auto& t : h->slots) {
+    if (t.busy && t.done) (void)hipEventSynchronize(t.done);
+    t.busy = false;
+    free_slot_buffers(t);
+    if (t.copy) (void)hipStreamDestroy(t.copy);
+    if (t.staged) (void)hipEventDestroy(t.staged);
+    if (t.classified) (void)hipEventDestroy(t.classified);
+    if (t.done) (void)hipEventDestroy(t.done);
+    t.copy = nullptr;
+    t.staged = t.classified = t.done = nullptr;
+  }
+  if (h->host_compute) (void)hipStreamDestroy(h->host_compute);
+  h->host_compute = nullptr;
 }
 
 int upload(nbg_maglev* h) {
@@ -173,25 +209,71 @@ bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
   return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024;
 }
 
-// Run fn(begin, end) over [0, n) on up to 8 host threads (large batches only: the gather of
-// scattered mbuf windows is bound by host memory latency, not bandwidth).
+// Persistent host worker pool for the host path's gather and MAC write-back (bound by host
+// memory latency over scattered mbufs, not bandwidth): up to 16 threads (the GPU box's CPU share), started on first use and
+// kept for the life of the process (no thread start per batch).  One job at a time.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* pool = new HostPool();  // never destroyed: its workers live as long as the process
+    return *pool;
+  }
+  // fn(begin, end) over [0, n) split into one contiguous part per thread (the caller runs one)
+  void run(uint64_t n, const std::function<void(uint64_t, uint64_t)>& fn) {
+    if (n < 32768 || workers_ == 0) {
+      fn(0, n);
+      return;
+    }
+    std::lock_guard<std::mutex> job_lock(job_mutex_);
+    const unsigned parts = workers_ + 1;
+    const uint64_t per = (n + parts - 1) / parts;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = [&](unsigned k) {
+        const uint64_t b = std::min(n, k * per), e = std::min(n, b + per);
+        if (b < e) fn(b, e);
+      };
+      pending_ = workers_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    job_(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_cv_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  HostPool() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    workers_ = (hw ? std::min(hw, 16u) : 1u) - 1;
+    for (unsigned k = 1; k <= workers_; ++k) std::thread([this, k] { loop(k); }).detach();
+  }
+  void loop(unsigned k) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void(unsigned)> job;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        job = job_;
+      }
+      job(k);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_cv_.notify_one();
+    }
+  }
+  unsigned workers_ = 0;
+  std::mutex job_mutex_, m_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(unsigned)> job_;
+  unsigned pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
 template <typename F>
 void parallel_for(uint64_t n, F fn) {
-  const unsigned hw = std::thread::hardware_concurrency();
-  unsigned t = hw ? std::min(hw, 8u) : 1u;
-  if (n < 32768) t = 1;
-  if (t <= 1) {
-    fn(uint64_t(0), n);
-    return;
-  }
-  std::vector<std::thread> pool;
-  const uint64_t per = (n + t - 1) / t;
-  for (unsigned k = 1; k < t; ++k) {
-    const uint64_t b = k * per, e = std::min(n, b + per);
-    if (b < e) pool.emplace_back([=] { fn(b, e); });
-  }
-  fn(uint64_t(0), std::min(n, per));
-  for (auto& th : pool) th.join();
+  HostPool::get().run(n, std::function<void(uint64_t, uint64_t)>(fn));
 }
 
 int finish_create(nbg_maglev* h, int device, nbg_maglev** out) {
@@ -261,7 +343,6 @@ void nbg_maglev_destroy(nbg_maglev* h) {
     free_scratch(h);
     free_host_path(h);
     (void)hipFree(h->d_lut);
-    if (h->host_stream) (void)hipStreamDestroy(h->host_stream);
   }
   delete h;
 }
@@ -527,75 +608,167 @@ int nbg_maglev_check(nbg_maglev* h) {
   return NBG_OK;
 }
 
-int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
-                             uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out) {
-  if (!h || (!pkt_ptrs && n) || (!lens && n) || (!backend_out && n))
-    return set_error(NBG_EINVAL, "classify_host: null argument");
-  if (n >= (1ull << 30)) return set_error(NBG_EINVAL, "classify_host: n must be < 2^30");
-  DeviceGuard g(h->device);
-  if (!h->host_stream) NBG_HIP(hipStreamCreateWithFlags(&h->host_stream, hipStreamNonBlocking));
-  if (n == 0) {
-    if (counts_out) std::memset(counts_out, 0, (h->nb + 1) * sizeof(uint32_t));
-    return NBG_OK;
-  }
-  // Header window per packet: bytes the path can read = 14 + max(20, 4*IHL + 4) <= 78.
-  std::atomic<uint32_t> need{64};
+}  // extern "C"
+
+namespace {
+
+// Stage the header windows of a host batch at a `win`-byte stride (the first min(len, win) bytes of
+// every frame) and return the stride the batch needs: the path reads 14 + max(20, 4*IHL + 4)
+// bytes (utils/flow.rs:53-62) — 38 for IHL 5 — so 48-B windows (three 16-B chunks) serve every
+// frame longer than 48 B with IHL <= 7; 64 B up to IHL 11, 80 B beyond.  The IHL byte is read from
+// the staged copy, so one pass over the (scattered) mbufs both gathers and sizes; frames shorter
+// than the stride are staged whole and take the kernel's byte-wise path.  Software prefetch runs
+// kAhead frames ahead: the gather is bound by host memory latency, one cache line per mbuf.
+uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint8_t* h_win,
+                     uint16_t* h_len) {
+  constexpr uint64_t kAhead = 16;
+  std::atomic<uint32_t> need{48};
   parallel_for(n, [&](uint64_t b, uint64_t e) {
-    uint32_t m = 64;
+    uint32_t m = 48;
     for (uint64_t i = b; i < e; ++i) {
-      if (lens[i] > 64) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (pkt_ptrs[i][14] & 0xfu) * 4 + 4));
+      if (i + kAhead < e) __builtin_prefetch(pkt_ptrs[i + kAhead], 0, 0);
+      const uint32_t l = lens[i], c = std::min<uint32_t>(l, win);
+      uint8_t* w = h_win + i * win;
+      std::memcpy(w, pkt_ptrs[i], c);
+      h_len[i] = static_cast<uint16_t>(l);
+      if (l > 48) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (w[14] & 0xfu) * 4 + 4));
     }
     uint32_t cur = need.load();
     while (m > cur && !need.compare_exchange_weak(cur, m)) {
     }
   });
-  const uint32_t win = need <= 64 ? 64 : 80;
-  if (n > h->host_cap || win != h->host_win) {
-    free_host_path(h);
-    const uint64_t cap = std::max<uint64_t>(n, 4096);
-    NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_win), cap * win, hipHostMallocDefault));
-    NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_len), cap * 2, hipHostMallocDefault));
-    NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&h->h_mac), cap * 12, hipHostMallocDefault));
-    NBG_HIP(hipMalloc(&h->d_win, cap * win));
-    NBG_HIP(hipMalloc(&h->d_mac, cap * 12));
-    NBG_HIP(hipMalloc(&h->d_len, cap * 2));
-    NBG_HIP(hipMalloc(&h->d_backend, cap * 2));
-    NBG_HIP(hipMalloc(&h->d_perm, cap * 4));
-    h->host_cap = cap;
-    h->host_win = win;
+  const uint32_t m = need.load();
+  return m <= 48 ? 48 : (m <= 64 ? 64 : 80);
+}
+
+int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
+  if (!t.copy) {
+    NBG_HIP(hipStreamCreateWithFlags(&t.copy, hipStreamNonBlocking));
+    NBG_HIP(hipEventCreateWithFlags(&t.staged, hipEventDisableTiming));
+    NBG_HIP(hipEventCreateWithFlags(&t.classified, hipEventDisableTiming));
+    NBG_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
   }
-  uint8_t* h_win = h->h_win;
-  uint16_t* h_len = h->h_len;
-  parallel_for(n, [=](uint64_t b, uint64_t e) {
-    for (uint64_t i = b; i < e; ++i) {
-      const uint32_t c = std::min<uint32_t>(lens[i], win);
-      std::memcpy(h_win + i * win, pkt_ptrs[i], c);
-      h_len[i] = lens[i];
-    }
-  });
-  hipStream_t s = h->host_stream;
-  NBG_HIP(hipMemcpyAsync(h->d_win, h->h_win, n * win, hipMemcpyHostToDevice, s));
-  NBG_HIP(hipMemcpyAsync(h->d_len, h->h_len, n * 2, hipMemcpyHostToDevice, s));
-  uint32_t* d_counts = counts_out || perm_out ? h->d_counts : nullptr;
-  const bool swap = flags & NBG_SWAP_MACS;
-  // the swap comes back as dense 12-B records (no in-place rewrite of the staging windows)
-  int rc = nbg_maglev_classify_device_ex(h, h->d_win, nullptr, h->d_len, win, 0, n, flags | NBG_OWNED_WINDOWS,
-                                         h->d_backend, perm_out ? h->d_perm : nullptr, d_counts,
-                                         swap ? h->d_mac : nullptr, s);
-  if (rc) return rc;
-  NBG_HIP(hipMemcpyAsync(backend_out, h->d_backend, n * 2, hipMemcpyDeviceToHost, s));
-  if (perm_out) NBG_HIP(hipMemcpyAsync(perm_out, h->d_perm, n * 4, hipMemcpyDeviceToHost, s));
-  if (counts_out) NBG_HIP(hipMemcpyAsync(counts_out, h->d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, s));
-  if (swap) NBG_HIP(hipMemcpyAsync(h->h_mac, h->d_mac, n * 12, hipMemcpyDeviceToHost, s));
-  NBG_HIP(hipStreamSynchronize(s));
-  if (swap) {
-    const uint8_t* h_mac = h->h_mac;
+  if (n <= t.cap) return NBG_OK;
+  free_slot_buffers(t);
+  const uint64_t cap = std::max<uint64_t>(n, 4096);
+  const size_t nbins = h->nb + 1;
+  const size_t win_bytes = cap * 80 + 64;  // any window stride, + the last packet's 4th chunk
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_win), win_bytes, hipHostMallocDefault));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_len), cap * 2, hipHostMallocDefault));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_mac), cap * 12, hipHostMallocDefault));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_backend), cap * 2, hipHostMallocDefault));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_perm), cap * 4, hipHostMallocDefault));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_counts), nbins * 4, hipHostMallocDefault));
+  NBG_HIP(hipMalloc(&t.d_win, win_bytes));
+  NBG_HIP(hipMalloc(&t.d_len, cap * 2));
+  NBG_HIP(hipMalloc(&t.d_mac, cap * 12));
+  NBG_HIP(hipMalloc(&t.d_backend, cap * 2));
+  NBG_HIP(hipMalloc(&t.d_perm, cap * 4));
+  NBG_HIP(hipMalloc(&t.d_counts, nbins * 4));
+  NBG_HIP(hipMemset(t.d_win, 0, win_bytes));  // the slack past the last window is read, never used
+  t.cap = cap;
+  return NBG_OK;
+}
+
+// Complete the batch held by slot t: wait for its D2H, hand the results to the caller's buffers
+// and write the swapped MACs into the mbufs (the egress rewrite of MacHeader::swap_addresses).
+int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
+  if (!t.busy) return NBG_OK;
+  t.busy = false;
+  NBG_HIP(hipEventSynchronize(t.done));
+  const uint64_t n = t.n;
+  if (t.backend_out) std::memcpy(t.backend_out, t.h_backend, n * 2);
+  if (t.perm_out) std::memcpy(t.perm_out, t.h_perm, n * 4);
+  if (t.counts_out) std::memcpy(t.counts_out, t.h_counts, (h->nb + 1) * 4);
+  if (t.swap) {
+    const uint8_t* h_mac = t.h_mac;
+    uint8_t* const* pkt_ptrs = t.pkt_ptrs;
+    const uint16_t* lens = t.lens;
     parallel_for(n, [=](uint64_t b, uint64_t e) {
-      for (uint64_t i = b; i < e; ++i)
+      for (uint64_t i = b; i < e; ++i) {
+        if (i + 16 < e) __builtin_prefetch(pkt_ptrs[i + 16], 1, 0);
         if (lens[i] >= 14) std::memcpy(pkt_ptrs[i], h_mac + i * 12, 12);
+      }
     });
   }
   return NBG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
+                           uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out,
+                           uint64_t* ticket) {
+  if (!h || !ticket || (!pkt_ptrs && n) || (!lens && n) || (!backend_out && n))
+    return set_error(NBG_EINVAL, "host_submit: null argument");
+  if (n >= (1ull << 30)) return set_error(NBG_EINVAL, "host_submit: n must be < 2^30");
+  if (h->pending) return set_error(NBG_EINVAL, "host_submit: a deferred group is pending (nbg_maglev_finish_group)");
+  DeviceGuard g(h->device);
+  if (!h->host_compute) NBG_HIP(hipStreamCreateWithFlags(&h->host_compute, hipStreamNonBlocking));
+  const uint64_t tk = h->next_ticket;
+  auto& t = h->slots[tk % NBG_HOST_SLOTS];
+  int rc = slot_complete(h, t);  // the slot's previous batch, if its wait has not come yet
+  if (rc) return rc;
+  if ((rc = slot_reserve(h, t, n))) return rc;
+  const bool swap = flags & NBG_SWAP_MACS;
+  t.pkt_ptrs = pkt_ptrs;
+  t.lens = lens;
+  t.n = n;
+  t.swap = swap;
+  t.backend_out = backend_out;
+  t.perm_out = perm_out;
+  t.counts_out = counts_out;
+  t.ticket = tk;
+  h->next_ticket = tk + 1;
+  if (n == 0) {
+    if (counts_out) std::memset(counts_out, 0, (h->nb + 1) * sizeof(uint32_t));
+    *ticket = tk;
+    return NBG_OK;
+  }
+  // gather at 48-B windows; a batch with longer IP headers is staged again at the stride it needs
+  uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len);
+  if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len);
+  // copies on the slot's stream, kernels in submit order on the handle's compute stream (they
+  // share the handle's grouping scratch), results back on the slot's stream
+  NBG_HIP(hipMemcpyAsync(t.d_win, t.h_win, n * win, hipMemcpyHostToDevice, t.copy));
+  NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, t.copy));
+  NBG_HIP(hipEventRecord(t.staged, t.copy));
+  NBG_HIP(hipStreamWaitEvent(h->host_compute, t.staged, 0));
+  const bool group = perm_out || counts_out;
+  rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n,
+                                     (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL)) | NBG_OWNED_WINDOWS, t.d_backend,
+                                     perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr,
+                                     swap ? t.d_mac : nullptr, h->host_compute);
+  if (rc) return rc;
+  NBG_HIP(hipEventRecord(t.classified, h->host_compute));
+  NBG_HIP(hipStreamWaitEvent(t.copy, t.classified, 0));
+  NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, t.copy));
+  if (perm_out) NBG_HIP(hipMemcpyAsync(t.h_perm, t.d_perm, n * 4, hipMemcpyDeviceToHost, t.copy));
+  if (counts_out) NBG_HIP(hipMemcpyAsync(t.h_counts, t.d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, t.copy));
+  if (swap) NBG_HIP(hipMemcpyAsync(t.h_mac, t.d_mac, n * 12, hipMemcpyDeviceToHost, t.copy));
+  NBG_HIP(hipEventRecord(t.done, t.copy));
+  t.busy = true;
+  *ticket = tk;
+  return NBG_OK;
+}
+
+int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket) {
+  if (!h) return set_error(NBG_EINVAL, "host_wait: null handle");
+  if (ticket == 0 || ticket >= h->next_ticket) return set_error(NBG_EINVAL, "host_wait: unknown ticket %llu",
+                                                                (unsigned long long)ticket);
+  auto& t = h->slots[ticket % NBG_HOST_SLOTS];
+  if (t.ticket != ticket) return NBG_OK;  // its slot was reused: the batch was completed then
+  DeviceGuard g(h->device);
+  return slot_complete(h, t);
+}
+
+int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
+                             uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out) {
+  uint64_t tk = 0;
+  int rc = nbg_maglev_host_submit(h, pkt_ptrs, lens, n, flags, backend_out, perm_out, counts_out, &tk);
+  return rc ? rc : nbg_maglev_host_wait(h, tk);
 }
 
 }  // extern "C"

@@ -145,6 +145,26 @@ class Maglev:
             stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
         check(lib.nbg_maglev_finish_group(self._h, stream), "nbg_maglev_finish_group")
 
+    def host_submit(self, ptrs: np.ndarray, lens: np.ndarray, backend: np.ndarray, perm: Optional[np.ndarray] = None,
+                    counts: Optional[np.ndarray] = None, swap_macs: bool = True) -> int:
+        """Pipelined host path (nbg_maglev_host_submit): frame i is `lens[i]` bytes at address
+        `ptrs[i]` (u64 numpy arrays of host mbuf data pointers).  Returns a ticket; backend / perm /
+        counts (numpy) and the frames' MAC swap are complete when host_wait(ticket) returns.  The
+        caller keeps every array (and the frames) alive until then."""
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = ptrs.size
+        ticket = C.c_uint64(0)
+        rc = lib.nbg_maglev_host_submit(self._h, ptrs.ctypes.data, lens.ctypes.data, n,
+                                        NBG_SWAP_MACS if swap_macs else 0, backend.ctypes.data,
+                                        None if perm is None else perm.ctypes.data,
+                                        None if counts is None else counts.ctypes.data, C.byref(ticket))
+        check(rc, "nbg_maglev_host_submit")
+        return ticket.value
+
+    def host_wait(self, ticket: int) -> None:
+        check(lib.nbg_maglev_host_wait(self._h, ticket), "nbg_maglev_host_wait")
+
     def group_by_host(self, frames: Sequence[bytearray], swap_macs: bool = True, group: bool = True):
         """Host mbuf path: frames are mutable byte buffers (their MACs are swapped in place).
         Returns numpy (backend u16[n], perm u32[n] | None, counts u32[nb+1] | None)."""
