@@ -158,6 +158,23 @@ def scatter_shard(global_buf, out, rank: int, world: int) -> None:
         dist.scatter(out, None, src=0)
 
 
+def gather_results(backend, counts, gbuf, gcounts, rank: int, world: int) -> None:
+    """Config C4's return leg: rank 0 collects every shard's backend[] (u16, sent as bytes: RCCL has
+    no 16-bit integer type) and per-group counts (RCCL gather over xGMI on GPUs; gloo in the CPU
+    tests).  Shard-major order == global packet order."""
+    import torch
+    import torch.distributed as dist
+
+    b = backend.view(torch.uint8)
+    c = counts.view(torch.int32)
+    if rank == 0:
+        dist.gather(b, list(gbuf.chunk(world)), dst=0)
+        dist.gather(c, list(gcounts.chunk(world)), dst=0)
+    else:
+        dist.gather(b, None, dst=0)
+        dist.gather(c, None, dst=0)
+
+
 def read_traffic():
     """HBM bytes per classify launch from the committed PMC profile (profiles/pmc_*.json), if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
@@ -267,10 +284,13 @@ def main():
                     buf_r, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(r, 0))
                     glob[r * BATCH * SLOT:(r + 1) * BATCH * SLOT].copy_(torch.from_numpy(buf_r))
             cur = torch.cuda.current_stream(dev).cuda_stream
+            gb = torch.empty(world * BATCH * 2, dtype=torch.uint8, device=dev) if rank == 0 else None
+            gc = torch.empty(world * (N_BACKENDS + 1), dtype=torch.int32, device=dev) if rank == 0 else None
 
             def sstep():
                 scatter_shard(glob, recv, rank, world)
                 mgs[0].group_by(recv, BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True, stream=cur, **outs[0])
+                gather_results(outs[0]["backend"], outs[0]["counts"], gb, gc, rank, world)
 
             for _ in range(3):
                 sstep()
@@ -284,12 +304,15 @@ def main():
             st_el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
             dist.all_reduce(st_el, op=dist.ReduceOp.MAX)
             st_s = float(st_el[0])
+            if rank == 0 and int(gc.sum()) != world * BATCH:
+                raise RuntimeError(f"gathered counts sum {int(gc.sum())} != {world * BATCH}")
             scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
                        "ms_per_step": round(st_s / args.scatter_steps * 1e3, 4), "steps": args.scatter_steps,
                        "root_egress_GBps": round(BATCH * SLOT * (world - 1) * args.scatter_steps / st_s / 1e9, 1),
                        "what": "rank 0 scatters world x 1M 64-B packets (ncclScatter over xGMI), each rank classifies "
-                               "its shard (MAC swap + grouping); single stream per rank"}
-            del recv, glob
+                               "its shard (MAC swap + grouping), rank 0 gathers every shard's backend[] and counts "
+                               "(ncclGather); single stream per rank"}
+            del recv, glob, gb, gc
         except Exception as e:  # informational; the device-resident value above stands on its own
             log(f"[rank {rank}] scatter-inclusive pass failed: {e}")
             scatter = {"error": str(e)[:200]}

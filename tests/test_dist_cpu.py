@@ -55,7 +55,20 @@ def _worker(rank, world, port, out):
     recv = torch.empty(n * 64, dtype=torch.uint8)
     bench.scatter_shard(glob, recv, rank, world)
     scatter_ok = np.array_equal(recv.numpy(), buf)
+    # ... and its return leg: rank 0 gathers every shard's backend[] and group counts
+    be_t = torch.from_numpy(be.astype(np.uint16).view(np.int16).copy())
+    cnt_t = torch.from_numpy(counts.astype(np.uint32).view(np.int32).copy())
+    gb = torch.empty(world * n * 2, dtype=torch.uint8) if rank == 0 else None
+    gc = torch.empty(world * (bench.N_BACKENDS + 1), dtype=torch.int32) if rank == 0 else None
+    bench.gather_results(be_t, cnt_t, gb, gc, rank, world)
+    gather_ok = True
+    if rank == 0:
+        exp_be = np.concatenate([orc.classify(nb.make_trace(n, 0, seed=bench.shard_seed(r, 0))[0], n, lut,
+                                              stride=64, fixed_len=60) for r in range(world)])
+        got_be = gb.numpy().view(np.uint16)
+        gather_ok = np.array_equal(got_be, exp_be) and int(gc.sum()) == world * n
     out[rank] = {"lut_ok": np.array_equal(lut, nb.build_lut(names, bench.TABLE)), "scatter_ok": scatter_ok,
+                 "gather_ok": gather_ok,
                  "same_lut": len({int(d) for d in all_d}) == 1, "counts": c.numpy().tolist(),
                  "first": buf[:64].tobytes()}
     dist.destroy_process_group()
@@ -74,6 +87,7 @@ def test_two_rank_shards_gloo():
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     assert all(out[r]["lut_ok"] and out[r]["same_lut"] and out[r]["scatter_ok"] for r in range(world))
+    assert out[0]["gather_ok"]
     assert out[0]["first"] != out[1]["first"]  # distinct shards
     # global reference: concatenate the shards and group once
     lut = nb.build_lut([f"backend-{i}" for i in range(bench.N_BACKENDS)], bench.TABLE)
