@@ -134,6 +134,32 @@ def test_imix_descriptors(torch_cuda, nb, m, lut_lds):
     mg.close()
 
 
+def test_c3_full_1m(torch_cuda):
+    """BASELINE config C3 size: 1,048,576 IMIX frames (64-B aligned descriptors, in-place swap over
+    owned windows), 1000 backends, M = 655373 (u16 LUT, hist_kernel + scan_kernel grouping)."""
+    from netbricks_amd import Maglev, make_trace
+
+    names = [f"be{i}" for i in range(1000)]
+    mg = Maglev(names, 655373)
+    n = 1 << 20
+    buf, off, ln = make_trace(n, 1, seed=1000)
+    lut = orc.lut_build(names, 655373)
+    dev = torch_cuda.device("cuda:0")
+    d_buf = torch_cuda.from_numpy(buf.copy()).to(dev)
+    d_off = torch_cuda.from_numpy(off.view(np.int32)).to(dev).view(torch_cuda.uint32)
+    d_len = torch_cuda.from_numpy(ln.view(np.int16)).to(dev).view(torch_cuda.uint16)
+    r = mg.group_by(d_buf, n, offsets=d_off, lens=d_len, owned_windows=True)
+    torch_cuda.cuda.synchronize()
+    mg.check()
+    got = (d_buf.cpu().numpy(), r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16),
+           r.perm.view(torch_cuda.int32).cpu().numpy().view(np.uint32),
+           r.counts.view(torch_cuda.int32).cpu().numpy().view(np.uint32))
+    exp = _oracle(buf, n, lut, 1000, offs=off, lens=ln)
+    _assert_same(got, exp)
+    assert got[3].sum() == n and (got[3][:1000] > 0).all()
+    mg.close()
+
+
 def _edge_frames(rng):
     """Hand-built edge cases: IHL 0..15 with options, runts, non-IPv4, odd lengths."""
     frames = []
