@@ -483,6 +483,15 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
   CPROBE(3)
 }
 
+// Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
+// SGPR-base + 32-bit VGPR-offset form (one VGPR per address instead of two).
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
+}
+__device__ __forceinline__ uint32_t ld_u16(const uint16_t* base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
+}
+
 // Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
 // exclusive prefix and the total.
 template <uint32_t NT>
@@ -580,8 +589,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 #else
 #define GPROBE(k)
 #endif
+#ifndef NBG_GROUP_WAVES
+#define NBG_GROUP_WAVES 4  // waves per SIMD the group kernel is compiled for: <= 64 VGPRs, so a resident
+                           // group block leaves the other streams' classify waves their registers
+#endif
 template <int SCAN>
-__global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
+__global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupArgs a) {
 #ifdef NBG_GPROBE
   uint64_t gpt[12] = {};
 #endif
@@ -607,7 +620,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
   {
     const uint32_t wb = pbeg + wave * (64u * kGRounds);
 #pragma unroll
-    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = a.backend[min(wb + r * 64u + lane, a.n_pkts - 1u)];
+    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = ld_u16(a.backend, min(wb + r * 64u + lane, a.n_pkts - 1u) * 2u);
   }
   GPROBE(1)
   // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
@@ -628,7 +641,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
       for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
         uint32_t h[kU];
 #pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) h[k] = a.part_hist[min(q0 + k * L, a.n_parts - 1u) * nbins + b];
+        for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * nbins + b) * 4u);
 #pragma unroll
         for (uint32_t k = 0; k < kU; ++k) {
           pre += q0 + k * L < c ? h[k] : 0u;
@@ -712,7 +725,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
     lds_sync();
     GPROBE(9)
-    uint32_t bins[kGRounds], ranks[kGRounds];
+    uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
@@ -731,8 +744,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
         rank = prior + __popcll(eq & lt);
         if ((eq & lt) == 0) mycnt[bin] = prior + __popcll(eq);
       }
-      bins[r] = valid ? bin : 0xffffffffu;
-      ranks[r] = rank;
+      br[r] = valid ? (rank << 16) | bin : 0xffffffffu;
     }
     GPROBE(10)
     // the next chunk's backends (partitions of more than one chunk): loaded now, behind this
@@ -740,7 +752,7 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     if (cbase + kChunk < pend) {
 #pragma unroll
       for (int r = 0; r < kGRounds; ++r)
-        pre_bin[r] = a.backend[min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u)];
+        pre_bin[r] = ld_u16(a.backend, min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u) * 2u);
     }
     lds_sync();
     GPROBE(4)
@@ -777,10 +789,11 @@ __global__ __launch_bounds__(kGBlock) void group_kernel(GroupArgs a) {
     GPROBE(6)
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
-      if (bins[r] != 0xffffffffu) {
-        const uint32_t j = sub[bins[r]] + mycnt[bins[r]] + ranks[r];
+      if (br[r] != 0xffffffffu) {
+        const uint32_t bin = br[r] & 0xffffu;
+        const uint32_t j = sub[bin] + mycnt[bin] + (br[r] >> 16);
         sidx[j] = wbase + r * 64u + lane;
-        sbin[j] = static_cast<uint16_t>(bins[r]);
+        sbin[j] = static_cast<uint16_t>(bin);
       }
     }
     lds_sync();
