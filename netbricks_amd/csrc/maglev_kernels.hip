@@ -593,7 +593,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
 #define NBG_GROUP_WAVES 4  // waves per SIMD the group kernel is compiled for: <= 64 VGPRs, so a resident
                            // group block leaves the other streams' classify waves their registers
 #endif
-template <int SCAN>
+// BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
+template <int SCAN, int BITS>
 __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupArgs a) {
 #ifdef NBG_GPROBE
   uint64_t gpt[12] = {};
@@ -605,10 +606,14 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   const uint32_t c = blockIdx.x;
   GPROBE(0)
+#ifdef NBG_GROUP_EMPTY  // measurement build: the launch and its stream boundary only
+  return;
+#endif
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbins;        // [nbins]
-  uint32_t* cnt = tot + nbins;         // [kW][nbins]
-  uint32_t* sub = cnt + kW * nbins;    // [nbins] per-chunk bin sizes, then chunk-local starts
+  const uint32_t cst = nbins + 1;      // cnt row stride: one scratch slot for lanes past the end
+  uint32_t* cnt = tot + nbins;         // [kW][nbins + 1]
+  uint32_t* sub = cnt + kW * cst;      // [nbins] per-chunk bin sizes, then chunk-local starts
   uint32_t* sidx = sub + nbins;        // [kChunk]
   uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
   uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (kScanLds)
@@ -720,9 +725,10 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   }
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t* mycnt = cnt + wave * nbins;
+  const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
+  uint32_t* mycnt = cnt + wave * cst;
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
-    for (uint32_t k = tid; k < kW * nbins; k += kGBlock) cnt[k] = 0;
+    for (uint32_t k = tid; k < kW * cst; k += kGBlock) cnt[k] = 0;
     lds_sync();
     GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
@@ -731,19 +737,24 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     for (int r = 0; r < kGRounds; ++r) {
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
-      const uint32_t bin = valid ? (pre_bin[r] == NBG_SENTINEL ? a.nb : pre_bin[r]) : 0u;
-      unsigned long long eq = __ballot(valid);
-      for (uint32_t bit = 0; bit < a.bits; ++bit) {
-        const bool set = (bin >> bit) & 1u;
-        const unsigned long long bb = __ballot(set);
-        eq &= set ? bb : ~bb;
+      const uint32_t bin = pre_bin[r] == NBG_SENTINEL ? a.nb : pre_bin[r];
+      // lanes with my bin (and my validity): per bit, keep the lanes whose ballot bit equals mine
+      const uint32_t mv = valid ? ~0u : 0u;
+      const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
+      uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
+#pragma unroll
+      for (int bit = 0; bit < BITS; ++bit) {
+        const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
+        const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
+        elo &= ~(static_cast<uint32_t>(bb) ^ m);
+        ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
       }
-      uint32_t rank = 0;
-      if (valid) {
-        const uint32_t prior = mycnt[bin];
-        rank = prior + __popcll(eq & lt);
-        if ((eq & lt) == 0) mycnt[bin] = prior + __popcll(eq);
-      }
+      // every lane of a bin stores the same new count (no branch); lanes past the end use the
+      // scratch slot
+      const uint32_t slot = valid ? bin : nbins;
+      const uint32_t prior = mycnt[slot];
+      mycnt[slot] = prior + __popc(elo) + __popc(ehi);
+      const uint32_t rank = prior + __popc(elo & lt_lo) + __popc(ehi & lt_hi);
       br[r] = valid ? (rank << 16) | bin : 0xffffffffu;
     }
     GPROBE(10)
@@ -759,14 +770,14 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     // per bin: offsets of each wave inside the bin (16-lane segmented scan over waves) ...
     for (uint32_t t = tid; t < nbins * kW; t += kGBlock) {
       const uint32_t b = t / kW, w = t % kW;
-      const uint32_t v = cnt[w * nbins + b];
+      const uint32_t v = cnt[w * cst + b];
       uint32_t x = v;
 #pragma unroll
       for (uint32_t d = 1; d < kW; d <<= 1) {
         const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d, kW));
         if (w >= d) x += y;
       }
-      cnt[w * nbins + b] = x - v;
+      cnt[w * cst + b] = x - v;
       if (w == kW - 1) sub[b] = x;  // the bin's packets in this chunk
     }
     lds_sync();
@@ -909,7 +920,7 @@ int launch_scan(const ScanArgs& a, void* stream) {
 }
 
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
-  size_t w = static_cast<size_t>(nbins) * (3 + kGBlock / 64) + kChunk + kChunk / 2;
+  size_t w = static_cast<size_t>(nbins) * 3 + static_cast<size_t>(nbins + 1) * (kGBlock / 64) + kChunk + kChunk / 2;
   if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }
@@ -938,9 +949,14 @@ int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
 }
 
 int launch_group(const GroupArgs& a, int scan, void* stream) {
+#ifdef NBG_SKIP_GROUP_LAUNCH  // measurement build: classify + histograms only
+  return 0;
+#endif
   const size_t lds = group_lds(a.nb + 1, a.n_parts, scan);
-  auto fn = scan == kScanDirect ? group_kernel<kScanDirect>
-                                : (scan == kScanLds ? group_kernel<kScanLds> : group_kernel<kScanKernel>);
+  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7>
+                                                : (scan == kScanLds ? group_kernel<kScanLds, 7> : group_kernel<kScanKernel, 7>))
+                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10>
+                                               : (scan == kScanLds ? group_kernel<kScanLds, 10> : group_kernel<kScanKernel, 10>));
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess)

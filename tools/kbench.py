@@ -84,15 +84,42 @@ def main():
                  torch.empty(args.nb + 1, dtype=torch.uint32, device=dev),
                  torch.empty(n * 12, dtype=torch.uint8, device=dev)) for _ in range(S)]
 
-        def ms(i, S=S, mgs=mgs, sts=sts, outs=outs, mac=True):
+        def ms(i, S=S, mgs=mgs, sts=sts, outs=outs, mac=True, group=True, scatter=True):
             j = i % S
             be, pm, ct, mo = outs[j]
-            mgs[j].group_by(bufs[i % 8], n, backend=be, perm=pm, counts=ct,
+            mgs[j].group_by(bufs[i % 8], n, backend=be, perm=pm if scatter else None, counts=ct, group=group,
+                            scatter=scatter,
                             mac_out=mo if mac else None, stream=sts[j].cuda_stream, **kw(i))
 
         extra[f"full path l2 mac_out x{S} streams"] = ms
         extra[f"full path l2 inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False))
+        extra[f"classify only inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False, group=False))
+        extra[f"classify only mac_out x{S} streams"] = (lambda i, f=ms: f(i, group=False))
+        extra[f"counts only inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False, scatter=False))
         extra[f"_keep{S}"] = (mgs, sts, outs)
+        if S % 2 == 0:
+            # S handles; classify on streams 0..S/2-1, the deferred group kernel on streams S/2..S-1
+            H = S // 2
+            gdone = [None] * S
+
+            def split(i, S=S, H=H, mgs=mgs, sts=sts, outs=outs, gdone=gdone, mac=False):
+                j = i % S
+                cs, gs = sts[j % H], sts[H + j % H]
+                be, pm, ct, mo = outs[j]
+                if gdone[j] is not None:
+                    cs.wait_event(gdone[j])
+                mgs[j].group_by(bufs[i % 8], n, backend=be, perm=pm, counts=ct, defer_group=True,
+                                mac_out=mo if mac else None, stream=cs.cuda_stream, **kw(i))
+                ev = torch.cuda.Event()
+                ev.record(cs)
+                gs.wait_event(ev)
+                mgs[j].finish_group(gs.cuda_stream)
+                g = torch.cuda.Event()
+                g.record(gs)
+                gdone[j] = g
+
+            extra[f"split path inplace x{S} streams"] = split
+            extra[f"split path mac_out x{S} streams"] = (lambda i, f=split: f(i, mac=True))
     variants.update({k: v for k, v in extra.items() if not k.startswith("_keep")})
     if args.only:
         keys = [k.strip() for k in args.only.split(",")]
