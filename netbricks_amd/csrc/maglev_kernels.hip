@@ -492,17 +492,26 @@ __device__ __forceinline__ uint32_t ld_u16(const uint16_t* base, uint32_t byte_o
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
 }
 
+// Inclusive scan over the 64 lanes of a wave with DPP moves (no LDS round trips): shifts by
+// 1, 2, 4, 8 inside each 16-lane row, then row 0's / rows 0-1's totals broadcast into the rows
+// above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).  Lanes a move does not
+// write keep the `old` operand, 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false));
+  return x;
+}
+
 // Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
 // exclusive prefix and the total.
 template <uint32_t NT>
 __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wave, uint32_t& total) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
-    if (lane >= static_cast<uint32_t>(d)) x += y;
-  }
+  const uint32_t x = wave_incl_scan(v);
   if (lane == 63u) s_wave[wave] = x;
   lds_sync();
   uint32_t wpre = 0, tot = 0;
@@ -613,8 +622,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   uint32_t* tot = base + nbins;        // [nbins]
   const uint32_t cst = nbins + 1;      // cnt row stride: one scratch slot for lanes past the end
   uint32_t* cnt = tot + nbins;         // [kW][nbins + 1]
-  uint32_t* sub = cnt + kW * cst;      // [nbins] per-chunk bin sizes, then chunk-local starts
-  uint32_t* sidx = sub + nbins;        // [kChunk]
+  uint32_t* sidx = cnt + kW * cst;     // [kChunk]
   uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
   uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (kScanLds)
 
@@ -641,8 +649,9 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
       const uint32_t b = t % nbins, j = t / nbins;
       uint32_t pre = 0, all = 0;
-      // kU loads in flight per thread: one L2 round trip per kU rows (n_parts <= 256, L >= 1)
-      constexpr uint32_t kU = 16;
+      // kU loads in flight per thread: one L2 round trip per kU rows (n_parts <= 256, L >= 1;
+      // 65 backends: L = 7, 37 rows per thread, one round trip)
+      constexpr uint32_t kU = 40;
       for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
         uint32_t h[kU];
 #pragma unroll
@@ -697,13 +706,12 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   }
   GPROBE(2)
   lds_sync();
-  {
-    const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
-    const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
+  if (wave == 0) {  // group bases: one wave scans the totals (no block-wide scan)
+    const uint32_t ch = (nbins + 63) / 64;
+    const uint32_t lo = min(lane * ch, nbins), hi = min(lo + ch, nbins);
     uint32_t s = 0;
     for (uint32_t b = lo; b < hi; ++b) s += tot[b];
-    uint32_t all;
-    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave, all);
+    uint32_t gb = wave_incl_scan(s) - s;
     for (uint32_t b = lo; b < hi; ++b) {
       const uint32_t t = tot[b];
       if (c == 0 && a.counts) a.counts[b] = t;
@@ -728,8 +736,9 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
   uint32_t* mycnt = cnt + wave * cst;
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
-    for (uint32_t k = tid; k < kW * cst; k += kGBlock) cnt[k] = 0;
-    lds_sync();
+    // each wave zeroes its own counter row: every reader of the previous chunk's counters has
+    // passed a barrier since, and one wave's LDS operations execute in order
+    for (uint32_t k = lane; k < cst; k += 64) mycnt[k] = 0;
     GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
@@ -767,51 +776,45 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     }
     lds_sync();
     GPROBE(4)
-    // per bin: offsets of each wave inside the bin (16-lane segmented scan over waves) ...
-    for (uint32_t t = tid; t < nbins * kW; t += kGBlock) {
-      const uint32_t b = t / kW, w = t % kW;
-      const uint32_t v = cnt[w * cst + b];
-      uint32_t x = v;
-#pragma unroll
-      for (uint32_t d = 1; d < kW; d <<= 1) {
-        const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d, kW));
-        if (w >= d) x += y;
-      }
-      cnt[w * cst + b] = x - v;
-      if (w == kW - 1) sub[b] = x;  // the bin's packets in this chunk
+    // one exclusive scan over the counters in bin-major order (bin, wave): the chunk-local slot
+    // where wave w's packets of bin b start
+    const uint32_t ne = nbins * kW;
+    const uint32_t per = (ne + kGBlock - 1) / kGBlock;
+    const uint32_t e0 = min(tid * per, ne), e1 = min(e0 + per, ne);
+    uint32_t esum = 0;
+    for (uint32_t e = e0; e < e1; ++e) esum += cnt[(e % kW) * cst + e / kW];
+    uint32_t ctotal;
+    uint32_t x = block_excl_scan_n<kGBlock>(esum, s_wave, ctotal);
+    for (uint32_t e = e0; e < e1; ++e) {
+      const uint32_t k = (e % kW) * cst + e / kW;
+      const uint32_t v = cnt[k];
+      cnt[k] = x;
+      x += v;
     }
     lds_sync();
     GPROBE(5)
-    // ... and the chunk-local start of each bin (scan over bins)
-    const uint32_t ch = (nbins + kGBlock - 1) / kGBlock;
-    const uint32_t lo = min(tid * ch, nbins), hi = min(lo + ch, nbins);
-    uint32_t csum = 0;
-    for (uint32_t b = lo; b < hi; ++b) csum += sub[b];
-    uint32_t ctotal;
-    uint32_t lstart = block_excl_scan_n<kGBlock>(csum, s_wave, ctotal);
-    for (uint32_t b = lo; b < hi; ++b) {
-      const uint32_t n = sub[b];
-      tot[b] = base[b] - lstart;  // perm position of sorted slot j of bin b = tot[b] + j
-      sub[b] = lstart;            // chunk-local start of bin b
-      base[b] += n;               // advance past this chunk's packets of bin b
-      lstart += n;
+    // per bin: perm position of chunk slot j of bin b = tot[b] + j; advance past the bin
+    for (uint32_t b = tid; b < nbins; b += kGBlock) {
+      const uint32_t st = cnt[b];                                // wave 0's start = the bin's start
+      const uint32_t en = b + 1 < nbins ? cnt[b + 1] : ctotal;
+      tot[b] = base[b] - st;
+      base[b] += en - st;
     }
-    lds_sync();
     GPROBE(6)
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       if (br[r] != 0xffffffffu) {
         const uint32_t bin = br[r] & 0xffffu;
-        const uint32_t j = sub[bin] + mycnt[bin] + (br[r] >> 16);
+        const uint32_t j = mycnt[bin] + (br[r] >> 16);
         sidx[j] = wbase + r * 64u + lane;
         sbin[j] = static_cast<uint16_t>(bin);
       }
     }
     lds_sync();
     GPROBE(7)
-    // coalesced output: consecutive sorted slots of one bin are consecutive perm entries
+    // coalesced output: consecutive sorted slots of one bin are consecutive perm entries.  The
+    // next chunk's first writes to sidx/sbin/tot come after the barriers of its scan.
     for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
-    lds_sync();
   }
   zero_next();
   GPROBE(8)
@@ -920,7 +923,7 @@ int launch_scan(const ScanArgs& a, void* stream) {
 }
 
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
-  size_t w = static_cast<size_t>(nbins) * 3 + static_cast<size_t>(nbins + 1) * (kGBlock / 64) + kChunk + kChunk / 2;
+  size_t w = static_cast<size_t>(nbins) * 2 + static_cast<size_t>(nbins + 1) * (kGBlock / 64) + kChunk + kChunk / 2;
   if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }
