@@ -217,6 +217,31 @@ def test_repeat_calls_epochs(torch_cuda, mg65):
         _assert_same(_run(torch_cuda, mg65, buf, n), _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
 
 
+@pytest.mark.parametrize("n", [1, 32, 100])
+def test_many_small_batches(torch_cuda, n):
+    """Dozens of small back-to-back batches on one handle (both histogram buffers, every
+    partition-row and super-row reset), on the device and the host path."""
+    import netbricks_amd as nb
+    from netbricks_amd import make_trace
+
+    mg = nb.Maglev(NAMES65, 65537)
+    lut = orc.lut_build(NAMES65, 65537)
+    for k in range(40):
+        buf, _, _ = make_trace(n, 0, seed=100 + k)
+        _assert_same(_run(torch_cuda, mg, buf, n), _oracle(buf, n, lut, 65, stride=64, fixed_len=60))
+    for k in range(40):
+        buf, off, ln = make_trace(n, 1, seed=200 + k)
+        frames = [bytearray(buf[o:o + l].tobytes()) for o, l in zip(off, ln)]
+        pbuf, poff, pln = _pack([bytearray(f) for f in frames], 64)
+        exp = _oracle(pbuf, len(frames), lut, 65, offs=poff, lens=pln)
+        be, perm, counts = mg.group_by_host(frames)
+        np.testing.assert_array_equal(be, exp[1])
+        np.testing.assert_array_equal(perm, exp[2])
+        np.testing.assert_array_equal(counts, exp[3])
+        for f, o, l in zip(frames, poff, pln):
+            assert bytes(f) == exp[0][o:o + l].tobytes()
+
+
 def test_host_path(torch_cuda, mg65):
     """nbg_maglev_classify_host: mbuf-like host frames -> H2D -> kernel -> D2H, MACs swapped in place."""
     rng = np.random.default_rng(11)
