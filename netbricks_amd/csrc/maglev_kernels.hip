@@ -474,10 +474,20 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     // one flush per block into its partition row (the block's packets never straddle two):
     // 4096-packet rows take ~16 blocks' adds, so they rarely contend
     lds_sync();
-    uint32_t* row = a.part_hist + static_cast<size_t>(blockIdx.x * kW * tpw * 64u / a.part_pkts) * nbins;
-    for (uint32_t b = tid; b < nbins; b += NT) {
-      const uint32_t h = hist[b];
-      if (h) atomicAdd(&row[b], h);
+    const uint32_t p = blockIdx.x * kW * tpw * 64u / a.part_pkts;
+    if (a.hist16) {  // two bins per word: half the atomics, and half the rows' bytes for the group kernel
+      const uint32_t hw = (nbins + 1) >> 1;
+      uint32_t* row = a.part_hist + static_cast<size_t>(p) * hw;
+      for (uint32_t w = tid; w < hw; w += NT) {
+        const uint32_t h = hist[2 * w] | (2 * w + 1 < nbins ? hist[2 * w + 1] << 16 : 0u);
+        if (h) atomicAdd(&row[w], h);
+      }
+    } else {
+      uint32_t* row = a.part_hist + static_cast<size_t>(p) * nbins;
+      for (uint32_t b = tid; b < nbins; b += NT) {
+        const uint32_t h = hist[b];
+        if (h) atomicAdd(&row[b], h);
+      }
     }
   }
   CPROBE(3)
@@ -643,8 +653,38 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   }
   if constexpr (SCAN == kScanDirect) {
     lds_sync();
-    // L threads per bin, each summing a strided subset of the partition rows straight from L2
-    // (consecutive threads read consecutive bins of one row: coalesced)
+    // L threads per row word, each summing a strided subset of the partition rows straight from
+    // L2 (consecutive threads read consecutive words of one row: coalesced)
+    if (a.hist16) {
+      const uint32_t hw = (nbins + 1) >> 1;
+      const uint32_t L = hw >= kGBlock ? 1u : kGBlock / hw;
+      for (uint32_t t = tid; t < hw * L; t += kGBlock) {
+        const uint32_t w = t % hw, j = t / hw;
+        uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
+        // 65 backends: 33 words, L = 15, 18 rows per thread: one L2 round trip
+        constexpr uint32_t kU = 24;
+        for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
+          uint32_t h[kU];
+#pragma unroll
+          for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * hw + w) * 4u);
+#pragma unroll
+          for (uint32_t k = 0; k < kU; ++k) {
+            const uint32_t q = q0 + k * L;
+            const uint32_t lo = q < a.n_parts ? h[k] & 0xffffu : 0u, hi = q < a.n_parts ? h[k] >> 16 : 0u;
+            all_lo += lo;
+            all_hi += hi;
+            pre_lo += q < c ? lo : 0u;
+            pre_hi += q < c ? hi : 0u;
+          }
+        }
+        if (pre_lo) atomicAdd(&base[2 * w], pre_lo);
+        if (all_lo) atomicAdd(&tot[2 * w], all_lo);
+        if (2 * w + 1 < nbins) {
+          if (pre_hi) atomicAdd(&base[2 * w + 1], pre_hi);
+          if (all_hi) atomicAdd(&tot[2 * w + 1], all_hi);
+        }
+      }
+    } else {
     const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
     for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
       const uint32_t b = t % nbins, j = t / nbins;
@@ -664,6 +704,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
       }
       if (pre) atomicAdd(&base[b], pre);
       if (all) atomicAdd(&tot[b], all);
+    }
     }
   } else if constexpr (SCAN == kScanLds) {
     // stage the partition histograms: every load issued before any LDS store (one round trip)

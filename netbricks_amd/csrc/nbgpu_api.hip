@@ -461,6 +461,10 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const bool hist_k = group && !hist_in_classify(nbins);  // histograms by hist_kernel instead
   a.part_hist = group && !hist_k ? part_cur : nullptr;
   a.part_pkts = part_pkts;
+  const int scan = group ? pick_group_scan(nbins, n_parts) : kScanKernel;
+  // packed 16-bit partition rows where the classify kernel writes them and the group kernel sums
+  // them itself (partition counts stay below 65536)
+  a.hist16 = group && !hist_k && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
   if (lpm) {
     a.tbl24 = lpm->d_tbl24;
     a.tbl_long = lpm->d_tbl_long;
@@ -471,7 +475,6 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   int rc = launch_classify(a, h->wide, lds, grid, stream);
   if (rc) return rc;
   if (group) {
-    const int scan = pick_group_scan(nbins, n_parts);
     ScanArgs sa{};
     sa.part_hist = part_cur;
     sa.part_prefix = h->d_part_prefix;
@@ -497,6 +500,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     ga.part_hist = part_cur;
     ga.part_prefix = h->d_part_prefix;
     ga.totals = h->d_totals;
+    ga.hist16 = a.hist16;
     ga.part_hist_next = part_next;
     ga.next_words = kMaxParts * nbins;
     ga.counts = d_counts ? d_counts : h->d_counts;

@@ -53,6 +53,7 @@ struct ClassifyArgs {
   uint8_t* mac_out;         // nullable: dense 12-B swapped-MAC records instead of in-place swap
   uint32_t* part_hist;      // nullable: [n_parts][nb+1] partition histograms (pre-zeroed)
   uint32_t part_pkts;       // packets per partition
+  uint32_t hist16;          // part_hist rows hold two 16-bit bins per word (partitions < 65536 packets)
   // chained test/lpm stage (nbg_chain_lpm_maglev_device); tbl24 == nullptr: Maglev alone
   const uint16_t* tbl24;
   const uint16_t* tbl_long;
@@ -87,6 +88,7 @@ struct GroupArgs {
   const uint32_t* part_hist;  // [n_parts][nb+1]      (kScanLds / kScanDirect)
   const uint32_t* part_prefix;// [n_parts][nb+1]      (scan_kernel path)
   const uint32_t* totals;     // [nb+1]               (scan_kernel path)
+  uint32_t hist16;            // kScanDirect: rows of two 16-bit bins per word ((nbins + 1) / 2 words)
   uint32_t* part_hist_next;   // zeroed for the next call
   uint32_t next_words;
   uint32_t* counts;           // nullable
