@@ -88,6 +88,19 @@ def test_c2_full_1m(torch_cuda, mg65, lut_lds):
     assert np.array_equal(np.sort(perm), np.arange(n, dtype=np.uint32))
 
 
+@pytest.mark.parametrize("n", [(1 << 21) + 12345, (1 << 24) + 1000])
+def test_c2_multi_chunk_partitions(torch_cuda, mg65, n):
+    """Batches above 1M packets: partitions of several 4096-packet chunks per group block; above
+    15.7M the partition counts no longer fit 16 bits and the rows stay 32-bit."""
+    from netbricks_amd import make_trace
+
+    buf, _, _ = make_trace(n, 0, seed=n & 0xFFFF)
+    lut = orc.lut_build(NAMES65, 65537)
+    got = _run(torch_cuda, mg65, buf, n)
+    exp = _oracle(buf, n, lut, 65, stride=64, fixed_len=60)
+    _assert_same(got, exp)
+
+
 def test_no_swap_and_no_group(torch_cuda, mg65):
     from netbricks_amd import make_trace
 
