@@ -747,17 +747,48 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   }
   GPROBE(2)
   lds_sync();
-  if (wave == 0) {  // group bases: one wave scans the totals (no block-wide scan)
-    const uint32_t ch = (nbins + 63) / 64;
-    const uint32_t lo = min(lane * ch, nbins), hi = min(lo + ch, nbins);
-    uint32_t s = 0;
-    for (uint32_t b = lo; b < hi; ++b) s += tot[b];
-    uint32_t gb = wave_incl_scan(s) - s;
-    for (uint32_t b = lo; b < hi; ++b) {
-      const uint32_t t = tot[b];
-      if (c == 0 && a.counts) a.counts[b] = t;
-      base[b] += gb;  // group base + prefix over earlier partitions
-      gb += t;
+  // group bases (exclusive scan of the totals over bins).  Loops have compile-time trip counts
+  // (bins < 2^BITS) so that their LDS reads issue back to back.
+  constexpr uint32_t kMaxBins = 1u << BITS;
+  if constexpr (kMaxBins <= 128) {  // one wave, <= 2 bins per lane (no block-wide scan)
+    if (wave == 0) {
+      uint32_t t2[2], s = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        t2[k] = b < nbins ? tot[b] : 0u;
+        s += t2[k];
+      }
+      uint32_t gb = wave_incl_scan(s) - s;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        if (b < nbins) {
+          if (c == 0 && a.counts) a.counts[b] = t2[k];
+          base[b] += gb;  // group base + prefix over earlier partitions
+        }
+        gb += t2[k];
+      }
+    }
+  } else {  // the whole block, <= kMaxBins / kGBlock bins per thread
+    constexpr uint32_t kCh = (kMaxBins + kGBlock - 1) / kGBlock;
+    uint32_t tk[kCh], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kCh; ++k) {
+      const uint32_t b = tid * kCh + k;
+      tk[k] = b < nbins ? tot[b] : 0u;
+      s += tk[k];
+    }
+    uint32_t all;
+    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave, all);
+#pragma unroll
+    for (uint32_t k = 0; k < kCh; ++k) {
+      const uint32_t b = tid * kCh + k;
+      if (b < nbins) {
+        if (c == 0 && a.counts) a.counts[b] = tk[k];
+        base[b] += gb;
+      }
+      gb += tk[k];
     }
   }
   lds_sync();
@@ -779,7 +810,9 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
     // each wave zeroes its own counter row: every reader of the previous chunk's counters has
     // passed a barrier since, and one wave's LDS operations execute in order
-    for (uint32_t k = lane; k < cst; k += 64) mycnt[k] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (kMaxBins + 64) / 64; ++k)
+      if (lane + k * 64 < cst) mycnt[lane + k * 64] = 0;
     GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
@@ -819,18 +852,23 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     GPROBE(4)
     // one exclusive scan over the counters in bin-major order (bin, wave): the chunk-local slot
     // where wave w's packets of bin b start
+    // (each thread owns kPer consecutive elements: whole bins' wave counters when kPer >= kW)
+    constexpr uint32_t kPer = (kMaxBins * kW + kGBlock - 1) / kGBlock;
     const uint32_t ne = nbins * kW;
-    const uint32_t per = (ne + kGBlock - 1) / kGBlock;
-    const uint32_t e0 = min(tid * per, ne), e1 = min(e0 + per, ne);
-    uint32_t esum = 0;
-    for (uint32_t e = e0; e < e1; ++e) esum += cnt[(e % kW) * cst + e / kW];
+    uint32_t ev[kPer], esum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t e = tid * kPer + k;
+      ev[k] = e < ne ? cnt[(e % kW) * cst + e / kW] : 0u;
+      esum += ev[k];
+    }
     uint32_t ctotal;
     uint32_t x = block_excl_scan_n<kGBlock>(esum, s_wave, ctotal);
-    for (uint32_t e = e0; e < e1; ++e) {
-      const uint32_t k = (e % kW) * cst + e / kW;
-      const uint32_t v = cnt[k];
-      cnt[k] = x;
-      x += v;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t e = tid * kPer + k;
+      if (e < ne) cnt[(e % kW) * cst + e / kW] = x;
+      x += ev[k];
     }
     lds_sync();
     GPROBE(5)
