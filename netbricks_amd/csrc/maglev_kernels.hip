@@ -628,10 +628,11 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
 #ifdef NBG_GROUP_EMPTY  // measurement build: the launch and its stream boundary only
   return;
 #endif
+  const uint32_t nbp = (nbins + 3) & ~3u;
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
-  uint32_t* tot = base + nbins;        // [nbins]
-  const uint32_t cst = nbins + 1;      // cnt row stride: one scratch slot for lanes past the end
-  uint32_t* cnt = tot + nbins;         // [kW][nbins + 1]
+  uint32_t* tot = base + nbp;          // [nbins]
+  const uint32_t cst = (nbins + 4) & ~3u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
+  uint32_t* cnt = tot + nbp;           // [kW][cst]
   uint32_t* sidx = cnt + kW * cst;     // [kChunk]
   uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
   uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (kScanLds)
@@ -811,8 +812,8 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     // each wave zeroes its own counter row: every reader of the previous chunk's counters has
     // passed a barrier since, and one wave's LDS operations execute in order
 #pragma unroll
-    for (uint32_t k = 0; k < (kMaxBins + 64) / 64; ++k)
-      if (lane + k * 64 < cst) mycnt[lane + k * 64] = 0;
+    for (uint32_t k = 0; k < (kMaxBins + 4 + 255) / 256; ++k)
+      if ((lane + k * 64) * 4 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
     GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
@@ -1002,7 +1003,8 @@ int launch_scan(const ScanArgs& a, void* stream) {
 }
 
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
-  size_t w = static_cast<size_t>(nbins) * 2 + static_cast<size_t>(nbins + 1) * (kGBlock / 64) + kChunk + kChunk / 2;
+  const size_t nbp = (nbins + 3) & ~3u, cst = (nbins + 4) & ~3u;
+  size_t w = nbp * 2 + cst * (kGBlock / 64) + kChunk + kChunk / 2;
   if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }
