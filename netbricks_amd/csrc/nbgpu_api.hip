@@ -94,8 +94,7 @@ struct nbg_maglev {
     uint16_t* d_backend = nullptr;
     uint32_t* d_perm = nullptr;
     uint32_t* d_counts = nullptr;
-    hipStream_t copy = nullptr;  // H2D and D2H of this slot
-    hipEvent_t staged = nullptr, classified = nullptr, done = nullptr;
+    hipEvent_t done = nullptr;  // after the slot's D2H copies (on the handle's host stream)
     bool busy = false;
     uint64_t ticket = 0;
     // the submitted batch (the caller keeps these valid until its wait)
@@ -163,12 +162,8 @@ void free_host_path(nbg_maglev* h) {
     if (t.busy && t.done) (void)hipEventSynchronize(t.done);
     t.busy = false;
     free_slot_buffers(t);
-    if (t.copy) (void)hipStreamDestroy(t.copy);
-    if (t.staged) (void)hipEventDestroy(t.staged);
-    if (t.classified) (void)hipEventDestroy(t.classified);
     if (t.done) (void)hipEventDestroy(t.done);
-    t.copy = nullptr;
-    t.staged = t.classified = t.done = nullptr;
+    t.done = nullptr;
   }
   if (h->host_compute) (void)hipStreamDestroy(h->host_compute);
   h->host_compute = nullptr;
@@ -646,12 +641,7 @@ uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
 }
 
 int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
-  if (!t.copy) {
-    NBG_HIP(hipStreamCreateWithFlags(&t.copy, hipStreamNonBlocking));
-    NBG_HIP(hipEventCreateWithFlags(&t.staged, hipEventDisableTiming));
-    NBG_HIP(hipEventCreateWithFlags(&t.classified, hipEventDisableTiming));
-    NBG_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
-  }
+  if (!t.done) NBG_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
   if (n <= t.cap) return NBG_OK;
   free_slot_buffers(t);
   const uint64_t cap = std::max<uint64_t>(n, 4096);
@@ -734,25 +724,25 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   // gather at 48-B windows; a batch with longer IP headers is staged again at the stride it needs
   uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len);
   if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len);
-  // copies on the slot's stream, kernels in submit order on the handle's compute stream (they
-  // share the handle's grouping scratch), results back on the slot's stream
-  NBG_HIP(hipMemcpyAsync(t.d_win, t.h_win, n * win, hipMemcpyHostToDevice, t.copy));
-  NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, t.copy));
-  NBG_HIP(hipEventRecord(t.staged, t.copy));
-  NBG_HIP(hipStreamWaitEvent(h->host_compute, t.staged, 0));
+  // copies and kernels in submit order on the handle's one host stream (the kernels share the
+  // handle's grouping scratch).  No cross-stream event: with the copies on a stream of their own
+  // and an event wait on the compute stream, kernels were seen reading windows whose H2D copy had
+  // not landed (zero windows, sporadically, with many streams in the process).  The host gathers
+  // the next batch while this one runs.
+  hipStream_t hs = h->host_compute;
+  NBG_HIP(hipMemcpyAsync(t.d_win, t.h_win, n * win, hipMemcpyHostToDevice, hs));
+  NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
   const bool group = perm_out || counts_out;
   rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n,
                                      (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL)) | NBG_OWNED_WINDOWS, t.d_backend,
                                      perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr,
-                                     swap ? t.d_mac : nullptr, h->host_compute);
+                                     swap ? t.d_mac : nullptr, hs);
   if (rc) return rc;
-  NBG_HIP(hipEventRecord(t.classified, h->host_compute));
-  NBG_HIP(hipStreamWaitEvent(t.copy, t.classified, 0));
-  NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, t.copy));
-  if (perm_out) NBG_HIP(hipMemcpyAsync(t.h_perm, t.d_perm, n * 4, hipMemcpyDeviceToHost, t.copy));
-  if (counts_out) NBG_HIP(hipMemcpyAsync(t.h_counts, t.d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, t.copy));
-  if (swap) NBG_HIP(hipMemcpyAsync(t.h_mac, t.d_mac, n * 12, hipMemcpyDeviceToHost, t.copy));
-  NBG_HIP(hipEventRecord(t.done, t.copy));
+  NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, hs));
+  if (perm_out) NBG_HIP(hipMemcpyAsync(t.h_perm, t.d_perm, n * 4, hipMemcpyDeviceToHost, hs));
+  if (counts_out) NBG_HIP(hipMemcpyAsync(t.h_counts, t.d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, hs));
+  if (swap) NBG_HIP(hipMemcpyAsync(t.h_mac, t.d_mac, n * 12, hipMemcpyDeviceToHost, hs));
+  NBG_HIP(hipEventRecord(t.done, hs));
   t.busy = true;
   *ticket = tk;
   return NBG_OK;

@@ -62,8 +62,9 @@ def check(frames, names, out, idx):
     for i, f in enumerate(frames):
         buf[offs[i]:offs[i] + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
     be = orc.classify(buf, n, lut, offs=offs, lens=lens)
-    for o, i in zip(out, idx):
-        assert o == buf[offs[i]:offs[i] + lens[i]].tobytes()
+    bad = [(k, i) for k, (o, i) in enumerate(zip(out, idx)) if o != buf[offs[i]:offs[i] + lens[i]].tobytes()]
+    assert not bad, (f"{len(bad)} of {n} transmitted frames differ; first (tx position, rx index): {bad[:8]}; "
+                     f"tx {out[bad[0][0]][:14].hex()} expected {buf[offs[bad[0][1]]:offs[bad[0][1]] + 14].tobytes().hex()}")
     # per-group FIFO: within each backend the transmit order is the arrival order
     last = {}
     for i in idx:
