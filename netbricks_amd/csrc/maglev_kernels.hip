@@ -12,7 +12,7 @@
 //   transposes them through LDS to one packet per lane, and the lane holding chunk 0
 //   applies the MAC swap in registers and writes the window back with full-line stores.
 // scan_kernel — (many backends only) per backend bin, exclusive scan of the partition
-//   histograms over partitions, and the bin totals.
+//   histograms over partitions, and the bin totals (64 bins per block, coalesced rows).
 // group_kernel — per partition: the per-bin prefix over earlier partitions and the group
 //   bases, then per 4096-packet chunk wave ballot multisplit ranks (stable), a local counting
 //   sort in LDS, and coalesced stores of perm[] = packet indices grouped by backend.
@@ -536,48 +536,23 @@ __device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wa
   return wpre + x - v;
 }
 
-// Block-wide exclusive scan of one value per thread; returns the exclusive prefix and the total.
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
-    if (lane >= static_cast<uint32_t>(d)) x += y;
-  }
-  if (lane == 63u) s_wave[wave] = x;
-  __syncthreads();
-  uint32_t wpre = 0, tot = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kBlock / 64; ++w) {
-    const uint32_t t = s_wave[w];
-    if (w < wave) wpre += t;
-    tot += t;
-  }
-  __syncthreads();
-  total = tot;
-  return wpre + x - v;
-}
-
 // Many backends: the partition histograms come from this kernel instead of the classify kernel
 // (whose per-block flush would cost about one global atomic per packet at ~1000 bins).  One
-// 1024-thread block per partition counts its packets' backends in LDS and stores the whole row.
+// 512-thread block per partition counts its packets' backends in LDS and stores the whole row.
 __global__ __launch_bounds__(kGBlock) void hist_kernel(HistArgs a) {
   extern __shared__ __align__(16) uint32_t hs[];
   const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c = blockIdx.x;
   const uint32_t pbeg = c * a.part_pkts, pend = min(pbeg + a.part_pkts, a.n_pkts);
   for (uint32_t b = tid; b < nbins; b += kGBlock) hs[b] = 0;
   lds_sync();
-  for (uint32_t i0 = pbeg; i0 < pend; i0 += 4 * kGBlock) {
-    uint32_t v[4];
+  // one chunk per pass, every load unconditional (clamped) and in flight together
+  for (uint32_t i0 = pbeg; i0 < pend; i0 += kChunk) {
+    uint32_t v[kGRounds];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t i = i0 + k * kGBlock + tid;
-      v[k] = i < pend ? a.backend[i] : 0xffffffffu;
-    }
+    for (int k = 0; k < kGRounds; ++k) v[k] = ld_u16(a.backend, min(i0 + k * kGBlock + tid, a.n_pkts - 1u) * 2u);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (v[k] != 0xffffffffu) atomicAdd(&hs[v[k] == NBG_SENTINEL ? a.nb : v[k]], 1u);
+    for (int k = 0; k < kGRounds; ++k) {
+      if (i0 + k * kGBlock + tid < pend) atomicAdd(&hs[v[k] == NBG_SENTINEL ? a.nb : v[k]], 1u);
     }
   }
   lds_sync();
@@ -585,16 +560,41 @@ __global__ __launch_bounds__(kGBlock) void hist_kernel(HistArgs a) {
   for (uint32_t b = tid; b < nbins; b += kGBlock) row[b] = hs[b];
 }
 
-// Fallback for many backends: one block per bin, exclusive scan of part_hist[.][bin] over
-// partitions and the bin's grand total.
-__global__ __launch_bounds__(kBlock) void scan_kernel(ScanArgs a) {
-  __shared__ uint32_t s_wave[kBlock / 64];
-  const uint32_t tid = threadIdx.x, b = blockIdx.x;
-  const uint32_t v = tid < a.n_parts ? a.part_hist[static_cast<size_t>(tid) * a.nbins + b] : 0u;
-  uint32_t total;
-  const uint32_t pre = block_excl_scan(v, s_wave, total);
-  if (tid < a.n_parts) a.part_prefix[static_cast<size_t>(tid) * a.nbins + b] = pre;
-  if (tid == 0) a.totals[b] = total;
+// Many backends: exclusive scan of part_hist[.][bin] over partitions, and every bin's total.
+// One block per 64 consecutive bins, one lane per bin; wave w scans partitions [32w, 32w + 32)
+// in registers (each row segment is one coalesced 256-B load, all 32 in flight), and the waves'
+// sums are combined through LDS.
+constexpr uint32_t kScanBins = 64, kScanWaves = kMaxParts / 32;
+__global__ __launch_bounds__(kScanWaves * 64) void scan_kernel(ScanArgs a) {
+  __shared__ uint32_t s_sum[kScanWaves][kScanBins];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+  const uint32_t b = blockIdx.x * kScanBins + lane;
+  const uint32_t bc = min(b, a.nbins - 1u), q0 = wave * 32u;
+  uint32_t v[32];
+#pragma unroll
+  for (uint32_t k = 0; k < 32; ++k) v[k] = ld_u32(a.part_hist, (min(q0 + k, a.n_parts - 1u) * a.nbins + bc) * 4u);
+  uint32_t run = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 32; ++k) {
+    const uint32_t x = q0 + k < a.n_parts ? v[k] : 0u;
+    v[k] = run;  // exclusive within this wave's partitions
+    run += x;
+  }
+  s_sum[wave][lane] = run;
+  __syncthreads();
+  uint32_t off = 0, total = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kScanWaves; ++w) {
+    const uint32_t t = s_sum[w][lane];
+    off += w < wave ? t : 0u;
+    total += t;
+  }
+  if (b < a.nbins) {
+#pragma unroll
+    for (uint32_t k = 0; k < 32; ++k)
+      if (q0 + k < a.n_parts) a.part_prefix[static_cast<size_t>(q0 + k) * a.nbins + b] = off + v[k];
+    if (wave == 0) a.totals[b] = total;
+  }
 }
 
 // One 1024-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
@@ -996,7 +996,8 @@ int launch_hist(const HistArgs& a, void* stream) {
 }
 
 int launch_scan(const ScanArgs& a, void* stream) {
-  hipLaunchKernelGGL(scan_kernel, dim3(a.nbins), dim3(kBlock), 0, static_cast<hipStream_t>(stream), a);
+  hipLaunchKernelGGL(scan_kernel, dim3((a.nbins + kScanBins - 1) / kScanBins), dim3(kScanWaves * 64), 0,
+                     static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "scan launch: %s", hipGetErrorString(e));
   return NBG_OK;
