@@ -5,9 +5,11 @@ Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,57
 64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM.  One step = one batch
 through `nbg_maglev_classify_device` (classify kernel + grouping kernel), MAC swap in place.
 Steps rotate over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache) and are issued
-round-robin on `--streams` (default 4) HIP streams (independent batches, one handle per stream: NetBricks
+round-robin on `--streams` (default 3) HIP streams (independent batches, one handle per stream: NetBricks
 runs one pipeline per RX queue), so one batch's latency-bound grouping overlaps the next
-batch's bandwidth-bound classify.
+batch's bandwidth-bound classify.  Three streams plus the default stream fill HIP's 4 hardware
+queues (GPU_MAX_HW_QUEUES) one each; a fourth stream would share a queue and serialise behind
+another (measured: 3 streams 34.0-35.3 Gpps, 4 streams 32.3-32.8 on one box).
 
 Roofline: the classify kernel (dominant) is timed with HIP events around each launch in a
 separate single-stream pass (NBG_DEFER_GROUP splits it from the grouping kernel).
@@ -191,7 +193,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--mac-record", action="store_true",
                     help="write the swapped MACs as dense 12-B egress records instead of in place")
     ap.add_argument("--no-cpu-baseline", action="store_true")

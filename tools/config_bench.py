@@ -30,7 +30,7 @@ N_BATCHES = 8
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3,c5")
-    ap.add_argument("--streams", type=int, default=4)
+    ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     args = ap.parse_args()
