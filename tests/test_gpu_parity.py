@@ -101,6 +101,20 @@ def test_c2_multi_chunk_partitions(torch_cuda, mg65, n):
     _assert_same(got, exp)
 
 
+def test_many_backends_multi_chunk(torch_cuda):
+    """1000 backends at 16.8M packets: hist_kernel + scan_kernel over partitions of several chunks
+    (partition counts above 16 bits)."""
+    import netbricks_amd as nb
+    from netbricks_amd import make_trace
+
+    names = [f"backend-{i}" for i in range(1000)]
+    mg = nb.Maglev(names, 655373)
+    n = (1 << 24) + 1000
+    buf, _, _ = make_trace(n, 0, seed=77)
+    lut = orc.lut_build(names, 655373)
+    _assert_same(_run(torch_cuda, mg, buf, n), _oracle(buf, n, lut, 1000, stride=64, fixed_len=60))
+
+
 def test_no_swap_and_no_group(torch_cuda, mg65):
     from netbricks_amd import make_trace
 
