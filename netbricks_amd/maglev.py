@@ -16,8 +16,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_SENTINEL, NBG_SWAP_MACS, NBG_WB_PARTIAL,
-                   check, lib)
+from ._lib import (NBG_DEFER_GROUP, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_SENTINEL, NBG_SWAP_MACS,
+                   NBG_WB_PARTIAL, check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
 
@@ -150,7 +150,8 @@ class Maglev:
         """Pipelined host path (nbg_maglev_host_submit): frame i is `lens[i]` bytes at address
         `ptrs[i]` (u64 numpy arrays of host mbuf data pointers).  Returns a ticket; backend / perm /
         counts (numpy) and the frames' MAC swap are complete when host_wait(ticket) returns.  The
-        caller keeps every array (and the frames) alive until then."""
+        caller keeps the frames alive until then; this wrapper holds the pointer, length and output
+        arrays it passes to the library (converted copies included) until the batch completes."""
         ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         n = ptrs.size
@@ -160,10 +161,18 @@ class Maglev:
                                         None if perm is None else perm.ctypes.data,
                                         None if counts is None else counts.ctypes.data, C.byref(ticket))
         check(rc, "nbg_maglev_host_submit")
-        return ticket.value
+        t = ticket.value
+        # the library reads ptrs/lens and writes the outputs until the batch completes: at its wait,
+        # or when a later submit reuses its staging slot (NBG_HOST_SLOTS submits later)
+        inflight = self.__dict__.setdefault("_inflight", {})
+        for k in [k for k in inflight if k <= t - NBG_HOST_SLOTS]:
+            del inflight[k]
+        inflight[t] = (ptrs, lens, backend, perm, counts)
+        return t
 
     def host_wait(self, ticket: int) -> None:
         check(lib.nbg_maglev_host_wait(self._h, ticket), "nbg_maglev_host_wait")
+        self.__dict__.get("_inflight", {}).pop(ticket, None)
 
     def group_by_host(self, frames: Sequence[bytearray], swap_macs: bool = True, group: bool = True):
         """Host mbuf path: frames are mutable byte buffers (their MACs are swapped in place).

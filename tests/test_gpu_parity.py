@@ -470,3 +470,45 @@ def test_host_pipeline_large_batch(torch_cuda, mg65):
     np.testing.assert_array_equal(out["perm"], exp[2])
     np.testing.assert_array_equal(out["counts"], exp[3])
     np.testing.assert_array_equal(pool.reshape(n, room)[:, :60], exp[0].reshape(n, 64)[:, :60])
+
+
+def test_host_pipeline_many_handles_and_streams(torch_cuda):
+    """Three handles with interleaved submits (batches of 1 to 3000 frames, waits out of order)
+    while device batches run on torch streams of the same process: the host path keeps each
+    batch's copies and kernels in order with no cross-stream events to lose."""
+    import netbricks_amd as nb
+    from netbricks_amd import make_trace
+
+    lut = orc.lut_build(NAMES65, 65537)
+    handles = [nb.Maglev(NAMES65, 65537) for _ in range(3)]
+    streams = [torch_cuda.cuda.Stream() for _ in range(4)]
+    dev_bufs = [torch_cuda.from_numpy(make_trace(65536, 0, seed=500 + k)[0]).cuda() for k in range(4)]
+    rng = np.random.default_rng(5)
+    pending = []
+    for k in range(24):
+        n = int(rng.choice([1, 32, 100, 1000, 3000]))
+        buf, off, ln = make_trace(n, 1, seed=600 + k)
+        frames = [bytearray(buf[o:o + l].tobytes()) for o, l in zip(off, ln)]
+        pool, ptrs, lens = _mbuf_pool(frames)
+        out = dict(backend=np.empty(n, np.uint16), perm=np.empty(n, np.uint32), counts=np.empty(66, np.uint32))
+        h = handles[k % 3]
+        pending.append((h, h.host_submit(ptrs, lens, **out), frames, pool, out))
+        # device work of another handle on other streams meanwhile
+        j = k % 4
+        handles[(k + 1) % 3].group_by(dev_bufs[j], 65536, stream=streams[j].cuda_stream)
+        if k % 5 == 4:  # some waits early, out of order
+            h2, t2, *_ = pending[-2]
+            h2.host_wait(t2)
+    for h, t, *_ in reversed(pending):
+        h.host_wait(t)
+    torch_cuda.cuda.synchronize()
+    for h, t, frames, pool, out in pending:
+        pbuf, poff, pln = _pack([bytearray(f) for f in frames], 64)
+        exp = _oracle(pbuf, len(frames), lut, 65, offs=poff, lens=pln)
+        np.testing.assert_array_equal(out["backend"], exp[1])
+        np.testing.assert_array_equal(out["perm"], exp[2])
+        np.testing.assert_array_equal(out["counts"], exp[3])
+        for i, (o, l) in enumerate(zip(poff.tolist(), pln.tolist())):
+            assert pool[i * 2048:i * 2048 + l].tobytes() == exp[0][o:o + l].tobytes(), i
+    for h in handles:
+        h.close()
