@@ -455,9 +455,13 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     for (uint32_t i = 0; i < tpw; ++i) {
       const uint32_t wbase = (t0 + i) * 64u;
       if (wbase >= a.n_pkts) break;  // wave-uniform
+      // The tile's loads are issued at raised wave priority, so a newly started wave gets its HBM
+      // requests out ahead of resident waves' hash/gather work (bench +2 % in place, +4 % records).
+      __builtin_amdgcn_s_setprio(kLoadPrio);
       const TileMeta meta = load_meta<LAYOUT>(a, wbase, lane);
       TileRegs cur;
       load_tile<LAYOUT>(a, wbase, meta, part, quad, cur);
+      __builtin_amdgcn_s_setprio(0);
       transpose(cur);
 #ifdef NBG_CPROBE
       if (first) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); CPROBE(1) first = false; }
