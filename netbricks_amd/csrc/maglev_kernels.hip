@@ -632,6 +632,9 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
 #ifdef NBG_GROUP_EMPTY  // measurement build: the launch and its stream boundary only
   return;
 #endif
+#ifdef NBG_GROUP_PRIO  // experiment: the latency-bound group waves ahead of other streams' classify
+  __builtin_amdgcn_s_setprio(NBG_GROUP_PRIO);
+#endif
   const uint32_t nbp = (nbins + 3) & ~3u;
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbp;          // [nbins]
