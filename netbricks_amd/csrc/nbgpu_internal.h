@@ -23,7 +23,10 @@ constexpr int kBlock = 256;          // classify threads per workgroup (4 waves)
 constexpr int kLdsBlock = 1024;      // classify threads per workgroup with the LDS-staged LUT (1 per CU)
 constexpr int kXStride = 48;         // LDS bytes per packet in the transpose: chunks 0..2 (a 12-dword row
                                      // stride keeps the b128 reads conflict-free; 8 blocks fit per CU)
-constexpr int kLoadPrio = 3;         // s_setprio while a classify wave issues its tile loads
+#ifndef NBG_LOAD_PRIO
+#define NBG_LOAD_PRIO 3
+#endif
+constexpr int kLoadPrio = NBG_LOAD_PRIO;  // s_setprio while a classify wave issues its tile loads
 #ifndef NBG_GBLOCK
 #define NBG_GBLOCK 512
 #endif
