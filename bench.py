@@ -5,28 +5,37 @@ Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,57
 64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM.  One step = one batch
 through `nbg_maglev_classify_device` (classify kernel + grouping kernel), MAC swap in place.
 Steps rotate over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache) and are issued
-round-robin on `--streams` (default 3) HIP streams (independent batches, one handle per stream: NetBricks
-runs one pipeline per RX queue), so one batch's latency-bound grouping overlaps the next
-batch's bandwidth-bound classify.  Three streams plus the default stream fill HIP's 4 hardware
-queues (GPU_MAX_HW_QUEUES) one each; a fourth stream would share a queue and serialise behind
-another (measured: 3 streams 34.0-35.3 Gpps, 4 streams 32.3-32.8 on one box).
+round-robin on `--streams` (default 3) HIP streams (independent batches, one handle per stream:
+NetBricks runs one pipeline per RX queue, scheduler/context.rs:241-255), so one batch's
+latency-bound grouping overlaps the next batch's bandwidth-bound classify.
+
+Process model.  `python bench.py --gpus N` is a launcher: it never touches the GPU, spawns N
+rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their environment),
+waits for them and prints rank 0's JSON line.  `--gpus 1` runs one rank through the same code.
+Under `torch.distributed.run` (WORLD_SIZE already set) the process is a rank itself.  Every rank
+owns its own batches (weak scaling, no data-path collective in the timed region); the LUT is
+built on rank 0 and broadcast once over RCCL (setup, untimed).  `--selftest` runs the same
+launcher and rank logic on the CPU with gloo and no HIP call (the CPU test of the launcher).
 
 Roofline: the classify kernel (dominant) is timed with HIP events around each launch in a
-separate single-stream pass (NBG_DEFER_GROUP splits it from the grouping kernel).
+separate single-stream pass (NBG_DEFER_GROUP splits it from the grouping kernel); its HBM
+traffic is measured in the same invocation by two rocprofv3 --pmc passes (FETCH_SIZE,
+WRITE_SIZE) of a short child run, at N = 1.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): packet batches shard trivially; each
-rank owns its own batches (weak scaling, no data-path collective).  The LUT is built on rank 0
-and broadcast once over RCCL (setup, untimed).
-
-Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
+Prints ONE JSON line (rank 0 / the launcher; see DESIGN.md "Measurement").
 """
 from __future__ import annotations
 
 import argparse
-import glob
+import csv
+import hashlib
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -41,49 +50,90 @@ SLOT = 64
 FRAME = 60
 N_BATCHES = 8
 SEED = 0x4E42474D41474C56
-# algorithmic bytes per packet: classify kernel = 64 B read + 12 B MAC write
-# + 2 B backend write; the whole path adds the grouping kernel's 4 B perm write (= 82 B, C2).
-CLASSIFY_BYTES = 64 + 12 + 2
-PATH_BYTES = 82
+# algorithmic bytes per packet of the classify kernel per variant:
+#   in place: 64 B packet read + 12 B MAC write + 2 B backend write
+#   records:  64 B packet read + 12 B dense MAC record + 2 B backend
+#   read only (north_star's parse + hash + lookup): 64 B read + 2 B backend
+# the whole path adds the grouping kernel's 4 B perm write.
+CLASSIFY_BYTES = {"in_place": 64 + 12 + 2, "records": 64 + 12 + 2, "read_only": 64 + 2}
+PATH_BYTES = {k: v + 4 for k, v in CLASSIFY_BYTES.items()}
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_WARMUP, PMC_STEPS = 10, 40
+PMC_VARIANTS = ("in_place", "records", "read_only")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(batch_host, lut, target_cpu_s=12.0):
-    """Reference per-core loop restated in C (oracle/, kind "port"), timed on this host's cores."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import orc  # test infrastructure: the oracle is the baseline/checker only
+# ---------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle's C port of the reference's per-core loop
+# ---------------------------------------------------------------------------------------------
 
-    L = orc.lib()
+def cpu_inventory():
+    """(CPUs in the affinity mask, cgroup CPU quota in CPUs or None, CPU model).  The GPU box pins a
+    256-CPU affinity mask under a 16-CPU cgroup quota: the quota is the share that really runs."""
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
-    lut32 = np.ascontiguousarray(lut, dtype=np.uint32)
-    buf = batch_host.copy()
-
-    def one():
-        return L.orc_cpu_baseline(buf.ctypes.data, None, SLOT, None, FRAME, BATCH, lut32.ctypes.data, TABLE,
-                                  N_BACKENDS, 1, threads, None)
-
-    one()  # cold pass: page faults, thread start-up
-    t = one()  # a warm pass sizes the sample
-    passes = int(min(max(1, target_cpu_s / max(t * threads, 1e-6)), 2000))
-    total_s = sum(one() for _ in range(passes))
-    mpps = passes * BATCH / total_s / 1e6
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(p), 2)
+    except Exception:
+        pass
     try:
         model = [ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name")][0]
     except Exception:
         model = "unknown"
-    return {"value": round(mpps, 2), "unit": "Mpps", "cores": threads, "kind": "port",
-            "sample": f"{passes} passes over one 1,048,576-packet C2 batch (64-B UDP, 65 backends, M=65537; "
-                      f"FNV-keyed memo map nf.rs:91,104, 32-pkt bursts, per-group 1024-slot rings), "
-                      f"{threads} pinned threads, {total_s * threads:.1f} CPU-s; host CPU: {model}"}
+    return cores, quota, model
 
+
+def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
+    """The reference's per-core producer loop restated in C (oracle/, kind "port"), timed on this
+    host's cores: MAC swap, ipv4_extract_flow, FNV-1a, the FNV-keyed memo map (nf.rs:91,104),
+    lut[hash % M], 32-packet bursts, enqueue into per-group 1024-slot rings.  One pinned thread per
+    allowed core, each streaming its contiguous shard of all 8 batches (512 MiB: DRAM, not cache)
+    `reps` times; single-core and no-memo-map variants beside."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc  # test infrastructure: the oracle is the baseline/checker only
+
+    L = orc.lib()
+    affinity, quota, model = cpu_inventory()
+    cores = max(1, min(affinity, int(quota))) if quota else affinity  # threads that can run at once
+    lut32 = np.ascontiguousarray(lut, dtype=np.uint32)
+    buf = np.concatenate(host_bufs)
+    n_all = BATCH * len(host_bufs)
+
+    def run(n, threads, reps, cache):
+        return L.orc_cpu_baseline_reps(buf.ctypes.data, None, SLOT, None, FRAME, n, lut32.ctypes.data, TABLE,
+                                       N_BACKENDS, 1 if cache else 0, threads, reps, None)
+
+    def measure(n, threads, cache, cpu_s):
+        t = run(n, threads, 1, cache)  # cold pass: page faults, memo fill; also sizes the sample
+        reps = int(min(max(1, cpu_s / max(t * threads, 1e-6)), 10000))
+        s = run(n, threads, reps, cache)
+        return n * reps / s / 1e6, reps, s * threads
+
+    single, r1, c1 = measure(BATCH, 1, True, 2.0)
+    allc, ra, ca = measure(n_all, cores, True, target_cpu_s)
+    nocache, rn, cn = measure(n_all, cores, False, target_cpu_s / 2)
+    return {"value": round(allc, 1), "unit": "Mpps", "cores": cores, "kind": "port",
+            "single_core_mpps": round(single, 2), "no_cache_mpps": round(nocache, 1),
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "cpu_model": model,
+            "sample": f"C port of the reference loop (FNV-keyed memo map nf.rs:91,104, 32-pkt bursts, per-group "
+                      f"1024-slot rings) over the {len(host_bufs)} C2 batches ({n_all:,} 64-B UDP packets, 65 backends, "
+                      f"M=65537): {cores} pinned threads (min of the {affinity}-CPU affinity mask and the cgroup "
+                      f"quota {quota}) x {ra} passes ({ca:.1f} CPU-s); single core {r1} passes "
+                      f"over one 1M batch ({c1:.1f} CPU-s); no memo map {rn} passes ({cn:.1f} CPU-s); "
+                      f"host CPU: {model}"}
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-rank helpers (shared with tests/test_dist_cpu.py)
+# ---------------------------------------------------------------------------------------------
 
 def shard_seed(rank: int, batch: int) -> int:
     """Seed of rank `rank`'s batch `batch`: every rank owns distinct packets (weak scaling)."""
@@ -104,6 +154,39 @@ def shared_lut(names, table, rank, world, device):
     if world > 1:
         dist.broadcast(lut_t, 0)
     return lut_t.cpu().numpy().astype(np.uint16)
+
+
+def lut_digest(lut) -> str:
+    return hashlib.sha256(np.ascontiguousarray(lut, dtype="<u2").tobytes()).hexdigest()[:16]
+
+
+def scatter_shard(global_buf, out, rank: int, world: int) -> None:
+    """Config C4's data-path collective: rank 0 holds the whole batch (world contiguous shards)
+    and scatters shard r to rank r (RCCL ncclScatter over xGMI on GPUs; gloo in the CPU tests).
+    Shard-major order == global packet order, so per-shard grouping composes (SURVEY.md §8e)."""
+    import torch.distributed as dist
+
+    if rank == 0:
+        dist.scatter(out, list(global_buf.chunk(world)), src=0)
+    else:
+        dist.scatter(out, None, src=0)
+
+
+def gather_results(backend, counts, gbuf, gcounts, rank: int, world: int) -> None:
+    """Config C4's return leg: rank 0 collects every shard's backend[] (u16, sent as bytes: RCCL has
+    no 16-bit integer type) and per-group counts (RCCL gather over xGMI on GPUs; gloo in the CPU
+    tests).  Shard-major order == global packet order (SURVEY.md §8e)."""
+    import torch
+    import torch.distributed as dist
+
+    b = backend.view(torch.uint8)
+    c = counts.view(torch.int32)
+    if rank == 0:
+        dist.gather(b, list(gbuf.chunk(world)), dst=0)
+        dist.gather(c, list(gcounts.chunk(world)), dst=0)
+    else:
+        dist.gather(b, None, dst=0)
+        dist.gather(c, None, dst=0)
 
 
 class KernelTimer:
@@ -148,136 +231,269 @@ class KernelTimer:
             self.hip.hipEventDestroy(b)
 
 
-def scatter_shard(global_buf, out, rank: int, world: int) -> None:
-    """Config C4's data-path collective: rank 0 holds the whole batch (world contiguous shards)
-    and scatters shard r to rank r (RCCL ncclScatter over xGMI on GPUs; gloo in the CPU tests).
-    Shard-major order == global packet order, so per-shard grouping composes (SURVEY.md §8e)."""
-    import torch.distributed as dist
+# ---------------------------------------------------------------------------------------------
+# PMC traffic (launcher, N = 1): two rocprofv3 --pmc passes of a short child run
+# ---------------------------------------------------------------------------------------------
 
-    if rank == 0:
-        dist.scatter(out, list(global_buf.chunk(world)), src=0)
-    else:
-        dist.scatter(out, None, src=0)
+def _pmc_rows(d, counter):
+    """Classify-kernel counter values (bytes) in dispatch order from one --pmc pass."""
+    path = None
+    for dp, _, files in os.walk(d):
+        for f in files:
+            if f.endswith("counter_collection.csv"):
+                path = os.path.join(dp, f)
+    if path is None:
+        raise RuntimeError(f"no counter_collection.csv under {d}")
+    rows = []
+    for row in csv.DictReader(open(path)):
+        if row.get("Counter_Name") == counter and "classify_kernel" in row.get("Kernel_Name", ""):
+            rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0))
+    rows.sort()
+    return [v for _, v in rows]
 
 
-def gather_results(backend, counts, gbuf, gcounts, rank: int, world: int) -> None:
-    """Config C4's return leg: rank 0 collects every shard's backend[] (u16, sent as bytes: RCCL has
-    no 16-bit integer type) and per-group counts (RCCL gather over xGMI on GPUs; gloo in the CPU
-    tests).  Shard-major order == global packet order (SURVEY.md §8e)."""
+def pmc_traffic(timeout_s: int = 150):
+    """HBM bytes per classify launch for each variant, measured now (MI355X_MICROARCH.md HBM
+    section: FETCH_SIZE x2 on gfx950 for 16-B-per-lane streaming reads, WRITE_SIZE as read; both in
+    KB).  The child (`--pmc-child`) runs PMC_WARMUP + PMC_STEPS launches of each variant in order."""
+    if shutil.which("rocprofv3") is None:
+        return {"error": "rocprofv3 not found"}
+    env = dict(os.environ, TMPDIR="/tmp")
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"nbg_pmc_{counter}_", dir="/tmp")
+        cmd = ["timeout", "-k", "5", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", counter, "--kernel-trace",
+               "-d", d, "-o", "run", "--output-format", "csv", "--", sys.executable, os.path.abspath(__file__),
+               "--pmc-child"]
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        if r.returncode != 0:
+            shutil.rmtree(d, ignore_errors=True)
+            return {"error": f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr[-300:]}"}
+        try:
+            vals[counter] = _pmc_rows(d, counter)
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    seg = PMC_WARMUP + PMC_STEPS
+    out = {"counters": "FETCH_SIZE x2 + WRITE_SIZE (separate rocprofv3 --pmc passes, KB = 1024 B)",
+           "launches_per_variant": PMC_STEPS}
+    for k, name in enumerate(PMC_VARIANTS):
+        f = vals["FETCH_SIZE"][k * seg + PMC_WARMUP:(k + 1) * seg]
+        w = vals["WRITE_SIZE"][k * seg + PMC_WARMUP:(k + 1) * seg]
+        if len(f) != PMC_STEPS or len(w) != PMC_STEPS:
+            return {"error": f"unexpected classify dispatch count ({len(vals['FETCH_SIZE'])}, "
+                             f"{len(vals['WRITE_SIZE'])})"}
+        rd, wr = 2.0 * float(np.mean(f)), float(np.mean(w))
+        out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
+                     "algorithmic_bytes": BATCH * CLASSIFY_BYTES[name],
+                     "ratio": round((rd + wr) / (BATCH * CLASSIFY_BYTES[name]), 3)}
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# launcher
+# ---------------------------------------------------------------------------------------------
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args, argv) -> int:
+    """Spawn args.gpus rank processes (this process never initialises the GPU), wait for all of
+    them, and print rank 0's JSON line (+ the PMC traffic at N = 1).  A failing rank ends the job."""
+    n = args.gpus
+    if n < 1:
+        raise SystemExit("--gpus must be >= 1")
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NBG_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+    rcs = [None] * n
+    out0 = b""
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.kill()
+                    rcs[r] = p.wait()
+            break
+        time.sleep(0.05)
+    out0 = procs[0].stdout.read()
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        log(f"bench: rank(s) failed: {bad}")
+        return max(abs(rc) for _, rc in bad) or 1
+    lines = [ln for ln in out0.decode().splitlines() if ln.startswith("{")]
+    if not lines:
+        log("bench: rank 0 printed no JSON line")
+        return 1
+    line = json.loads(lines[-1])
+    if n == 1 and not args.selftest and not args.no_pmc:
+        t0 = time.time()
+        pmc = pmc_traffic()
+        log(f"bench: PMC passes {time.time() - t0:.0f}s")
+        line["pmc"] = pmc
+        if isinstance(pmc, dict) and "in_place" in pmc:
+            line["roofline"]["traffic"] = pmc["in_place"]["hbm_bytes"]
+            for k, v in line.get("variants", {}).items():
+                if k in pmc and isinstance(v, dict):
+                    v["traffic"] = pmc[k]["hbm_bytes"]
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+# ---------------------------------------------------------------------------------------------
+# one rank
+# ---------------------------------------------------------------------------------------------
+
+def run_rank(args) -> None:
     import torch
     import torch.distributed as dist
 
-    b = backend.view(torch.uint8)
-    c = counts.view(torch.int32)
-    if rank == 0:
-        dist.gather(b, list(gbuf.chunk(world)), dst=0)
-        dist.gather(c, list(gcounts.chunk(world)), dst=0)
-    else:
-        dist.gather(b, None, dst=0)
-        dist.gather(c, None, dst=0)
-
-
-def read_traffic():
-    """HBM bytes per classify launch from the committed PMC profile (profiles/pmc_*.json), if any."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-    if not files:
-        return None
-    try:
-        return json.load(open(files[-1])).get("classify_hbm_bytes_per_launch")
-    except Exception:
-        return None
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--streams", type=int, default=3)
-    ap.add_argument("--mac-record", action="store_true",
-                    help="write the swapped MACs as dense 12-B egress records instead of in place")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--scatter-steps", type=int, default=50,
-                    help="N>1: steps of the scatter-inclusive pass (RCCL scatter from rank 0 + classify); 0 = skip")
-    args = ap.parse_args()
-
-    import torch
-    import torch.distributed as dist
+    import netbricks_amd as nb
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
-    import netbricks_amd as nb
-
-    names = [f"backend-{i}" for i in range(N_BACKENDS)]
-    if world > 1:
-        lut = shared_lut(names, TABLE, rank, world, dev)  # RCCL broadcast, once per backend set
-        mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(args.streams)]
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}")
+    gpu = not args.selftest
+    if gpu:
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
     else:
-        mgs = [nb.Maglev(names, TABLE, device=local) for _ in range(args.streams)]
-        lut = mgs[0].lut()
-
-    t0 = time.time()
-    host0 = None
-    dbufs = []
-    for b in range(N_BATCHES):
-        buf, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(rank, b))
-        if b == 0:
-            host0 = buf.copy()
-        dbufs.append(torch.from_numpy(buf).to(dev))
-    log(f"[rank {rank}] traces ready in {time.time() - t0:.1f}s")
-    streams = [torch.cuda.Stream(dev) for _ in range(args.streams)]
-    outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
-                 perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
-                 counts=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev),
-                 mac_out=torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) if args.mac_record else None)
-            for _ in range(args.streams)]
-
-    def step(i):
-        j = i % args.streams
-        mgs[j].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
-                        stream=streams[j].cuda_stream, **outs[j])
+        dev = torch.device("cpu")
+    if world > 1:
+        if gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
 
     def sync_all():
-        torch.cuda.synchronize(dev)
+        if gpu:
+            torch.cuda.synchronize(dev)
 
-    for i in range(args.warmup):
-        step(i)
-    sync_all()
-    for m in mgs:
-        m.check()
+    def gather_floats(x: float):
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        if world == 1:
+            return [x]
+        out = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(out, t)
+        return [float(o[0]) for o in out]
 
-    # ---- timed region: K steps over all streams, bracketed by barrier + synchronize
-    if world > 1:
-        dist.barrier()
-    sync_all()
-    start_ev = torch.cuda.Event(enable_timing=True)
-    start_ev.record(torch.cuda.current_stream(dev))
-    for st in streams:
-        st.wait_event(start_ev)
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    sync_all()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        dist.barrier()
-    for m in mgs:
-        m.check()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t[0])
+    names = [f"backend-{i}" for i in range(N_BACKENDS)]
+    lut = shared_lut(names, TABLE, rank, world, dev) if world > 1 else nb.build_lut(names, TABLE)
+    digest = lut_digest(lut)
+    # every rank's LUT digest (first 56 bits as an integer), so rank 0 can show they agree
+    digests = [f"{int(v):013x}" for v in gather_floats(float(int(digest[:13], 16)))]
+
+    t0 = time.time()
+    host_bufs, dbufs = [], []
+    for b in range(1 if args.selftest else N_BATCHES):
+        buf, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(rank, b))
+        if rank == 0 and world == 1:
+            host_bufs.append(buf.copy())
+        dbufs.append(torch.from_numpy(buf).to(dev) if gpu else torch.from_numpy(buf))
+    log(f"[rank {rank}] traces ready in {time.time() - t0:.1f}s")
+
+    if gpu:
+        mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(args.streams)]
+        streams = [torch.cuda.Stream(dev) for _ in range(args.streams)]
+        outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                     perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                     counts=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev))
+                for _ in range(args.streams)]
+        recs = [torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) for _ in range(args.streams)]
+
+    def variant_kw(variant, j):
+        if variant == "records":
+            return dict(swap_macs=True, mac_out=recs[j])
+        return dict(swap_macs=variant == "in_place")
+
+    def step(i, variant="in_place"):
+        if not gpu:
+            return  # selftest: the launcher / process-group / timing logic without HIP
+        j = i % args.streams
+        mgs[j].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME,
+                        stream=streams[j].cuda_stream, **variant_kw(variant, j), **outs[j])
+
+    def timed(variant, steps, warmup, barrier=False):
+        for i in range(warmup):
+            step(i, variant)
+        sync_all()
+        if gpu:
+            for m in mgs:
+                m.check()
+        if barrier and world > 1:
+            dist.barrier()
+        sync_all()
+        if gpu:
+            start_ev = torch.cuda.Event()
+            start_ev.record(torch.cuda.current_stream(dev))
+            for st in streams:
+                st.wait_event(start_ev)
+        t_start = time.perf_counter()
+        for i in range(steps):
+            step(i, variant)
+        sync_all()
+        el = time.perf_counter() - t_start
+        if barrier and world > 1:
+            dist.barrier()
+        if gpu:
+            for m in mgs:
+                m.check()
+        return el
+
+    def kernel_pass(variant, steps):
+        """Classify kernel alone: single stream, HIP events around each launch on the stream it
+        runs on; the grouping is deferred and launched after the stop event."""
+        st = streams[0]
+        kt, gt = KernelTimer(steps), KernelTimer(steps)
+        for i in range(steps):
+            kt.start(i, st.cuda_stream)
+            mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, defer_group=True,
+                            stream=st.cuda_stream, **variant_kw(variant, 0), **outs[0])
+            kt.stop(i, st.cuda_stream)
+            gt.start(i, st.cuda_stream)
+            mgs[0].finish_group(st.cuda_stream)
+            gt.stop(i, st.cuda_stream)
+        sync_all()
+        c_ms, g_ms = kt.ms(), gt.ms()
+        kt.close()
+        gt.close()
+        ach = BATCH * CLASSIFY_BYTES[variant] / (c_ms.mean() / 1e3) / 1e9
+        return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "group_kernel_avg_us": round(g_ms.mean() * 1e3, 2)}
+
+    if args.pmc_child:  # under rocprofv3 --pmc: each variant's launches in a fixed order
+        for v in PMC_VARIANTS:
+            for i in range(PMC_WARMUP + PMC_STEPS):
+                mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME,
+                                stream=streams[0].cuda_stream, **variant_kw(v, 0), **outs[0])
+            sync_all()
+            mgs[0].check()
+        return
+
+    # ---- timed region: K steps over all streams, bracketed by barrier + synchronize, max over ranks
+    elapsed_rank = timed("in_place", args.steps, args.warmup, barrier=True)
+    per_rank_s = gather_floats(elapsed_rank)
+    elapsed = max(per_rank_s)
 
     # ---- C4 scatter-inclusive pass (N > 1): every step rank 0 scatters world x 1M packets over
     #      xGMI and each rank classifies its shard; reported beside the device-resident value
     scatter = None
-    if world > 1 and args.scatter_steps > 0:
+    if gpu and world > 1 and args.scatter_steps > 0:
         try:
             recv = torch.empty(BATCH * SLOT, dtype=torch.uint8, device=dev)
             glob = torch.cat([dbufs[0]] + [torch.empty_like(dbufs[0]) for _ in range(world - 1)]) if rank == 0 else None
@@ -303,9 +519,7 @@ def main():
             for _ in range(args.scatter_steps):
                 sstep()
             sync_all()
-            st_el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
-            dist.all_reduce(st_el, op=dist.ReduceOp.MAX)
-            st_s = float(st_el[0])
+            st_s = max(gather_floats(time.perf_counter() - t1))
             if rank == 0 and int(gc.sum()) != world * BATCH:
                 raise RuntimeError(f"gathered counts sum {int(gc.sum())} != {world * BATCH}")
             scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
@@ -319,48 +533,39 @@ def main():
             log(f"[rank {rank}] scatter-inclusive pass failed: {e}")
             scatter = {"error": str(e)[:200]}
 
-    # ---- roofline pass: classify kernel timed alone (single stream, HIP events around each launch
-    #      on the stream it runs on; grouping deferred and launched after the stop event)
-    st = streams[0]
-    kt, gt = KernelTimer(args.steps), KernelTimer(args.steps)
-    t_single = time.perf_counter()
-    for i in range(args.steps):
-        kt.start(i, st.cuda_stream)
-        mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True,
-                        defer_group=True, stream=st.cuda_stream, **outs[0])
-        kt.stop(i, st.cuda_stream)
-        gt.start(i, st.cuda_stream)
-        mgs[0].finish_group(st.cuda_stream)
-        gt.stop(i, st.cuda_stream)
-    sync_all()
-    single_ms = (time.perf_counter() - t_single) / args.steps * 1e3
-    classify_ms = kt.ms()
-    group_ms = gt.ms()
-    kt.close()
-    gt.close()
-
-    total_pkts = BATCH * args.steps * world
-    mpps = total_pkts / elapsed / 1e6
-    ms_step = elapsed / args.steps * 1e3
-    path_gbps = BATCH * PATH_BYTES * args.steps / elapsed / 1e9  # per GPU
-    ach = BATCH * CLASSIFY_BYTES / (classify_ms.mean() / 1e3) / 1e9
-    traffic = read_traffic()
+    # ---- roofline: the in-place classify kernel timed alone; labelled variants beside (N = 1)
+    roof, variants = None, {}
+    if gpu:
+        roof = kernel_pass("in_place", args.steps)
+        if world == 1 and not args.no_variants:
+            for v in ("records", "read_only"):
+                el = timed(v, args.steps, args.warmup)
+                k = kernel_pass(v, args.steps)
+                variants[v] = {"value": round(BATCH * args.steps / el / 1e6, 1), "unit": "Mpps",
+                               "ms_per_step": round(el / args.steps * 1e3, 5),
+                               "classify_bytes_per_pkt": CLASSIFY_BYTES[v], "path_bytes_per_pkt": PATH_BYTES[v],
+                               **k}
+            variants["records"]["what"] = ("MAC swap written as dense 12-B egress records (packet bytes untouched) "
+                                           "+ grouping, same streams")
+            variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + grouping, "
+                                             "same streams")
 
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if gpu and world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(host0, lut)
+                cpu = cpu_baseline(host_bufs, lut)
             except Exception as e:  # the baseline is informational; never fail the bench on it
                 log(f"cpu baseline failed: {e}")
+        total_pkts = BATCH * args.steps * world
         line = {
             "metric": "Mpps + HBM GB/s device-resident Maglev (64B pkts)",
-            "value": round(mpps, 1),
+            "value": round(total_pkts / elapsed / 1e6, 1),
             "unit": "Mpps",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 5),
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -369,27 +574,67 @@ def main():
             "config": {"workload": "C2: Maglev 65 backends / 65537-slot LUT, 64B synthetic UDP, "
                                    "1M-packet device-resident batch per GPU",
                        "backends": N_BACKENDS, "table_size": TABLE, "batch_pkts": BATCH, "slot_bytes": SLOT,
-                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES,
-                       "mac_swap": "12-B egress records" if args.mac_record else "in place",
+                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "mac_swap": "in place",
                        "group_by": "perm + counts", "streams": args.streams, "parallelism": f"shard{world}"},
-            "hbm_gbps_per_gpu": round(path_gbps, 1),
-            "hbm_bytes_per_pkt": PATH_BYTES,
-            "single_stream_ms_per_step": round(single_ms, 5),
-            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "classify_kernel<GlobalU8,F4,HIST,1>", "bytes_per_pkt": CLASSIFY_BYTES,
-                         "pkts_per_launch": BATCH, "avg_launch_us": round(classify_ms.mean() * 1e3, 2),
-                         "group_kernel_avg_us": round(group_ms.mean() * 1e3, 2)},
-            "cpu_baseline": cpu,
+            "per_gpu_mpps": [round(BATCH * args.steps / s / 1e6, 1) for s in per_rank_s],
+            "lut_digest": digest,
+            "lut_digest_per_rank": digests,
+            "hbm_gbps_per_gpu": round(BATCH * PATH_BYTES["in_place"] * args.steps / elapsed / 1e9, 1),
+            "hbm_bytes_per_pkt": PATH_BYTES["in_place"],
         }
+        if roof is not None:
+            line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                "frac": roof["frac"], "traffic": None,
+                                "kernel": "classify_kernel<GlobalU8,F4,HIST,lean> (in-place MAC swap)",
+                                "bytes_per_pkt": CLASSIFY_BYTES["in_place"], "pkts_per_launch": BATCH,
+                                "avg_launch_us": roof["avg_launch_us"],
+                                "group_kernel_avg_us": roof["group_kernel_avg_us"],
+                                "timing": "single-stream pass, HIP events around each classify launch (grouping "
+                                          "deferred); `value` is the multi-stream rate, where the grouping of one "
+                                          "batch overlaps the classify of the next"}
+        if variants:
+            line["variants"] = variants
+        line["cpu_baseline"] = cpu
         if scatter is not None:
             line["scatter_inclusive"] = scatter
+        if args.selftest:
+            line["selftest"] = True
+            line["data"] = "synthetic (launcher selftest on CPU: no HIP call, steps are empty)"
         print(json.dumps(line), flush=True)
-    for m in mgs:
-        m.close()
+    if gpu:
+        for m in mgs:
+            m.close()
     if world > 1:
         dist.destroy_process_group()
 
 
+def parse_args(argv):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the records / read-only variant passes")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
+    ap.add_argument("--inline", action="store_true",
+                    help="run as a single rank in this process (no launcher; for running under a profiler)")
+    ap.add_argument("--selftest", action="store_true",
+                    help="launcher + rank logic on the CPU with gloo, no HIP call (tests)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--scatter-steps", type=int, default=50,
+                    help="N>1: steps of the scatter-inclusive pass (RCCL scatter from rank 0 + classify); 0 = skip")
+    return ap.parse_args(argv)
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if "WORLD_SIZE" in os.environ or args.inline or args.pmc_child:
+        run_rank(args)
+        return 0
+    return launch(args, argv)
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

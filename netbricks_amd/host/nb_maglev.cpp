@@ -61,9 +61,10 @@ int main(int argc, char** argv) {
       for (size_t i : port->tx_index()) std::fprintf(f, "%zu\n", i);
       std::fclose(f);
     }
-    std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"backends\": %zu}\n", port->rx_total(),
-                static_cast<unsigned long long>(pipe.tx->sent),
-                static_cast<unsigned long long>(pipe.groups->dropped()), names.size());
+    std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"would_panic\": %llu, \"backends\": %zu}\n",
+                port->rx_total(), static_cast<unsigned long long>(pipe.tx->sent),
+                static_cast<unsigned long long>(pipe.groups->dropped()),
+                static_cast<unsigned long long>(pipe.groups->would_panic()), names.size());
   } catch (const nb::NbError& e) {
     std::fprintf(stderr, "nb_maglev: %s\n", e.what());
     return e.code == NBG_ENODEV ? 3 : 1;

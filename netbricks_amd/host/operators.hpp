@@ -32,15 +32,45 @@
 namespace nb {
 
 // ---- packets ----------------------------------------------------------------------------
-// Stand-in for rte_mbuf: data pointer + data_len + the two metadata slots NetBricks uses to
-// save the parsed header and offset (interface/packet.rs:55-64, 217-221).
+// Stand-in for rte_mbuf: data pointer + data_len + the metadata slots NetBricks uses to save the
+// parsed header and offset (interface/packet.rs:54-57: HEADER_SLOT 0, OFFSET_SLOT 1).
+constexpr size_t kHeaderSlot = 0, kOffsetSlot = 1;
 struct MBuf {
   std::vector<uint8_t> storage;  // data room (DPDK: >= 2 KiB, so 64-B windows are owned)
   uint16_t data_len = 0;
   uintptr_t meta[2] = {0, 0};    // HEADER_SLOT, OFFSET_SLOT
   uint64_t port_seq = 0;         // position in the receiving port's stream (bookkeeping)
   uint8_t* data() { return storage.data(); }
+  uint8_t* data_address(size_t off) { return storage.data() + off; }  // native/zcsi/mbuf.rs:34-37
+  // native/zcsi/mbuf.rs:8-21
+  static uintptr_t read_metadata_slot(const MBuf* m, size_t slot) { return m->meta[slot]; }
+  static void write_metadata_slot(MBuf* m, size_t slot, uintptr_t v) { m->meta[slot] = v; }
 };
+
+// Packet<MacHeader, _>: the MAC header view a consumer gets back (interface/packet.rs:22-30).
+struct MacPacket {
+  MBuf* mbuf;
+  uint8_t* header;  // the MAC header (dst 0..5, src 6..11, ethertype 12..13)
+  size_t offset;    // the header's offset from the data start
+  uint8_t* payload() const { return header + 14; }  // MacHeader::offset() == 14 (headers/mac.rs:96-106)
+};
+
+// Packet::save_header_and_offset (interface/packet.rs:211-221) of the packet that
+// parse::<MacHeader>() makes from a received mbuf: the header is the data start and its offset is 0
+// (ReceiveBatch packets start at offset 0, packet_batch.rs:233; parse_header sets
+// offset = self.offset() + NullHeader::offset() = 0, packet.rs:392-399, null_header.rs:18-20).
+inline void save_header_and_offset(MBuf* m) {
+  MBuf::write_metadata_slot(m, kHeaderSlot, reinterpret_cast<uintptr_t>(m->data_address(0)));
+  MBuf::write_metadata_slot(m, kOffsetSlot, 0);
+}
+
+// Packet::restore_saved_header (interface/packet.rs:414-424): None when the header slot is null.
+inline bool restore_saved_header(MBuf* m, MacPacket* out) {
+  const uintptr_t hdr = MBuf::read_metadata_slot(m, kHeaderSlot);
+  if (hdr == 0) return false;
+  *out = MacPacket{m, reinterpret_cast<uint8_t*>(hdr), MBuf::read_metadata_slot(m, kOffsetSlot)};
+  return true;
+}
 
 struct PacketRx {  // interface/mod.rs:11-13
   virtual ~PacketRx() = default;
@@ -147,6 +177,53 @@ inline ParsedMacBatch transform(ParsedMacBatch p, MacSwap) {
   return p;
 }
 
+// RestoreHeader (operators/restore_header.rs:9-67) over a group's consumer batch: every received
+// mbuf gets its saved header back; a null header slot is the reference's `.unwrap()` panic
+// (restore_header.rs:64), thrown here as NbError.
+struct RestoreHeader : Batch {
+  explicit RestoreHeader(std::shared_ptr<Batch> p) : parent(std::move(p)) {}
+  void act() override {
+    parent->act();
+    pkts = parent->pkts;
+    packets.resize(pkts.size());
+    for (size_t i = 0; i < pkts.size(); ++i)
+      if (!restore_saved_header(pkts[i], &packets[i]))
+        throw NbError(NBG_EINVAL, "RestoreHeader: null saved header (restore_header.rs:64 unwrap)");
+  }
+  void done() override {
+    parent->done();
+    pkts.clear();
+    packets.clear();
+  }
+  std::shared_ptr<Batch> parent;
+  std::vector<MacPacket> packets;
+};
+
+// The enqueue half of GroupByProducer::execute (group_by.rs:46-51) for a whole classified batch —
+// the same steps, in the same order, as the Rust GpuMaglevProducer in INTEGRATION.md: walk the
+// groups in perm order; a would-panic packet (group ct = queues.size(): the reference panics on
+// it) is freed, never enqueued; every other packet gets save_header_and_offset and then
+// enqueue_one into its group's queue, where a full queue loses it (mpsc_mbuf_queue.rs:91-115).
+struct EnqueueStats {
+  uint64_t dropped = 0, would_panic = 0;
+};
+inline void enqueue_grouped(MBuf* const* batch, const uint32_t* perm, const uint32_t* counts,
+                            std::vector<std::shared_ptr<MpscQueue>>& queues, EnqueueStats& st) {
+  const size_t ct = queues.size();
+  size_t k = 0;
+  for (size_t g = 0; g <= ct; ++g) {
+    for (uint32_t j = 0; j < counts[g]; ++j) {
+      MBuf* m = batch[perm[k++]];
+      if (g == ct) {  // mbuf_free (native/zcsi/zcsi.rs:44): the pcap port owns the storage here
+        ++st.would_panic;
+        continue;
+      }
+      save_header_and_offset(m);
+      if (!queues[g]->enqueue_one(m)) ++st.dropped;
+    }
+  }
+}
+
 // The Maglev group function of test/maglev (nf.rs:101-106): lut[flow_hash % M].
 class MaglevGroup {
  public:
@@ -169,9 +246,9 @@ class MaglevGroup {
   std::shared_ptr<nbg_maglev> h_;
 };
 
-// GroupBy (group_by.rs:15-113) with the GPU producer.  Packets whose group index would be
-// out of range in the reference (the would-panic sentinel) go to group `ct` (an extra
-// queue, get_group(ct)); everything else keeps the reference semantics.
+// GroupBy (group_by.rs:15-113) with the GPU producer: ct queues, get_group(i) for i < ct.  Packets
+// the reference would panic on (the would-panic sentinel group) are freed by the producer and
+// counted (would_panic()); everything else keeps the reference semantics.
 class GroupBy {
  public:
   GroupBy(ParsedMacBatch parent, uint32_t groups, MaglevGroup fn, StandaloneScheduler& sched,
@@ -182,25 +259,25 @@ class GroupBy {
     // max_batch packets needs room for a whole batch in one group
     uint32_t qsize = 1024;
     while (qsize < 2 * max_batch) qsize <<= 1;
-    for (uint32_t i = 0; i <= groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(qsize));
+    for (uint32_t i = 0; i < groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(qsize));
     producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch);
     task_ = sched.add_task(producer_);
   }
   uint32_t len() const { return groups_; }
 
-  // get_group(i): a ReceiveBatch over the group's MPSC consumer (+ RestoreHeader: the saved
-  // header/offset are in the mbuf metadata slots).
-  std::shared_ptr<ReceiveBatch> get_group(uint32_t i) {
-    if (i > groups_) return nullptr;
+  // get_group(i): RestoreHeader over a ReceiveBatch of the group's MPSC consumer (group_by.rs:102-112).
+  std::shared_ptr<RestoreHeader> get_group(uint32_t i) {
+    if (i >= groups_) return nullptr;
     struct Consumer : PacketRx {
       std::shared_ptr<MpscQueue> q;
       uint32_t recv(MBuf** p, uint32_t cap) override { return q->dequeue(p, cap); }
     };
     auto c = std::make_shared<Consumer>();
     c->q = queues_[i];
-    return std::make_shared<ReceiveBatch>(c);
+    return std::make_shared<RestoreHeader>(std::make_shared<ReceiveBatch>(c));
   }
-  uint64_t dropped() const { return producer_->dropped; }
+  uint64_t dropped() const { return producer_->stats.dropped; }
+  uint64_t would_panic() const { return producer_->stats.would_panic; }
   uint64_t processed() const { return producer_->processed; }
 
  private:
@@ -229,7 +306,7 @@ class GroupBy {
       lens.resize(n);
       backend.resize(n);
       perm.resize(n);
-      counts.resize(queues.size());
+      counts.resize(queues.size() + 1);
       for (size_t i = 0; i < n; ++i) {
         ptrs[i] = batch[i]->data();
         lens[i] = batch[i]->data_len;
@@ -237,15 +314,7 @@ class GroupBy {
       check(nbg_maglev_classify_host(fn.handle(), ptrs.data(), lens.data(), n, parent.swap ? NBG_SWAP_MACS : 0u,
                                      backend.data(), perm.data(), counts.data()),
             "nbg_maglev_classify_host");
-      size_t k = 0;
-      for (size_t g = 0; g < queues.size(); ++g) {
-        for (uint32_t j = 0; j < counts[g]; ++j, ++k) {
-          MBuf* m = batch[perm[k]];
-          m->meta[0] = reinterpret_cast<uintptr_t>(m->data());  // save_header_and_offset
-          m->meta[1] = 14;
-          if (!queues[g]->enqueue_one(m)) ++dropped;           // full queue: packet lost
-        }
-      }
+      enqueue_grouped(batch.data(), perm.data(), counts.data(), queues, stats);
       processed += n;
     }
     ParsedMacBatch parent;
@@ -255,7 +324,8 @@ class GroupBy {
     std::vector<uint8_t*> ptrs;
     std::vector<uint16_t> lens, backend;
     std::vector<uint32_t> perm, counts;
-    uint64_t dropped = 0, processed = 0;
+    EnqueueStats stats;
+    uint64_t processed = 0;
   };
 
   uint32_t groups_;
@@ -268,7 +338,7 @@ class GroupBy {
 // execution receives one burst from the current group, sends it, and rotates the group.
 class MergeSend : public Executable {
  public:
-  MergeSend(std::vector<std::shared_ptr<ReceiveBatch>> parents, std::shared_ptr<PacketTx> port)
+  MergeSend(std::vector<std::shared_ptr<Batch>> parents, std::shared_ptr<PacketTx> port)
       : parents_(std::move(parents)), port_(std::move(port)) {}
   void execute() override {
     auto& b = *parents_[which_];
@@ -280,7 +350,7 @@ class MergeSend : public Executable {
   uint64_t sent = 0;
 
  private:
-  std::vector<std::shared_ptr<ReceiveBatch>> parents_;
+  std::vector<std::shared_ptr<Batch>> parents_;
   std::shared_ptr<PacketTx> port_;
   size_t which_ = 0;
 };
@@ -299,8 +369,8 @@ inline MaglevPipeline maglev(std::shared_ptr<Batch> parent, StandaloneScheduler&
   MaglevGroup lut(backends, lut_size);  // Maglev::new(backends, 65537), nf.rs:90
   auto groups = std::make_shared<GroupBy>(transform(parse_mac(std::move(parent)), MacSwap{}), ct, lut, s,
                                           max_batch);
-  std::vector<std::shared_ptr<ReceiveBatch>> outs;
-  for (uint32_t i = 0; i <= ct; ++i) outs.push_back(groups->get_group(i));  // + sentinel group
+  std::vector<std::shared_ptr<Batch>> outs;
+  for (uint32_t i = 0; i < ct; ++i) outs.push_back(groups->get_group(i));  // nf.rs:109
   auto tx = std::make_shared<MergeSend>(outs, std::move(port));
   s.add_task(tx);
   return {groups, tx};

@@ -253,9 +253,11 @@ typedef struct {
     uint32_t nb;
     int use_cache;
     int cpu;
+    uint32_t reps; /* passes over the shard (the memo map persists, as across the reference's batches) */
     uint16_t *backend; /* optional output */
     uint64_t checksum;
     double seconds;
+    double t_start, t_end; /* CLOCK_MONOTONIC seconds around the thread's loop */
 } orc_shard_t;
 
 #define RING 1024
@@ -290,6 +292,7 @@ static void *shard_main(void *arg) {
     uint64_t sum = 0;
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (uint32_t rep = 0; rep < s->reps; rep++)
     for (uint64_t b = s->begin; b < s->end; b += BURST) {
         uint64_t e = b + BURST < s->end ? b + BURST : s->end;
         /* transform: MAC swap over the burst */
@@ -322,6 +325,8 @@ static void *shard_main(void *arg) {
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     s->seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    s->t_start = (double)t0.tv_sec + 1e-9 * (double)t0.tv_nsec;
+    s->t_end = (double)t1.tv_sec + 1e-9 * (double)t1.tv_nsec;
     s->checksum = sum;
     memo_free(&memo);
     for (uint32_t g = 0; g < ng; g++) free(ring[g]);
@@ -332,27 +337,37 @@ static void *shard_main(void *arg) {
     return NULL;
 }
 
-/* Runs `threads` pinned threads, each over a contiguous shard of [0, n).
- * Returns wall seconds of the slowest shard (max over threads). */
-double orc_cpu_baseline(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens, uint32_t fixed_len,
-                        uint64_t n, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache, int threads,
-                        uint16_t *backend) {
+/* Runs `threads` pinned threads, each `reps` times over a contiguous shard of [0, n).
+ * Returns wall seconds from the first thread's loop start to the last thread's loop end (thread
+ * start-up excluded; threads that do not run concurrently, e.g. under a CPU quota, count in full). */
+double orc_cpu_baseline_reps(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
+                             uint32_t fixed_len, uint64_t n, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache,
+                             int threads, uint32_t reps, uint16_t *backend) {
     if (threads < 1) threads = 1;
+    if (reps < 1) reps = 1;
     orc_shard_t *sh = (orc_shard_t *)calloc(threads, sizeof(orc_shard_t));
     pthread_t *tid = (pthread_t *)calloc(threads, sizeof(pthread_t));
     for (int t = 0; t < threads; t++) {
         sh[t] = (orc_shard_t){buf, offs, stride, lens, fixed_len, n * t / threads, n * (t + 1) / threads,
-                              lut, m, nb, use_cache, threads > 1 ? t : -1, backend, 0, 0.0};
+                              lut, m, nb, use_cache, threads > 1 ? t : -1, reps, backend, 0, 0.0, 0.0, 0.0};
         pthread_create(&tid[t], NULL, shard_main, &sh[t]);
     }
-    double worst = 0.0;
+    double first = 0.0, last = 0.0;
     for (int t = 0; t < threads; t++) {
         pthread_join(tid[t], NULL);
-        if (sh[t].seconds > worst) worst = sh[t].seconds;
+        if (t == 0 || sh[t].t_start < first) first = sh[t].t_start;
+        if (t == 0 || sh[t].t_end > last) last = sh[t].t_end;
     }
     free(sh);
     free(tid);
-    return worst;
+    return last - first;
+}
+
+/* One pass per thread (the round-1 entry point). */
+double orc_cpu_baseline(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens, uint32_t fixed_len,
+                        uint64_t n, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache, int threads,
+                        uint16_t *backend) {
+    return orc_cpu_baseline_reps(buf, offs, stride, lens, fixed_len, n, lut, m, nb, use_cache, threads, 1, backend);
 }
 
 

@@ -41,6 +41,9 @@ def lib():
         L.orc_cpu_baseline.restype = C.c_double
         L.orc_cpu_baseline.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, C.c_uint64, C.c_uint32,
                                        C.c_int, C.c_int, _P]
+        L.orc_cpu_baseline_reps.restype = C.c_double
+        L.orc_cpu_baseline_reps.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, C.c_uint64,
+                                            C.c_uint32, C.c_int, C.c_int, C.c_uint32, _P]
         L.orc_lpm_build.restype = C.c_int
         L.orc_lpm_build.argtypes = [_P, _P, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64)]
         L.orc_lpm_lookup.restype = None

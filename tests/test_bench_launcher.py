@@ -1,0 +1,43 @@
+"""The bench launcher (`bench.py --gpus N`) end to end on the CPU: the parent spawns N rank
+processes (it never touches the GPU), each joins a gloo process group (`--selftest`: the same
+rank logic with no HIP call), and rank 0's JSON line reports N ranks, one rate per rank and the
+identical LUT digest on every rank (the LUT is built on rank 0 and broadcast).  Reference: one
+pipeline per RX queue, framework/src/scheduler/context.rs:241-255."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(n):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--selftest",
+                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=300,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_launcher_spawns_ranks(n):
+    line = _run(n)
+    assert line["n_gpus"] == n
+    assert line["selftest"] is True
+    assert len(line["per_gpu_mpps"]) == n
+    assert len(line["lut_digest_per_rank"]) == n
+    assert len(set(line["lut_digest_per_rank"])) == 1
+    assert line["lut_digest"].startswith(line["lut_digest_per_rank"][0])
+    assert line["config"]["parallelism"] == f"shard{n}"
+    assert line["scaling"] == "weak"
+
+
+def test_rank_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--selftest"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
