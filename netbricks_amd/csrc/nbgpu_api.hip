@@ -72,7 +72,9 @@ struct nbg_maglev {
   HistArgs pending_hist_args{};
   GroupArgs pending_args{};
   ScanArgs pending_scan{};
-  hipStream_t last_stream = nullptr;
+  hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
+  bool issued = false;                // a launch has been issued on last_stream
+  hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
   int grid_lds = 0, grid_global = 0;
   uint32_t tiles_per_wave = 1;        // L2-LUT classify: 64-packet tiles per wave (NBG_TPW)
   // descriptor mode without lengths: a fixed_len-filled u16[] (the kernel reads off[] and len[])
@@ -123,6 +125,38 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+// Setup copies and zeroing (handle creation, buffer growth) on a private non-blocking stream that
+// is synchronised before the call returns.  Never the legacy null stream: hipMemset there returns
+// before it runs and is not ordered with non-blocking streams (tools/memset_probe.py: 6 of 6 trials
+// with a busy null stream zeroed data a later copy on a non-blocking stream had written), which is
+// what let round-1 host-path kernels read zeroed staging windows.
+struct SetupStream {
+  hipStream_t s = nullptr;
+  hipError_t err = hipSuccess;
+  SetupStream() { err = hipStreamCreateWithFlags(&s, hipStreamNonBlocking); }
+  ~SetupStream() {
+    if (s) (void)hipStreamDestroy(s);
+  }
+  hipError_t zero(void* p, size_t bytes) { return err ? err : (err = hipMemsetAsync(p, 0, bytes, s)); }
+  hipError_t h2d(void* d, const void* hsrc, size_t bytes) {
+    return err ? err : (err = hipMemcpyAsync(d, hsrc, bytes, hipMemcpyHostToDevice, s));
+  }
+  hipError_t finish() { return err ? err : (err = hipStreamSynchronize(s)); }
+};
+
+// A handle's kernels share its scratch (the ping-pong partition histograms), so consecutive calls
+// must run in call order even when they name different streams (NBG_DEFER_GROUP's finish_group on
+// another stream, a host submit after device calls, or a caller that moves the handle between
+// streams): when the stream changes, the new stream waits for everything issued so far on the
+// previous one.  Calls that stay on one stream pay nothing.
+int order_after_last(nbg_maglev* h, hipStream_t s) {
+  if (!h->issued || h->last_stream == s) return NBG_OK;
+  if (!h->order_ev) NBG_HIP(hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming));
+  NBG_HIP(hipEventRecord(h->order_ev, h->last_stream));
+  NBG_HIP(hipStreamWaitEvent(s, h->order_ev, 0));
+  return NBG_OK;
+}
 
 void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_fixed_len);
@@ -181,13 +215,15 @@ int upload(nbg_maglev* h) {
     for (uint64_t j = 0; j < h->m; ++j) buf[j] = static_cast<uint8_t>(h->lut_host[j]);
   }
   NBG_HIP(hipMalloc(&h->d_lut, h->lut_bytes));
-  NBG_HIP(hipMemcpy(h->d_lut, buf.data(), h->lut_bytes, hipMemcpyHostToDevice));
   const size_t nbins = h->nb + 1;
   NBG_HIP(hipMalloc(&h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t)));
-  NBG_HIP(hipMemset(h->d_part_hist, 0, 2 * kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
+  SetupStream st;  // complete before the handle is returned: any caller stream may use it next
+  (void)st.h2d(h->d_lut, buf.data(), h->lut_bytes);
+  (void)st.zero(h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t));
+  NBG_HIP(st.finish());  // reports the first failure of the sequence
   if (const char* e = std::getenv("NBG_TPW")) {
     const int v = std::atoi(e);
     h->tiles_per_wave = 1;
@@ -338,6 +374,7 @@ void nbg_maglev_destroy(nbg_maglev* h) {
     free_scratch(h);
     free_host_path(h);
     (void)hipFree(h->d_lut);
+    if (h->order_ev) (void)hipEventDestroy(h->order_ev);
   }
   delete h;
 }
@@ -394,6 +431,8 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const uint32_t nbins = h->nb + 1;
   if (group && nbins > kMaxGroupBins)
     return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
+  int rc = order_after_last(h, static_cast<hipStream_t>(stream));
+  if (rc) return rc;
   const bool lds = use_lds_lut(h, flags);
   // each wave walks tpw consecutive 64-packet tiles (software-pipelined); the LDS-LUT variant
   // runs a resident grid of 1024-thread blocks so that the LUT staging is amortised
@@ -467,7 +506,9 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     a.gate = d_gate;
     a.mac_out = nullptr;
   }
-  int rc = launch_classify(a, h->wide, lds, grid, stream);
+  h->last_stream = static_cast<hipStream_t>(stream);
+  h->issued = true;
+  rc = launch_classify(a, h->wide, lds, grid, stream);
   if (rc) return rc;
   if (group) {
     ScanArgs sa{};
@@ -514,7 +555,6 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
       if ((rc = launch_group(ga, scan, stream))) return rc;
     }
   }
-  h->last_stream = static_cast<hipStream_t>(stream);
   return NBG_OK;
 }
 
@@ -557,9 +597,10 @@ int nbg_lpm_create(const uint32_t* prefixes, const uint8_t* lens, const uint16_t
   t->long_used = used;
   DeviceGuard g(device);
   const uint64_t nl = used ? used : 1;
+  SetupStream st;
   if (hipMalloc(&t->d_tbl24, t24.size() * 2) != hipSuccess || hipMalloc(&t->d_tbl_long, nl * 2) != hipSuccess ||
-      hipMemcpy(t->d_tbl24, t24.data(), t24.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(t->d_tbl_long, tl.data(), nl * 2, hipMemcpyHostToDevice) != hipSuccess) {
+      st.h2d(t->d_tbl24, t24.data(), t24.size() * 2) != hipSuccess ||
+      st.h2d(t->d_tbl_long, tl.data(), nl * 2) != hipSuccess || st.finish() != hipSuccess) {
     nbg_lpm_destroy(t);
     return set_error(NBG_ENOMEM, "nbg_lpm_create: device allocation/upload failed");
   }
@@ -591,17 +632,19 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   if (!h->pending) return NBG_OK;
   DeviceGuard g(h->device);
   h->pending = false;
-  int rc;
+  int rc = order_after_last(h, static_cast<hipStream_t>(stream));  // after the classify, on any stream
+  if (rc) return rc;
+  h->last_stream = static_cast<hipStream_t>(stream);
   if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;
   if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
   if ((rc = launch_group(h->pending_args, h->pending_scan_mode, stream))) return rc;
-  h->last_stream = static_cast<hipStream_t>(stream);
   return NBG_OK;
 }
 
 int nbg_maglev_check(nbg_maglev* h) {
   if (!h) return set_error(NBG_EINVAL, "check: null handle");
   DeviceGuard g(h->device);
+  if (!h->issued) return NBG_OK;
   NBG_HIP(hipStreamSynchronize(h->last_stream));
   NBG_HIP(hipGetLastError());
   return NBG_OK;
@@ -659,7 +702,9 @@ int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
   NBG_HIP(hipMalloc(&t.d_backend, cap * 2));
   NBG_HIP(hipMalloc(&t.d_perm, cap * 4));
   NBG_HIP(hipMalloc(&t.d_counts, nbins * 4));
-  NBG_HIP(hipMemset(t.d_win, 0, win_bytes));  // the slack past the last window is read, never used
+  // the slack past the last window is read, never used; zeroed in stream order before the H2D
+  // copies that follow on the same stream (not on the null stream: see SetupStream)
+  NBG_HIP(hipMemsetAsync(t.d_win, 0, win_bytes, h->host_compute));
   t.cap = cap;
   return NBG_OK;
 }

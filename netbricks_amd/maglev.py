@@ -28,6 +28,32 @@ def _ptr(t) -> Optional[int]:
     return t.data_ptr()
 
 
+def _check_np(name: str, a, dtype, min_size: int) -> None:
+    """The library writes min_size elements of `dtype` through a raw pointer: refuse anything else."""
+    if not isinstance(a, np.ndarray):
+        raise ValueError(f"{name}: expected a numpy array, got {type(a).__name__}")
+    if a.dtype != np.dtype(dtype):
+        raise ValueError(f"{name}: dtype {a.dtype}, expected {np.dtype(dtype)}")
+    if not a.flags.c_contiguous or not a.flags.writeable:
+        raise ValueError(f"{name}: must be C-contiguous and writeable")
+    if a.size < min_size:
+        raise ValueError(f"{name}: {a.size} elements, needs >= {min_size}")
+
+
+def _check_dev(name: str, t, dtype, min_size: int, device) -> None:
+    """Device outputs/inputs handed to the library as raw pointers: dtype, contiguity, size, device."""
+    if t is None:
+        return
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.numel() < min_size:
+        raise ValueError(f"{name}: {t.numel()} elements, needs >= {min_size}")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+
+
 def build_lut(backends: Sequence[str], lut_size: int = 65537) -> np.ndarray:
     """The product's host LUT builder (Maglev::new, nf.rs:70-76) -> u16 entries."""
     arr, lens, _keep = _lib.names_args(backends)
@@ -119,6 +145,18 @@ class Maglev:
         import torch
 
         dev = pkts.device
+        if pkts.dtype != torch.uint8 or not pkts.is_contiguous():
+            raise ValueError("pkts: expected a contiguous uint8 tensor")
+        if dev.type != "cuda" or dev.index != self.device:
+            raise ValueError(f"pkts: on {dev}, expected cuda:{self.device}")
+        if offsets is None and n_pkts and (n_pkts - 1) * stride + min(frame_len, stride) > pkts.numel():
+            raise ValueError("pkts: smaller than n_pkts fixed slots")
+        _check_dev("offsets", offsets, torch.uint32, n_pkts, dev)
+        _check_dev("lens", lens, torch.uint16, n_pkts, dev)
+        _check_dev("backend", backend, torch.uint16, n_pkts, dev)
+        _check_dev("perm", perm, torch.uint32, n_pkts, dev)
+        _check_dev("counts", counts, torch.uint32, self.n_backends + 1, dev)
+        _check_dev("mac_out", mac_out, torch.uint8, 12 * n_pkts, dev)
         if backend is None:
             backend = torch.empty(n_pkts, dtype=torch.uint16, device=dev)
         scatter = group and scatter
@@ -155,6 +193,13 @@ class Maglev:
         ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
         lens = np.ascontiguousarray(lens, dtype=np.uint16)
         n = ptrs.size
+        if lens.size != n:
+            raise ValueError(f"lens: {lens.size} entries for {n} frames")
+        _check_np("backend", backend, np.uint16, n)
+        if perm is not None:
+            _check_np("perm", perm, np.uint32, n)
+        if counts is not None:
+            _check_np("counts", counts, np.uint32, self.n_backends + 1)
         ticket = C.c_uint64(0)
         rc = lib.nbg_maglev_host_submit(self._h, ptrs.ctypes.data, lens.ctypes.data, n,
                                         NBG_SWAP_MACS if swap_macs else 0, backend.ctypes.data,
