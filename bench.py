@@ -246,7 +246,8 @@ def _pmc_rows(d, counter):
         raise RuntimeError(f"no counter_collection.csv under {d}")
     rows = []
     for row in csv.DictReader(open(path)):
-        if row.get("Counter_Name") == counter and "classify_kernel" in row.get("Kernel_Name", ""):
+        name = row.get("Kernel_Name", "")
+        if row.get("Counter_Name") == counter and ("classify_stream_kernel" in name or "classify_kernel" in name):
             rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0))
     rows.sort()
     return [v for _, v in rows]
@@ -585,7 +586,7 @@ def run_rank(args) -> None:
         if roof is not None:
             line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": roof["frac"], "traffic": None,
-                                "kernel": "classify_kernel<GlobalU8,F4,HIST,lean> (in-place MAC swap)",
+                                "kernel": "classify_stream_kernel<F4,HIST,in place> (LDS LUT, LDS-DMA tile ring)",
                                 "bytes_per_pkt": CLASSIFY_BYTES["in_place"], "pkts_per_launch": BATCH,
                                 "avg_launch_us": roof["avg_launch_us"],
                                 "group_kernel_avg_us": roof["group_kernel_avg_us"],

@@ -8,6 +8,15 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+try:
+    # torch ships its own libamdhip64 / libhsa-runtime64.  Load them before libnbgpu.so so that the
+    # library binds to that runtime (same SONAME): loaded first, libnbgpu.so would pull in the
+    # system runtime and torch a second one, and a second HSA runtime in the process sees no GPU
+    # ("no ROCm-capable device is detected").  Importing torch does not initialise the GPU.
+    import torch  # noqa: F401
+except ImportError:  # the C-ABI needs no torch; only the device-memory plumbing does
+    pass
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # NBG_LIB_OVERRIDE: diagnostic builds of the same library (tools/); never set by the product
 LIB_PATH = os.environ.get("NBG_LIB_OVERRIDE") or os.path.join(_HERE, "libnbgpu.so")

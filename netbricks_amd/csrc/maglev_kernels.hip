@@ -32,7 +32,7 @@ constexpr uint32_t kSentinel = NBG_SENTINEL;
 constexpr uint32_t kEth = 14;
 
 // LUT placement / width variants.
-enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3 };
+enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3, kLdsU8Tail = 4 };
 
 // Packet layouts: fixed slots (general), fixed slots known by the host to be 16-B aligned with
 // owned windows, no length array and frames >= 48 B (every chunk readable, no per-lane
@@ -92,6 +92,7 @@ __device__ __forceinline__ uint32_t lut_get(const ClassifyArgs& a, const uint8_t
   if constexpr (LUTM == kLdsU8) return lut_lds[idx];
   if constexpr (LUTM == kLdsU16) return reinterpret_cast<const uint16_t*>(lut_lds)[idx];
   if constexpr (LUTM == kGlobalU8) return static_cast<const uint8_t*>(a.lut)[idx];
+  if constexpr (LUTM == kLdsU8Tail) return idx < 65536u ? lut_lds[idx] : a.lut_tail;  // streaming kernel
   return static_cast<const uint16_t*>(a.lut)[idx];
 }
 
@@ -495,6 +496,258 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     }
   }
   CPROBE(3)
+}
+
+// ---- streaming classify (fixed 64-B-aligned slots, u8 LUT <= 65537 entries) -------------------
+//
+// One 512-thread block per CU (persistent).  The block stages the LUT in LDS once with LDS-DMA
+// (entries 0..65535; entry 65536 of a 65537-slot table is the kernel argument lut_tail), so the
+// per-packet lookup is an LDS read instead of an L2 gather (a 1M-packet batch of L2 gathers costs
+// ~3.3 us of L2 request throughput).  Each wave then streams 64-packet tiles through a
+// private ring of kRing LDS buffers: every packet's row lands packet-major by global_load_lds_dwordx4
+// straight from HBM — no VGPRs held by loads in flight, no transpose — while the wave classifies the
+// tile kStreamAhead tiles behind.  Tiles are interleaved so that the whole grid sweeps the batch
+// sequentially; the block's backend histogram is flushed once per unit of W tiles.
+//
+// LDS-DMA writes are ordered for the issuing wave's ds_read only by its own covering vmcnt
+// (MI355X_MICROARCH.md item 7).  hipcc does not count the inline-asm loads, so each tile is waited
+// for with a counted s_waitcnt vmcnt(4 * tiles issued after it): other VM operations issued in
+// between (stores, flush atomics, the compiler's slow-path loads) only make that wait conservative.
+#ifndef NBG_SW
+#define NBG_SW 8
+#endif
+#ifndef NBG_SRING
+#define NBG_SRING 2
+#endif
+constexpr int kStreamNT = 64 * NBG_SW;         // threads per block (8 waves)
+constexpr int kStreamW = kStreamNT / 64;
+constexpr int kRing = NBG_SRING;               // LDS tile buffers per wave
+constexpr int kStreamAhead = kRing - 1;        // tiles in flight while one is classified
+// LDS bytes per packet: 48 (chunks 0..2, all the classify reads) for read-only and records; 64 (the
+// whole slot) for the in-place swap, which then writes every line back whole from LDS (measured:
+// 48-B rows read faster, whole-line write-back beats 16-B partial-line stores)
+template <int MODE>
+constexpr uint32_t row_of() { return MODE == 1 ? 64u : 48u; }
+constexpr uint32_t kLutLds = 65536;            // LUT bytes staged in LDS
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)(p)));
+}
+
+// 16 B per active lane from `src` into LDS at m0 + lane * 16 (lds_base wave-uniform).
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Wait until tile i's four LDS-DMA loads landed: `ahead` tiles (0..5) were issued after it.
+__device__ __forceinline__ void wait_tile(uint32_t ahead) {
+  if (ahead >= 5) wait_vm<20>();
+  else if (ahead == 4) wait_vm<16>();
+  else if (ahead == 3) wait_vm<12>();
+  else if (ahead == 2) wait_vm<8>();
+  else if (ahead == 1) wait_vm<4>();
+  else wait_vm<0>();
+}
+
+// Issue tile `t` (64 packets from tile base `tb`) into the LDS buffer at `buf`: instruction k
+// covers packets 16k..16k+15.  48-B rows: lane l < 48 fetches chunk l % 3 of packet 16k + l / 3;
+// 64-B rows: lane l fetches chunk l % 4 of packet 16k + l / 4 (1 KiB contiguous).  Lanes past the
+// batch end fetch the batch base (their rows are never read).
+template <uint32_t kRow>
+__device__ __forceinline__ void issue_tile(const ClassifyArgs& a, uint32_t tb, uint32_t buf, uint32_t lane) {
+  constexpr uint32_t kCh = kRow / 16u;
+  if (kCh == 4u || lane < 16u * kCh) {
+    const uint32_t pk = lane / kCh, ch = lane - pk * kCh;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t p = tb + k * 16u + pk;
+      const uint8_t* src = p < a.n_pkts ? a.pkts + static_cast<size_t>(p) * a.stride + ch * 16u : a.pkts;
+      glds16(src, buf + k * (16u * kRow));
+    }
+  }
+}
+
+template <bool HIST>
+__device__ __forceinline__ void stream_flush(const ClassifyArgs& a, uint32_t* hist, uint32_t nbins, uint32_t part,
+                                             uint32_t lane) {
+  if constexpr (HIST) {
+    if (a.hist16) {
+      const uint32_t hw = (nbins + 1) >> 1;
+      uint32_t* row = a.part_hist + static_cast<size_t>(part) * hw;
+      for (uint32_t w = lane; w < hw; w += 64) {
+        const uint32_t h = hist[2 * w] | (2 * w + 1 < nbins ? hist[2 * w + 1] << 16 : 0u);
+        if (h) atomicAdd(&row[w], h);
+      }
+    } else {
+      uint32_t* row = a.part_hist + static_cast<size_t>(part) * nbins;
+      for (uint32_t b = lane; b < nbins; b += 64) {
+        const uint32_t h = hist[b];
+        if (h) atomicAdd(&row[b], h);
+      }
+    }
+    for (uint32_t b = lane; b < nbins; b += 64) hist[b] = 0;
+  }
+}
+
+// Classify one tile from its LDS ring buffer `x` (row of this lane's packet) and write the results.
+// Returns the bin to count (histogram) through `bin`; false when the lane has no packet.
+template <bool F4, int MODE, uint32_t kRow = row_of<MODE>()>
+__device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uint8_t* lut, const uint8_t* x,
+                                                uint32_t p, uint32_t& bin_out, bool& slow_out) {
+  const bool valid = p < a.n_pkts;
+  const uint4 c0 = *reinterpret_cast<const uint4*>(x);
+  const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
+  const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
+  const bool fast = valid && ((c0.w >> 16) & 0xfu) == 5u;  // lean layout: aligned, frames >= 48 B
+  // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
+  const uint32_t src = (c1.z >> 16) | (c1.w << 16);
+  const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
+  const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
+#if NBG_SABL == 2  // measurement build: no hash, no lookup (bin from the header bytes)
+  bin_out = (src ^ dst ^ ports) % a.nb;
+#elif NBG_SABL == 3  // measurement build: FNV, no lookup
+  uint32_t lo, hi;
+  fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+  bin_out = (lo ^ hi) % a.nb;
+#else
+  uint32_t lo, hi;
+  fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+  const uint32_t idx = F4 ? mod_f4(lo, hi) : mod_barrett(lo, hi, a.m, a.mu);
+  const uint32_t e = lut[idx & 0xffffu];
+  bin_out = (idx >> 16) ? a.lut_tail : e;
+#endif
+  if constexpr (MODE == 1) {
+    static_assert(kRow == 64, "the in-place swap writes whole slots back from 64-B rows");
+    // whole-line write-back from the tile's LDS rows: lane (quad, part) stores chunk `part` of packet
+    // 16k + quad (1 KiB contiguous per instruction), chunk 0 with the MACs swapped; a packet off
+    // the fast path keeps its chunk 0 for the byte-wise path
+    const uint8_t* tile = x - (p & 63u) * kRow;
+    const uint32_t part = p & 3u, quad = (p & 63u) >> 2;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t q = (p & ~63u) + k * 16u + quad;
+      uint4 v = *reinterpret_cast<const uint4*>(tile + (k * 16u + quad) * kRow + part * 16u);
+      // the quad's chunk-0 lane holds bytes 12..15 (IHL)
+      const uint32_t w3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v.w), 0x00, 0xf, 0xf, false));
+      const bool qfast = q < a.n_pkts && ((w3 >> 16) & 0xfu) == 5u;
+      if (part == 0u)
+        v = make_uint4((v.y >> 16) | (v.z << 16), (v.z >> 16) | (v.x << 16), (v.x >> 16) | (v.y << 16), v.w);
+      if (qfast) stg16_nt(a.pkts + static_cast<size_t>(q) * a.stride + part * 16u, v);
+    }
+  } else if constexpr (MODE == 2) {
+    if (fast) {
+      uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(p) * 12u);
+      mo[0] = (c0.y >> 16) | (c0.z << 16);
+      mo[1] = (c0.z >> 16) | (c0.x << 16);
+      mo[2] = (c0.x >> 16) | (c0.y << 16);
+    }
+  }
+  slow_out = valid && !fast;
+  return valid;
+}
+
+// The packet's backend (and its slow path, after the tile's next loads are issued).
+template <bool F4>
+__device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const uint8_t* lut, uint32_t p, uint32_t bin,
+                                                  bool slow) {
+  if (slow) {
+    uint32_t gate;
+    bin = classify_slow<kLdsU8Tail, F4, false>(a, lut, a.pkts + static_cast<size_t>(p) * a.stride, a.fixed_len, p,
+                                               gate);
+  }
+  a.backend[p] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+  return bin;
+}
+
+// MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
+template <bool F4, bool HIST, int MODE>
+__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a) {
+  constexpr uint32_t kRow = row_of<MODE>(), kTileLds = 64u * kRow;
+  extern __shared__ __align__(16) uint8_t smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nbins = a.nb + 1;
+  uint8_t* lut = smem;
+  uint8_t* ring = smem + kLutLds + wave * (kRing * kTileLds);
+  const uint32_t hstride = (nbins + 3) & ~3u;
+  uint32_t* hist_base = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
+  const uint32_t n_tiles = (a.n_pkts + 63u) >> 6;
+  // Interleaved units: unit u = tiles [u*W, u*W + W), one per wave; block b takes units b, b + G,
+  // b + 2G, ...  At any moment the grid reads consecutive units: one sequential sweep of the batch
+  // (contiguous per-wave runs read ~3k streams at a fixed stride and measured 10 % slower:
+  // HBM channel imbalance).  The block's histogram is double-buffered per unit and flushed by one
+  // wave behind one LDS-only barrier; a unit (W tiles = 512 packets) never straddles a partition.
+  const uint32_t n_units = (n_tiles + kStreamW - 1) / kStreamW;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t nt = b < n_units ? (n_units - b + G - 1) / G : 0u;  // units of this block (block-uniform)
+  auto tile_of = [&](uint32_t k) { return (b + k * G) * kStreamW + wave; };
+  uint32_t* hist = hist_base;  // [2][hstride]
+
+  // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
+  // waves (the device LUT is padded to whole pieces); the first tiles go out behind them
+#if NBG_SABL == 1  // measurement build: no LUT staging (wrong backends; timing only)
+  const uint32_t pieces = 0;
+#else
+  const uint32_t pieces = a.lut_lds_bytes >> 10;
+#endif
+  for (uint32_t q = wave; q < pieces; q += kStreamW)
+    glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
+  const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
+  for (uint32_t k = 0; k < first; ++k) issue_tile<kRow>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
+  if constexpr (HIST)
+    for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
+  // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
+  // makes every wave's pieces visible to every wave
+  wait_tile(first);
+  lds_sync();
+
+  for (uint32_t k = 0; k < nt; ++k) {
+    const uint32_t t = tile_of(k);
+    const uint32_t tb = t * 64u;
+    wait_tile(min(nt - 1u - k, static_cast<uint32_t>(kStreamAhead)));
+    const uint32_t p = tb + lane;
+    uint32_t bin = 0;
+    bool slow = false;
+    const bool valid = t < n_tiles && stream_classify<F4, MODE>(a, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+                                                                 p, bin, slow);
+    // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
+    // tile is classified, kStreamAhead tiles stay in flight
+    if (k + kRing < nt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue_tile<kRow>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
+    }
+    if (valid) {
+      bin = stream_finish<F4>(a, lut, p, bin, slow);
+      if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
+    }
+    if constexpr (HIST) {
+      // every wave's counts of unit k are in hist[k & 1]; one wave flushes it into the unit's
+      // partition row and zeroes it.  The next barrier (unit k + 1) orders that before unit k + 2
+      // counts into the same buffer.
+      lds_sync();
+      if (wave == k % kStreamW) {
+        uint32_t* h = hist + (k & 1u) * hstride;
+        stream_flush<HIST>(a, h, nbins, ((b + k * G) * kStreamW * 64u) / a.part_pkts, lane);
+      }
+    }
+  }
 }
 
 // Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
@@ -960,12 +1213,47 @@ int launch_mode(const ClassifyArgs& a, bool hist, int grid, size_t lds, hipStrea
   return hist ? launch_v<LUTM, false, true>(a, grid, lds, s) : launch_v<LUTM, false, false>(a, grid, lds, s);
 }
 
+template <bool F4, bool HIST>
+int launch_stream_mode(const ClassifyArgs& a, int mode, int grid, size_t lds, hipStream_t s) {
+  auto fn = mode == 1 ? classify_stream_kernel<F4, HIST, 1>
+                      : (mode == 2 ? classify_stream_kernel<F4, HIST, 2> : classify_stream_kernel<F4, HIST, 0>);
+  static bool attr_set[2][2][3] = {};
+  if (!attr_set[F4][HIST][mode]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return set_error(NBG_EIO, "streaming classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+    attr_set[F4][HIST][mode] = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "streaming classify launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
 size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
   const uint32_t waves = (lut_lds_bytes ? kLdsBlock : kBlock) / 64;
   return static_cast<size_t>(lut_lds_bytes) + waves * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
 }
 
 }  // namespace
+
+size_t stream_lds(uint32_t nb, int mode) {
+  const size_t hwords = 2 * (((nb + 1) + 3) & ~3u);
+  const size_t tile = 64u * (mode == 1 ? row_of<1>() : row_of<0>());
+  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + hwords * 4u;
+}
+
+int stream_waves_per_block() { return kStreamW; }
+
+int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
+  const bool hist = a.part_hist != nullptr;
+  const int mode = !a.swap ? 0 : (a.mac_out ? 2 : 1);
+  const size_t lds = stream_lds(a.nb, mode);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (a.m == 65537u)
+    return hist ? launch_stream_mode<true, true>(a, mode, grid, lds, s) : launch_stream_mode<true, false>(a, mode, grid, lds, s);
+  return hist ? launch_stream_mode<false, true>(a, mode, grid, lds, s) : launch_stream_mode<false, false>(a, mode, grid, lds, s);
+}
 
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;

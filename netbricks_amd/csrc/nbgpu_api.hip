@@ -58,7 +58,9 @@ struct nbg_maglev {
   std::vector<uint16_t> lut_host;
   void* d_lut = nullptr;      // u8 (nb <= 256) or u16 entries, padded to 16 B
   bool wide = false;
-  uint32_t lut_bytes = 0;     // padded device LUT bytes
+  uint32_t lut_bytes = 0;     // LUT bytes (padded to 16 B)
+  uint32_t lut_alloc = 0;     // device LUT allocation: lut_bytes rounded up to 1 KiB (LDS-DMA pieces)
+  int cus = 0;                // compute units (streaming classify: one block per CU)
   // grouping scratch (independent of the batch size: at most kMaxParts partitions)
   uint32_t* d_part_hist = nullptr;    // [2][kMaxParts][nb+1] ping-pong partition histograms
   uint32_t* d_part_prefix = nullptr;  // [kMaxParts][nb+1] (scan-kernel fallback)
@@ -208,20 +210,21 @@ int upload(nbg_maglev* h) {
   h->wide = h->nb > 256;
   const size_t esz = h->wide ? 2 : 1;
   h->lut_bytes = static_cast<uint32_t>((h->m * esz + 15) & ~uint64_t(15));
-  std::vector<uint8_t> buf(h->lut_bytes, 0);
+  h->lut_alloc = (h->lut_bytes + 1023u) & ~1023u;
+  std::vector<uint8_t> buf(h->lut_alloc, 0);
   if (h->wide) {
     std::memcpy(buf.data(), h->lut_host.data(), h->m * 2);
   } else {
     for (uint64_t j = 0; j < h->m; ++j) buf[j] = static_cast<uint8_t>(h->lut_host[j]);
   }
-  NBG_HIP(hipMalloc(&h->d_lut, h->lut_bytes));
+  NBG_HIP(hipMalloc(&h->d_lut, h->lut_alloc));
   const size_t nbins = h->nb + 1;
   NBG_HIP(hipMalloc(&h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
   SetupStream st;  // complete before the handle is returned: any caller stream may use it next
-  (void)st.h2d(h->d_lut, buf.data(), h->lut_bytes);
+  (void)st.h2d(h->d_lut, buf.data(), h->lut_alloc);
   (void)st.zero(h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t));
   NBG_HIP(st.finish());  // reports the first failure of the sequence
   if (const char* e = std::getenv("NBG_TPW")) {
@@ -229,6 +232,8 @@ int upload(nbg_maglev* h) {
     h->tiles_per_wave = 1;
     while (static_cast<int>(h->tiles_per_wave) < v && h->tiles_per_wave < 64) h->tiles_per_wave <<= 1;
   }
+  if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || h->cus <= 0)
+    return set_error(NBG_ENODEV, "hipDeviceGetAttribute(CU count) failed");
   int rc = classify_grid(true, h->lut_bytes, h->nb, h->device, &h->grid_lds);
   if (rc) return rc;
   return classify_grid(false, 0, h->nb, h->device, &h->grid_global);
@@ -238,6 +243,16 @@ int upload(nbg_maglev* h) {
 // occupancy); NBG_LUT_LDS stages it in LDS when it fits.
 bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
   return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024;
+}
+
+// The streaming classify kernel serves fixed 64-B-aligned slots with a u8 LUT of at most 65537
+// entries (config C2); NBG_STREAM=0 selects the tile-per-wave kernel instead (A/B measurements).
+bool use_stream(const nbg_maglev* h) {
+  static const bool on = [] {
+    const char* e = std::getenv("NBG_STREAM");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on && !h->wide && h->m <= 65537;
 }
 
 // Persistent host worker pool for the host path's gather and MAC write-back (bound by host
@@ -309,9 +324,11 @@ void parallel_for(uint64_t n, F fn) {
 
 int finish_create(nbg_maglev* h, int device, nbg_maglev** out) {
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+  const hipError_t ce = hipGetDeviceCount(&ndev);
+  if (ce != hipSuccess || ndev <= 0) {
     delete h;
-    return set_error(NBG_ENODEV, "no HIP device available (the Maglev path has no CPU fallback)");
+    return set_error(NBG_ENODEV, "no HIP device available (the Maglev path has no CPU fallback): %s, %d devices",
+                     hipGetErrorString(ce), ndev);
   }
   if (device < 0 || device >= ndev) {
     delete h;
@@ -508,7 +525,15 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   }
   h->last_stream = static_cast<hipStream_t>(stream);
   h->issued = true;
-  rc = launch_classify(a, h->wide, lds, grid, stream);
+  if (a.lean && !lds && !lpm && use_stream(h)) {
+    const uint64_t waves = static_cast<uint64_t>(h->cus) * stream_waves_per_block();
+    a.tiles_per_wave = static_cast<uint32_t>((n_tiles64 + waves - 1) / waves);
+    a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
+    a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+    rc = launch_classify_stream(a, h->cus, stream);
+  } else {
+    rc = launch_classify(a, h->wide, lds, grid, stream);
+  }
   if (rc) return rc;
   if (group) {
     ScanArgs sa{};
@@ -584,8 +609,10 @@ int nbg_lpm_create(const uint32_t* prefixes, const uint8_t* lens, const uint16_t
   if (!out || ((!prefixes || !lens || !gates) && n)) return set_error(NBG_EINVAL, "nbg_lpm_create: null argument");
   *out = nullptr;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
-    return set_error(NBG_ENODEV, "no HIP device available (the LPM path has no CPU fallback)");
+  const hipError_t ce = hipGetDeviceCount(&ndev);
+  if (ce != hipSuccess || ndev <= 0)
+    return set_error(NBG_ENODEV, "no HIP device available (the LPM path has no CPU fallback): %s, %d devices",
+                     hipGetErrorString(ce), ndev);
   if (device < 0 || device >= ndev) return set_error(NBG_ENODEV, "device %d out of range (%d devices)", device, ndev);
   std::vector<uint16_t> t24, tl;
   uint64_t used = 0;

@@ -47,6 +47,7 @@ struct ClassifyArgs {
   const void* lut;          // u8 or u16 entries
   uint32_t m;               // table size
   uint32_t lut_lds_bytes;   // bytes of LUT staged in LDS (0 = global gather)
+  uint32_t lut_tail;        // streaming kernel: entry 65536 of a 65537-slot u8 LUT (LDS holds 0..65535)
   uint64_t mu;              // floor(2^64 / m) for Barrett
   uint32_t nb;              // backends; bins = nb + 1 (sentinel bin = nb)
   uint32_t swap;
@@ -105,6 +106,10 @@ enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
 
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
+// Streaming classify (lean fixed slots, u8 LUT of <= 65537 entries staged in LDS): one block per
+// CU; a.tiles_per_wave = the contiguous 64-packet tiles of each of the grid's waves.
+int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream);
+int stream_waves_per_block();
 int launch_scan(const ScanArgs& a, void* stream);
 int launch_hist(const HistArgs& a, void* stream);
 bool hist_in_classify(uint32_t nbins);

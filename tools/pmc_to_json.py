@@ -19,7 +19,8 @@ def per_kernel(d, counter):
         if row["Counter_Name"] != counter:
             continue
         name = row["Kernel_Name"]
-        key = "classify" if "classify_kernel" in name else ("group" if "group_kernel" in name else None)
+        key = ("classify" if ("classify_kernel" in name or "classify_stream_kernel" in name)
+               else ("group" if "group_kernel" in name else None))
         if key:
             acc[key].append(float(row["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
