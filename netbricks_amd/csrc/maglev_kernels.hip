@@ -854,6 +854,202 @@ __global__ __launch_bounds__(kScanWaves * 64) void scan_kernel(ScanArgs a) {
   }
 }
 
+// ---- small batches: classify + stable grouping in one launch -------------------------------------
+// A batch of at most kSmallMax packets (one grouping partition) and at most kMaxGroupBins bins is
+// classified and grouped by one 1024-thread block: NetBricks' own bursts are 32 packets
+// (receive_batch.rs:26), where two launches and their gaps were the whole cost of a call.  Wave w
+// owns packets [256w, 256w + 256) in four 64-packet rounds.  Per packet: the chunks 0..2 of its
+// 64-B window are loaded as three 16-B vectors when the frame allows (aligned, >= 48 B), and it
+// takes the fast path (IHL 5) or the byte-wise path.  Then each round ranks its lanes among the
+// same bin (readlane match) into per-wave counters, one block scan over (bin, wave) in bin-major
+// order gives every wave's start per bin, and perm is scattered: per-group FIFO order as the
+// reference's producer (group_by.rs:46-51).
+constexpr uint32_t kSmallNT = 1024, kSmallW = kSmallNT / 64;
+constexpr uint32_t kSmallMax = 4 * kSmallNT;
+
+template <int LUTM, bool F4>
+__device__ __forceinline__ uint32_t small_classify(const ClassifyArgs& a, uint32_t p, uint32_t off, uint32_t len,
+                                                   const uint4* c) {
+  uint8_t* pk = a.pkts + off;
+  const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && len >= 48u;
+  if (vec && ((c[0].w >> 16) & 0xfu) == 5u) {
+    const uint32_t src = (c[1].z >> 16) | (c[1].w << 16);
+    const uint32_t dst = (c[1].w >> 16) | (c[2].x << 16);
+    const uint32_t ports = (c[2].x >> 16) | (c[2].y << 16);
+    uint32_t lo, hi;
+    fnv_flow(lo, hi, src, dst, ports, c[1].y >> 24);
+    const uint32_t bin = lookup<LUTM, F4>(a, nullptr, lo, hi);
+    if (a.swap) {
+      const uint32_t w0 = (c[0].y >> 16) | (c[0].z << 16), w1 = (c[0].z >> 16) | (c[0].x << 16),
+                     w2 = (c[0].x >> 16) | (c[0].y << 16);
+      if (a.mac_out) {
+        uint32_t* mo = reinterpret_cast<uint32_t*>(a.mac_out + static_cast<size_t>(p) * 12u);
+        mo[0] = w0;
+        mo[1] = w1;
+        mo[2] = w2;
+      } else {
+        *reinterpret_cast<uint4*>(pk) = make_uint4(w0, w1, w2, c[0].w);
+      }
+    }
+    return bin;
+  }
+  uint32_t gate;
+  return classify_slow<LUTM, F4, false>(a, nullptr, pk, len, p, gate);
+}
+
+template <int LUTM, bool F4>
+__global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupArgs g) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  const uint32_t nbins = a.nb + 1, nbp = (nbins + 3) & ~3u;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t* cnt = sm;                                            // [kSmallW][nbp]: per-wave counts
+  uint16_t* rank16 = reinterpret_cast<uint16_t*>(cnt + kSmallW * nbp);  // [kSmallMax]
+  uint16_t* bin16 = rank16 + kSmallMax;                          // [kSmallMax]
+  __shared__ uint32_t s_wave[kSmallW];
+  const bool group = g.perm || g.counts;
+  if (group)
+    for (uint32_t i = tid; i < kSmallW * nbp; i += kSmallNT) cnt[i] = 0;
+  // loads of the wave's four packets first (unconditional, clamped), then the classification
+  uint32_t off[4], len[4];
+  uint4 c[4][3];
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint32_t p = min(wave * 256u + r * 64u + lane, a.n_pkts - 1u);
+    off[r] = a.off ? a.off[p] : p * a.stride;
+    len[r] = a.len ? a.len[p] : a.fixed_len;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint8_t* pk = a.pkts + off[r];
+    const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && len[r] >= 48u;
+    const uint8_t* src = vec ? pk : a.pkts;  // the batch base is 16-B aligned by the host check
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) c[r][k] = *reinterpret_cast<const uint4*>(src + 16u * k);
+  }
+  if (group) lds_sync();
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint32_t p = wave * 256u + r * 64u + lane;
+    const bool valid = p < a.n_pkts;
+    uint32_t bin = 0xffffffffu;
+    if (valid) {
+      bin = small_classify<LUTM, F4>(a, p, off[r], len[r], c[r]);
+      a.backend[p] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+    }
+    if (group) {
+      uint32_t rank = 0;
+      bool last = true;
+      for (uint32_t j = 0; j < 64u; ++j) {
+        const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bin), j));
+        const bool eq = bj == bin;
+        rank += (eq && j < lane) ? 1u : 0u;
+        last = last && !(eq && j > lane);
+      }
+      uint32_t* wc = cnt + wave * nbp;
+      const uint32_t before = wc[valid ? bin : 0u];
+      __builtin_amdgcn_wave_barrier();
+      if (valid) {
+        rank16[p] = static_cast<uint16_t>(before + rank);
+        bin16[p] = static_cast<uint16_t>(bin);
+        if (last) wc[bin] = before + rank + 1u;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (!group) return;
+  lds_sync();
+  // exclusive scan over the counters in (bin, wave) order; each thread owns `per` consecutive entries
+  const uint32_t ne = nbins * kSmallW, per = (ne + kSmallNT - 1) / kSmallNT;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t e = tid * per + k;
+    sum += e < ne ? cnt[(e % kSmallW) * nbp + e / kSmallW] : 0u;
+  }
+  uint32_t total;
+  uint32_t x = block_excl_scan_n<kSmallNT>(sum, s_wave, total);
+  // counts: a bin's packets = the sum of its kSmallW wave counters (read before they are replaced)
+  if (g.counts)
+    for (uint32_t b = tid; b < nbins; b += kSmallNT) {
+      uint32_t t = 0;
+      for (uint32_t w = 0; w < kSmallW; ++w) t += cnt[w * nbp + b];
+      g.counts[b] = t;
+    }
+  lds_sync();
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t e = tid * per + k;
+    if (e < ne) {
+      const uint32_t v = cnt[(e % kSmallW) * nbp + e / kSmallW];
+      cnt[(e % kSmallW) * nbp + e / kSmallW] = x;
+      x += v;
+    }
+  }
+  lds_sync();
+  if (g.perm)
+    for (uint32_t p = tid; p < a.n_pkts; p += kSmallNT) g.perm[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
+}
+
+// ---- many backends (more than kMaxGroupBins - 1, up to 32767) ------------------------------------
+// The multisplit group kernel keeps a counter row per wave and bin in LDS, which does not scale to
+// 32768 bins.  Past 1023 backends the per-partition histograms (hist_kernel) and their prefix over
+// partitions (scan_kernel) feed two small kernels: bin_base_kernel scans the bin totals into group
+// bases (and writes counts), and group_wide_kernel walks each partition in packet order, one wave
+// per partition, with one LDS counter per bin: a lane's position is its bin's base + the bin's
+// prefix over earlier partitions + the bin's count so far in this partition + its rank among the
+// lanes of its 64-packet step with the same bin (a readlane match over the step), so perm keeps the
+// per-group FIFO order of group_by.rs:46-51 for any bin count.
+__global__ __launch_bounds__(kGBlock) void bin_base_kernel(GroupArgs a) {
+  __shared__ uint32_t s_wave[kGBlock / 64];
+  const uint32_t nbins = a.nb + 1, tid = threadIdx.x;
+  const uint32_t per = (nbins + kGBlock - 1) / kGBlock;  // consecutive bins per thread
+  uint32_t s = 0;
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t b = tid * per + k;
+    s += b < nbins ? a.totals[b] : 0u;
+  }
+  uint32_t all;
+  uint32_t base = block_excl_scan_n<kGBlock>(s, s_wave, all);
+  for (uint32_t k = 0; k < per; ++k) {
+    const uint32_t b = tid * per + k;
+    if (b < nbins) {
+      const uint32_t t = a.totals[b];
+      a.bin_base[b] = base;
+      if (a.counts) a.counts[b] = t;
+      base += t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
+  extern __shared__ __align__(16) uint32_t cnt[];  // [nbins]: packets of each bin seen so far
+  const uint32_t nbins = a.nb + 1, lane = threadIdx.x, c = blockIdx.x;
+  for (uint32_t b = lane; b < nbins; b += 64) cnt[b] = 0;
+  const uint32_t pbeg = c * a.part_pkts, pend = min(pbeg + a.part_pkts, a.n_pkts);
+  const uint32_t* prefix = a.part_prefix + static_cast<size_t>(c) * nbins;
+  for (uint32_t i0 = pbeg; i0 < pend; i0 += 64u) {
+    const uint32_t i = i0 + lane;
+    const bool valid = i < pend;
+    const uint32_t raw = ld_u16(a.backend, min(i, a.n_pkts - 1u) * 2u);
+    const uint32_t bin = !valid ? 0xffffffffu : (raw == NBG_SENTINEL ? a.nb : raw);
+    // rank among earlier lanes of this step with the same bin; the last such lane advances the count
+    uint32_t rank = 0;
+    bool last = true;
+    for (uint32_t j = 0; j < 64u; ++j) {
+      const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bin), j));
+      const bool eq = bj == bin;
+      rank += (eq && j < lane) ? 1u : 0u;
+      last = last && !(eq && j > lane);
+    }
+    // every lane reads its bin's count before any lane of the step writes one (one wave: its LDS
+    // operations execute in issue order; the wave barriers keep the compiler from moving them)
+    const uint32_t slot = valid ? bin : 0u;
+    const uint32_t before = cnt[slot];
+    __builtin_amdgcn_wave_barrier();
+    if (valid && a.perm) a.perm[a.bin_base[bin] + prefix[bin] + before + rank] = i;
+    if (valid && last) cnt[bin] = before + rank + 1u;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // One 1024-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
 // Prologue: prefix of this partition over earlier partitions and the group bases, either
 // reduced here from the partition histograms staged in LDS, or read from scan_kernel's
@@ -1154,7 +1350,12 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     GPROBE(7)
     // coalesced output: consecutive sorted slots of one bin are consecutive perm entries.  The
     // next chunk's first writes to sidx/sbin/tot come after the barriers of its scan.
-    for (uint32_t j = tid; j < ctotal; j += kGBlock) a.perm[tot[sbin[j]] + j] = sidx[j];
+    for (uint32_t j = tid; j < ctotal; j += kGBlock) {
+#ifdef NBG_GUARD  // diagnostic build: a store whose slot comes from inconsistent histograms is dropped
+      if (tot[sbin[j]] + j >= a.n_pkts) continue;
+#endif
+      a.perm[tot[sbin[j]] + j] = sidx[j];
+    }
   }
   zero_next();
   GPROBE(8)
@@ -1284,6 +1485,15 @@ int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uin
 
 int launch_hist(const HistArgs& a, void* stream) {
   const size_t lds = static_cast<size_t>(a.nb + 1) * 4;
+  if (lds > 64 * 1024) {  // many backends: up to 32768 bins (128 KiB)
+    static bool attr = false;
+    if (!attr) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(hist_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024) != hipSuccess)
+        return set_error(NBG_EIO, "hist: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+      attr = true;
+    }
+  }
   hipLaunchKernelGGL(hist_kernel, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "hist launch: %s", hipGetErrorString(e));
@@ -1295,6 +1505,43 @@ int launch_scan(const ScanArgs& a, void* stream) {
                      static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "scan launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+size_t small_lds(uint32_t nb) { return (kSmallW * (((nb + 1) + 3) & ~3u)) * 4u + kSmallMax * 4u; }
+
+int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream) {
+  auto fn = wide_lut ? (a.m == 65537u ? small_kernel<kGlobalU16, true> : small_kernel<kGlobalU16, false>)
+                     : (a.m == 65537u ? small_kernel<kGlobalU8, true> : small_kernel<kGlobalU8, false>);
+  const size_t lds = small_lds(a.nb);
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess)
+    return set_error(NBG_EIO, "small: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+  hipLaunchKernelGGL(fn, dim3(1), dim3(kSmallNT), lds, static_cast<hipStream_t>(stream), a, g);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "small launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+uint32_t small_max() { return kSmallMax; }
+
+int launch_group_wide(const GroupArgs& a, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(bin_base_kernel, dim3(1), dim3(kGBlock), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "bin_base launch: %s", hipGetErrorString(e));
+  const size_t lds = static_cast<size_t>(a.nb + 1) * 4;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(group_wide_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return set_error(NBG_EIO, "group_wide: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+    attr = true;
+  }
+  hipLaunchKernelGGL(group_wide_kernel, dim3(a.n_parts), dim3(64), lds, s, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "group_wide launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 

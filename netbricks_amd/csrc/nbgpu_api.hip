@@ -63,14 +63,17 @@ struct nbg_maglev {
   int cus = 0;                // compute units (streaming classify: one block per CU)
   // grouping scratch (independent of the batch size: at most kMaxParts partitions)
   uint32_t* d_part_hist = nullptr;    // [2][kMaxParts][nb+1] ping-pong partition histograms
+  uint32_t* d_part_graph = nullptr;   // [kMaxParts][nb+1] histograms of calls captured in a hipGraph
   uint32_t* d_part_prefix = nullptr;  // [kMaxParts][nb+1] (scan-kernel fallback)
   uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
+  uint32_t* d_bin_base = nullptr;     // [nb+1]            (wide grouping path)
   uint32_t parity = 0;
   uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
   bool pending = false;
   int pending_scan_mode = 0;
   bool pending_hist = false;
+  bool pending_wide = false;
   HistArgs pending_hist_args{};
   GroupArgs pending_args{};
   ScanArgs pending_scan{};
@@ -165,12 +168,16 @@ void free_scratch(nbg_maglev* h) {
   h->d_fixed_len = nullptr;
   h->fixed_len_cap = 0;
   (void)hipFree(h->d_part_hist);
+  (void)hipFree(h->d_part_graph);
   (void)hipFree(h->d_part_prefix);
   (void)hipFree(h->d_totals);
+  (void)hipFree(h->d_bin_base);
   (void)hipFree(h->d_counts);
   h->d_part_hist = nullptr;
+  h->d_part_graph = nullptr;
   h->d_part_prefix = nullptr;
   h->d_totals = nullptr;
+  h->d_bin_base = nullptr;
   h->d_counts = nullptr;
 }
 
@@ -220,8 +227,10 @@ int upload(nbg_maglev* h) {
   NBG_HIP(hipMalloc(&h->d_lut, h->lut_alloc));
   const size_t nbins = h->nb + 1;
   NBG_HIP(hipMalloc(&h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_part_graph, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_bin_base, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
   SetupStream st;  // complete before the handle is returned: any caller stream may use it next
   (void)st.h2d(h->d_lut, buf.data(), h->lut_alloc);
@@ -247,12 +256,25 @@ bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
 
 // The streaming classify kernel serves fixed 64-B-aligned slots with a u8 LUT of at most 65537
 // entries (config C2); NBG_STREAM=0 selects the tile-per-wave kernel instead (A/B measurements).
-bool use_stream(const nbg_maglev* h) {
+// Below ~2 units per block the per-block LUT staging (64 KiB from L2 for every CU) is not
+// amortised: smaller batches take the tile-per-wave kernel.
+bool use_stream(const nbg_maglev* h, uint64_t n_pkts) {
   static const bool on = [] {
     const char* e = std::getenv("NBG_STREAM");
     return !e || std::atoi(e) != 0;
   }();
-  return on && !h->wide && h->m <= 65537;
+  return on && !h->wide && h->m <= 65537 && n_pkts >= 262144;
+}
+
+// Batches of at most one partition take the single-launch small kernel; NBG_SMALL=0 disables it
+// (A/B measurements).
+bool use_small(uint64_t n_pkts, uint32_t nbins, uint32_t flags, const uint8_t* d_pkts) {
+  static const bool on = [] {
+    const char* e = std::getenv("NBG_SMALL");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on && n_pkts <= small_max() && nbins <= kMaxGroupBins && !(flags & (NBG_DEFER_GROUP | NBG_LUT_LDS)) &&
+         (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0;
 }
 
 // Persistent host worker pool for the host path's gather and MAC write-back (bound by host
@@ -446,9 +468,19 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   DeviceGuard g(h->device);
   const bool group = d_perm || d_counts;
   const uint32_t nbins = h->nb + 1;
-  if (group && nbins > kMaxGroupBins)
-    return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxGroupBins - 1);
-  int rc = order_after_last(h, static_cast<hipStream_t>(stream));
+  if (group && nbins > kMaxWideBins)
+    return set_error(NBG_EINVAL, "classify: group output supports at most %u backends", kMaxWideBins - 1);
+  const bool wide = group && nbins > kMaxGroupBins;  // wide grouping path (hist + scan + group_wide)
+  // A call captured into a hipGraph is replayed with the same arguments, so it must not rely on the
+  // ping-pong histograms (a replay would find them unzeroed): it zeroes and uses its own buffer,
+  // and leaves the handle's parity alone.  Cross-stream ordering cannot be recorded during capture:
+  // the caller orders the capture after the handle's earlier work.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  NBG_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap));
+  const bool capturing = cap != hipStreamCaptureStatusNone;
+  if (capturing && (flags & NBG_DEFER_GROUP))
+    return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP cannot be captured in a graph");
+  int rc = capturing ? NBG_OK : order_after_last(h, static_cast<hipStream_t>(stream));
   if (rc) return rc;
   const bool lds = use_lds_lut(h, flags);
   // each wave walks tpw consecutive 64-packet tiles (software-pipelined); the LDS-LUT variant
@@ -467,10 +499,12 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const uint64_t per = (n_pkts + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
   const uint32_t part_pkts = static_cast<uint32_t>(per * kChunk);
   const uint32_t n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
-  uint32_t* part_cur = h->d_part_hist + static_cast<size_t>(h->parity) * kMaxParts * nbins;
-  uint32_t* part_next = h->d_part_hist + static_cast<size_t>(h->parity ^ 1u) * kMaxParts * nbins;
+  uint32_t* part_cur = capturing ? h->d_part_graph : h->d_part_hist + static_cast<size_t>(h->parity) * kMaxParts * nbins;
+  uint32_t* part_next = capturing ? nullptr : h->d_part_hist + static_cast<size_t>(h->parity ^ 1u) * kMaxParts * nbins;
 
   if (d_off && !d_len) {
+    if (capturing && h->fixed_len_cap < n_pkts)
+      return set_error(NBG_EINVAL, "classify: make one call of this size before capturing it (no allocation in a graph)");
     if (h->fixed_len_cap < n_pkts) {
       (void)hipFree(h->d_fixed_len);
       h->d_fixed_len = nullptr;
@@ -512,7 +546,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const bool hist_k = group && !hist_in_classify(nbins);  // histograms by hist_kernel instead
   a.part_hist = group && !hist_k ? part_cur : nullptr;
   a.part_pkts = part_pkts;
-  const int scan = group ? pick_group_scan(nbins, n_parts) : kScanKernel;
+  const int scan = group && !wide ? pick_group_scan(nbins, n_parts) : kScanKernel;
   // packed 16-bit partition rows where the classify kernel writes them and the group kernel sums
   // them itself (partition counts stay below 65536)
   a.hist16 = group && !hist_k && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
@@ -523,15 +557,27 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     a.gate = d_gate;
     a.mac_out = nullptr;
   }
-  h->last_stream = static_cast<hipStream_t>(stream);
-  h->issued = true;
-  if (a.lean && !lds && !lpm && use_stream(h)) {
+  if (!capturing) {
+    h->last_stream = static_cast<hipStream_t>(stream);
+    h->issued = true;
+  }
+  if (!lpm && use_small(n_pkts, nbins, flags, d_pkts)) {
+    GroupArgs g{};
+    g.perm = d_perm;
+    g.counts = d_counts ? d_counts : (d_perm ? h->d_counts : nullptr);
+    return launch_small(a, g, h->wide, stream);
+  }
+  if (a.lean && !lds && !lpm && use_stream(h, n_pkts)) {
     const uint64_t waves = static_cast<uint64_t>(h->cus) * stream_waves_per_block();
     a.tiles_per_wave = static_cast<uint32_t>((n_tiles64 + waves - 1) / waves);
     a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
     a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+    if (capturing && a.part_hist)
+      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
     rc = launch_classify_stream(a, h->cus, stream);
   } else {
+    if (capturing && a.part_hist)
+      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
     rc = launch_classify(a, h->wide, lds, grid, stream);
   }
   if (rc) return rc;
@@ -563,10 +609,11 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     ga.totals = h->d_totals;
     ga.hist16 = a.hist16;
     ga.part_hist_next = part_next;
-    ga.next_words = kMaxParts * nbins;
+    ga.next_words = part_next ? kMaxParts * nbins : 0u;
     ga.counts = d_counts ? d_counts : h->d_counts;
     ga.perm = d_perm;
-    h->parity ^= 1u;
+    ga.bin_base = h->d_bin_base;
+    if (!capturing) h->parity ^= 1u;
     if (flags & NBG_DEFER_GROUP) {
       h->pending = true;
       h->pending_scan_mode = scan;
@@ -574,10 +621,11 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
       h->pending_hist_args = ha;
       h->pending_args = ga;
       h->pending_scan = sa;
+      h->pending_wide = wide;
     } else {
       if (hist_k && (rc = launch_hist(ha, stream))) return rc;
       if (scan == kScanKernel && (rc = launch_scan(sa, stream))) return rc;
-      if ((rc = launch_group(ga, scan, stream))) return rc;
+      if ((rc = wide ? launch_group_wide(ga, stream) : launch_group(ga, scan, stream))) return rc;
     }
   }
   return NBG_OK;
@@ -664,7 +712,9 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   h->last_stream = static_cast<hipStream_t>(stream);
   if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;
   if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
-  if ((rc = launch_group(h->pending_args, h->pending_scan_mode, stream))) return rc;
+  if ((rc = h->pending_wide ? launch_group_wide(h->pending_args, stream)
+                            : launch_group(h->pending_args, h->pending_scan_mode, stream)))
+    return rc;
   return NBG_OK;
 }
 

@@ -34,7 +34,9 @@ constexpr int kGBlock = NBG_GBLOCK;  // group kernel threads per workgroup (8 wa
 constexpr int kChunk = 4096;         // packets per group-kernel chunk
 constexpr int kGRounds = kChunk / kGBlock;  // group kernel rounds of 64 packets per wave per chunk
 constexpr uint32_t kMaxParts = 256;  // partitions per batch (part_pkts is a multiple of kChunk)
-constexpr uint32_t kMaxGroupBins = 1024;  // group output supports n_backends + 1 <= 1024
+constexpr uint32_t kMaxGroupBins = 1024;  // multisplit group kernel: n_backends + 1 <= 1024
+constexpr uint32_t kMaxWideBins = 32768;  // wide grouping path: n_backends <= 32767 (LUT sentinel bound,
+                                          // test/maglev/src/nf.rs:46)
 
 struct ClassifyArgs {
   uint8_t* pkts;
@@ -98,6 +100,7 @@ struct GroupArgs {
   uint32_t next_words;
   uint32_t* counts;           // nullable
   uint32_t* perm;             // nullable (counts only)
+  uint32_t* bin_base;         // [nb+1] wide path: first perm slot of every group
 };
 
 // How the group kernel gets each partition's per-bin prefix: from scan_kernel's output, by
@@ -116,6 +119,11 @@ bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
                       uint16_t* gate, void* stream);
 int launch_group(const GroupArgs& a, int scan, void* stream);
+int launch_group_wide(const GroupArgs& a, void* stream);  // nb + 1 > kMaxGroupBins
+// One launch for a batch of at most small_max() packets and at most kMaxGroupBins bins: classify
+// and (when g.perm / g.counts) group.  The batch base must be 16-B aligned.
+int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream);
+uint32_t small_max();
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan);
 int pick_group_scan(uint32_t nbins, uint32_t n_parts);
 int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid);

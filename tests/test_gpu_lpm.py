@@ -127,6 +127,32 @@ def test_chain_vs_oracle_at_size(torch_cuda, tables, mode, n, lut_lds):
     assert (eg == 3).any() and (eb == 0xFFFF).any()  # gate >= lpm_groups rejections exercised
 
 
+def test_chain_c5_bench_workload_1m_imix(torch_cuda, tables):
+    """Config C5 exactly as tools/config_bench.py measures it: a 1M-packet IMIX descriptor batch
+    (seed 1000), owned windows, the reference's 105 routes + the mixed route set, 65 backends /
+    65537 slots; every output bit-exact against the oracle."""
+    import netbricks_amd as nb
+    from netbricks_amd.lpm import Lpm
+
+    torch = torch_cuda
+    _, mg = tables
+    n = 1 << 20
+    routes = ROUTES["reference"] + ROUTES["mixed"]
+    lpm = Lpm(routes)
+    buf, off, ln = nb.make_trace(n, 1, seed=1000)
+    got = _chain(torch, mg, lpm, buf, n, offsets=off, lens=ln, owned_windows=True)
+    rc, t24, tl = orc.lpm_build(routes)
+    assert rc == 0
+    eg, eb = orc.chain_classify(buf, n, t24, tl, orc.lut_build(NAMES65, 65537), offs=off, lens=ln)
+    perm, counts = orc.group(eb, 65)
+    np.testing.assert_array_equal(got[1], eg)
+    np.testing.assert_array_equal(got[2], eb)
+    np.testing.assert_array_equal(got[4], counts)
+    np.testing.assert_array_equal(got[3], perm)
+    np.testing.assert_array_equal(got[0], buf)
+    lpm.close()
+
+
 def test_chain_reference_routes_and_groups(torch_cuda, tables):
     """test/lpm's own table on the synthetic trace (10/8 sources: every gate 0), and a
     smaller lpm_groups that turns gate 1 into a rejection."""

@@ -319,12 +319,33 @@ def test_mac_out_record(torch_cuda, mg65):
             assert not m[i].any()
 
 
-def test_many_backends_group_limit(torch_cuda):
-    """Group output is limited to 1023 backends; backend-only classify has no limit."""
+@pytest.mark.parametrize("nb,m,n,mode", [(1500, 65537, 3000, 0), (4096, 655373, 1 << 20, 0),
+                                        (4096, 655373, 300000, 1), (32767, 655373, 200000, 0)])
+def test_many_backends_wide_grouping(torch_cuda, nb, m, n, mode):
+    """More than 1023 backends (up to 32767, the LUT sentinel bound of nf.rs:46): the wide grouping
+    path (hist_kernel + scan_kernel + bin_base_kernel + group_wide_kernel) gives the oracle's
+    per-group FIFO order; fixed slots and IMIX descriptors, deferred grouping too."""
+    from netbricks_amd import Maglev, make_trace
+
+    names = [f"b{i}" for i in range(nb)]
+    mg = Maglev(names, m)
+    lut = orc.lut_build(names, m)
+    np.testing.assert_array_equal(mg.lut(), lut.astype(np.uint16))
+    buf, off, ln = make_trace(n, mode, seed=nb + n)
+    kw = dict(stride=64, fixed_len=60) if mode == 0 else dict(offs=off, lens=ln)
+    exp = _oracle(buf, n, lut, nb, **kw)
+    rkw = dict(stride=64, frame_len=60) if mode == 0 else dict(offs=off, lens=ln)
+    _assert_same(_run(torch_cuda, mg, buf, n, **rkw), exp)
+    mg.close()
+
+
+def test_group_limit_32767(torch_cuda):
+    """Grouping past 32767 backends is refused (the reference's 0x8000 fill sentinel collides just
+    above, nf.rs:46); backend-only classify has no such limit."""
     from netbricks_amd import Maglev, NbgError, make_trace
 
-    names = [f"b{i}" for i in range(1500)]
-    mg = Maglev(names, 65537)
+    names = [f"b{i}" for i in range(32768)]
+    mg = Maglev(names, 655373)
     n = 3000
     buf, _, _ = make_trace(n, 0, seed=8)
     d = torch_cuda.from_numpy(buf.copy()).to("cuda:0")
@@ -332,7 +353,7 @@ def test_many_backends_group_limit(torch_cuda):
         mg.group_by(d, n)
     r = mg.group_by(d, n, group=False, swap_macs=False)
     torch_cuda.cuda.synchronize()
-    exp = orc.classify(buf.copy(), n, orc.lut_build(names, 65537), stride=64, fixed_len=60, swap=False)
+    exp = orc.classify(buf.copy(), n, orc.lut_build(names, 655373), stride=64, fixed_len=60, swap=False)
     np.testing.assert_array_equal(r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16), exp)
     mg.close()
 
