@@ -32,7 +32,9 @@ constexpr uint32_t kSentinel = NBG_SENTINEL;
 constexpr uint32_t kEth = 14;
 
 // LUT placement / width variants.
-enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3, kLdsU8Tail = 4 };
+enum LutMode { kLdsU8 = 0, kLdsU16 = 1, kGlobalU8 = 2, kGlobalU16 = 3, kLdsU8Tail = 4, kIdx = 5 };
+// kIdx (NBG_LUT_TILED): no lookup; the classify kernel emits the LUT index (bit 31 set, so it
+// cannot be mistaken for the would-panic bin) and the tiled lookup resolves it later.
 
 // Packet layouts: fixed slots (general), fixed slots known by the host to be 16-B aligned with
 // owned windows, no length array and frames >= 48 B (every chunk readable, no per-lane
@@ -93,6 +95,7 @@ __device__ __forceinline__ uint32_t lut_get(const ClassifyArgs& a, const uint8_t
   if constexpr (LUTM == kLdsU16) return reinterpret_cast<const uint16_t*>(lut_lds)[idx];
   if constexpr (LUTM == kGlobalU8) return static_cast<const uint8_t*>(a.lut)[idx];
   if constexpr (LUTM == kLdsU8Tail) return idx < 65536u ? lut_lds[idx] : a.lut_tail;  // streaming kernel
+  if constexpr (LUTM == kIdx) return idx | 0x80000000u;
   return static_cast<const uint16_t*>(a.lut)[idx];
 }
 
@@ -350,8 +353,12 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
       a.gate[p_own] = static_cast<uint16_t>(gate);
       if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
     }
-    a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-    if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+    if constexpr (LUTM == kIdx) {
+      a.idx_out[p_own] = (bin & 0x80000000u) ? (bin & 0x7fffffffu) : 0xffffffffu;
+    } else {
+      a.backend[p_own] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+      if constexpr (HIST) atomicAdd(&hist[bin], 1u);
+    }
   }
 }
 
@@ -854,6 +861,92 @@ __global__ __launch_bounds__(kScanWaves * 64) void scan_kernel(ScanArgs a) {
   }
 }
 
+// ---- LDS-tiled lookup (NBG_LUT_TILED; config C3's named variant) --------------------------------
+// A u16 LUT larger than LDS (C3: 655373 entries = 1.25 MiB) is split into 64-KiB tiles of 32768
+// entries.  After the classify kernel has written each packet's LUT index (kIdx):
+//   tile_bucket_kernel  appends (packet, index in tile) to its tile's bucket: counts per tile in
+//                       LDS, one global reservation per tile per block, then the scatter;
+//   tile_lookup_kernel  one block per (tile, chunk of its bucket) stages the tile in LDS and
+//                       resolves its chunk: backend[packet] = tile[index].
+// Would-panic packets (index 0xffffffff) get the sentinel in the bucket kernel.  The measured
+// alternative to the L2 gather that BASELINE config C3 names.
+constexpr uint32_t kTileEntries = 32768;  // u16 entries per 64-KiB LUT tile
+constexpr uint32_t kBucketNT = 256, kBucketPkts = 4096, kLookupNT = 512, kLookupChunk = 8192;
+
+__global__ __launch_bounds__(kBucketNT) void tile_bucket_kernel(TileArgs a) {
+  extern __shared__ __align__(16) uint32_t tcnt[];  // [n_tiles] counts, then reserved bases
+  const uint32_t tid = threadIdx.x, p0 = blockIdx.x * kBucketPkts;
+  for (uint32_t t = tid; t < a.n_tiles; t += kBucketNT) tcnt[t] = 0;
+  __syncthreads();
+  constexpr uint32_t kPer = kBucketPkts / kBucketNT;
+  uint32_t idx[kPer], slot[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t p = p0 + k * kBucketNT + tid;
+    idx[k] = a.idx[min(p, a.n_pkts - 1u)];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t p = p0 + k * kBucketNT + tid;
+    slot[k] = 0;
+    if (p < a.n_pkts) {
+      if (idx[k] == 0xffffffffu) a.backend[p] = static_cast<uint16_t>(kSentinel);
+      else slot[k] = atomicAdd(&tcnt[idx[k] / kTileEntries], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t t = tid; t < a.n_tiles; t += kBucketNT)
+    tcnt[t] = tcnt[t] ? atomicAdd(&a.cursor[t], tcnt[t]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t p = p0 + k * kBucketNT + tid;
+    if (p < a.n_pkts && idx[k] != 0xffffffffu) {
+      const uint32_t t = idx[k] / kTileEntries;
+      a.bucket[static_cast<size_t>(t) * a.bucket_cap + tcnt[t] + slot[k]] =
+          (static_cast<uint64_t>(p) << 32) | (idx[k] - t * kTileEntries);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kLookupNT) void tile_lookup_kernel(TileArgs a) {
+  extern __shared__ __align__(16) uint16_t tlut[];  // one LUT tile
+  const uint32_t t = blockIdx.y, tid = threadIdx.x;
+  const uint32_t cnt = a.cursor[t];
+  const uint32_t c0 = blockIdx.x * kLookupChunk;
+  if (c0 >= cnt) return;  // block-uniform
+  const uint32_t entries = min(kTileEntries, a.m - t * kTileEntries);
+  const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.lut) + t * kTileEntries);
+  for (uint32_t v = tid; v < (entries + 7) / 8; v += kLookupNT) reinterpret_cast<uint4*>(tlut)[v] = src[v];
+  __syncthreads();
+  const uint64_t* b = a.bucket + static_cast<size_t>(t) * a.bucket_cap;
+  const uint32_t c1 = min(c0 + kLookupChunk, cnt);
+  for (uint32_t i = c0 + tid; i < c1; i += kLookupNT) {
+    const uint64_t e = b[i];
+    a.backend[static_cast<uint32_t>(e >> 32)] = tlut[static_cast<uint32_t>(e)];
+  }
+}
+
+// Stable rank of this lane among the lanes of its wave with the same `bin` (valid lanes only), and
+// how many lanes hold that bin: one ballot per bin bit plus one for validity, no loop over lanes.
+template <int BITS>
+__device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32_t lane, uint32_t& rank,
+                                                uint32_t& count) {
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t mv = valid ? ~0u : 0u;
+  const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
+  uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
+#pragma unroll
+  for (int bit = 0; bit < BITS; ++bit) {
+    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
+    const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
+    elo &= ~(static_cast<uint32_t>(bb) ^ m);
+    ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
+  }
+  rank = __popc(elo & static_cast<uint32_t>(lt)) + __popc(ehi & static_cast<uint32_t>(lt >> 32));
+  count = __popc(elo) + __popc(ehi);
+}
+
 // ---- small batches: classify + stable grouping in one launch -------------------------------------
 // A batch of at most kSmallMax packets (one grouping partition) and at most kMaxGroupBins bins is
 // classified and grouped by one 1024-thread block: NetBricks' own bursts are 32 packets
@@ -897,20 +990,24 @@ __device__ __forceinline__ uint32_t small_classify(const ClassifyArgs& a, uint32
   return classify_slow<LUTM, F4, false>(a, nullptr, pk, len, p, gate);
 }
 
-template <int LUTM, bool F4>
+template <int LUTM, bool F4, int BITS>
 __global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupArgs g) {
   extern __shared__ __align__(16) uint32_t sm[];
   const uint32_t nbins = a.nb + 1, nbp = (nbins + 3) & ~3u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  uint32_t* cnt = sm;                                            // [kSmallW][nbp]: per-wave counts
+  const uint32_t nw = blockDim.x >> 6;  // waves launched: ceil(n / 256)
+  uint32_t* cnt = sm;                                            // [nw][nbp]: per-wave counts
   uint16_t* rank16 = reinterpret_cast<uint16_t*>(cnt + kSmallW * nbp);  // [kSmallMax]
   uint16_t* bin16 = rank16 + kSmallMax;                          // [kSmallMax]
   __shared__ uint32_t s_wave[kSmallW];
   const bool group = g.perm || g.counts;
   if (group)
-    for (uint32_t i = tid; i < kSmallW * nbp; i += kSmallNT) cnt[i] = 0;
-  // loads of the wave's four packets first (unconditional, clamped), then the classification
-  uint32_t off[4], len[4];
+    for (uint32_t i = tid; i < nw * nbp; i += blockDim.x) cnt[i] = 0;
+  // this wave's rounds that hold packets (wave-uniform)
+  const uint32_t rounds = min(4u, (a.n_pkts - min(a.n_pkts, wave * 256u) + 63u) / 64u);
+  // loads of every round first (unconditional, clamped), then every round's classification (its
+  // LUT gathers in flight together), then the ranking
+  uint32_t off[4], len[4], bin[4];
   uint4 c[4][3];
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
@@ -926,66 +1023,67 @@ __global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupAr
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) c[r][k] = *reinterpret_cast<const uint4*>(src + 16u * k);
   }
-  if (group) lds_sync();
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
     const uint32_t p = wave * 256u + r * 64u + lane;
-    const bool valid = p < a.n_pkts;
-    uint32_t bin = 0xffffffffu;
-    if (valid) {
-      bin = small_classify<LUTM, F4>(a, p, off[r], len[r], c[r]);
-      a.backend[p] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-    }
-    if (group) {
-      uint32_t rank = 0;
-      bool last = true;
-      for (uint32_t j = 0; j < 64u; ++j) {
-        const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bin), j));
-        const bool eq = bj == bin;
-        rank += (eq && j < lane) ? 1u : 0u;
-        last = last && !(eq && j > lane);
-      }
-      uint32_t* wc = cnt + wave * nbp;
-      const uint32_t before = wc[valid ? bin : 0u];
-      __builtin_amdgcn_wave_barrier();
-      if (valid) {
-        rank16[p] = static_cast<uint16_t>(before + rank);
-        bin16[p] = static_cast<uint16_t>(bin);
-        if (last) wc[bin] = before + rank + 1u;
-      }
-      __builtin_amdgcn_wave_barrier();
+    bin[r] = 0xffffffffu;
+    if (r < rounds && p < a.n_pkts) {
+      bin[r] = small_classify<LUTM, F4>(a, p, off[r], len[r], c[r]);
+      a.backend[p] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
     }
   }
   if (!group) return;
+  lds_sync();  // counters zeroed
+  uint32_t* wc = cnt + wave * nbp;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    const uint32_t p = wave * 256u + r * 64u + lane;
+    const bool valid = p < a.n_pkts;
+    const uint32_t b = valid ? bin[r] : 0u;
+    uint32_t rank, count;
+    wave_match_rank<BITS>(b, valid, lane, rank, count);
+    // every lane of a bin reads the same count and stores the same new one (one wave: its LDS
+    // operations execute in issue order)
+    const uint32_t before = wc[b];
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      rank16[p] = static_cast<uint16_t>(before + rank);
+      bin16[p] = static_cast<uint16_t>(b);
+      wc[b] = before + count;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   lds_sync();
-  // exclusive scan over the counters in (bin, wave) order; each thread owns `per` consecutive entries
-  const uint32_t ne = nbins * kSmallW, per = (ne + kSmallNT - 1) / kSmallNT;
+  // exclusive scan over the counters in (bin, wave) order; each thread owns `per` consecutive
+  // entries; the waves' partial sums are combined through s_wave
+  const uint32_t ne = nbins * nw, per = (ne + blockDim.x - 1) / blockDim.x;
   uint32_t sum = 0;
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t e = tid * per + k;
-    sum += e < ne ? cnt[(e % kSmallW) * nbp + e / kSmallW] : 0u;
+    sum += e < ne ? cnt[(e % nw) * nbp + e / nw] : 0u;
   }
-  uint32_t total;
-  uint32_t x = block_excl_scan_n<kSmallNT>(sum, s_wave, total);
-  // counts: a bin's packets = the sum of its kSmallW wave counters (read before they are replaced)
+  const uint32_t xs = wave_incl_scan(sum);
+  if (lane == 63u) s_wave[wave] = xs;
+  // counts: a bin's packets = the sum of its wave counters (read before they are replaced)
   if (g.counts)
-    for (uint32_t b = tid; b < nbins; b += kSmallNT) {
+    for (uint32_t b = tid; b < nbins; b += blockDim.x) {
       uint32_t t = 0;
-      for (uint32_t w = 0; w < kSmallW; ++w) t += cnt[w * nbp + b];
+      for (uint32_t w = 0; w < nw; ++w) t += cnt[w * nbp + b];
       g.counts[b] = t;
     }
   lds_sync();
+  uint32_t x = xs - sum;
+  for (uint32_t w = 0; w < wave; ++w) x += s_wave[w];
   for (uint32_t k = 0; k < per; ++k) {
     const uint32_t e = tid * per + k;
     if (e < ne) {
-      const uint32_t v = cnt[(e % kSmallW) * nbp + e / kSmallW];
-      cnt[(e % kSmallW) * nbp + e / kSmallW] = x;
+      const uint32_t v = cnt[(e % nw) * nbp + e / nw];
+      cnt[(e % nw) * nbp + e / nw] = x;
       x += v;
     }
   }
   lds_sync();
   if (g.perm)
-    for (uint32_t p = tid; p < a.n_pkts; p += kSmallNT) g.perm[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
+    for (uint32_t p = tid; p < a.n_pkts; p += blockDim.x) g.perm[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
 }
 
 // ---- many backends (more than kMaxGroupBins - 1, up to 32767) ------------------------------------
@@ -1030,22 +1128,16 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
     const bool valid = i < pend;
     const uint32_t raw = ld_u16(a.backend, min(i, a.n_pkts - 1u) * 2u);
     const uint32_t bin = !valid ? 0xffffffffu : (raw == NBG_SENTINEL ? a.nb : raw);
-    // rank among earlier lanes of this step with the same bin; the last such lane advances the count
-    uint32_t rank = 0;
-    bool last = true;
-    for (uint32_t j = 0; j < 64u; ++j) {
-      const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bin), j));
-      const bool eq = bj == bin;
-      rank += (eq && j < lane) ? 1u : 0u;
-      last = last && !(eq && j > lane);
-    }
+    // rank among earlier lanes of this step with the same bin, and the bin's lanes in the step
+    uint32_t rank, count;
+    wave_match_rank<15>(valid ? bin : 0u, valid, lane, rank, count);
     // every lane reads its bin's count before any lane of the step writes one (one wave: its LDS
     // operations execute in issue order; the wave barriers keep the compiler from moving them)
     const uint32_t slot = valid ? bin : 0u;
     const uint32_t before = cnt[slot];
     __builtin_amdgcn_wave_barrier();
     if (valid && a.perm) a.perm[a.bin_base[bin] + prefix[bin] + before + rank] = i;
-    if (valid && last) cnt[bin] = before + rank + 1u;
+    if (valid) cnt[bin] = before + count;  // every lane of a bin stores the same new count
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -1508,17 +1600,55 @@ int launch_scan(const ScanArgs& a, void* stream) {
   return NBG_OK;
 }
 
+int launch_classify_idx(const ClassifyArgs& a, int grid, void* stream) {
+  const size_t lds = classify_lds(a.nb, 0);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  auto fn = a.off ? classify_kernel<kIdx, false, false, false, kDesc>
+                  : (a.lean ? classify_kernel<kIdx, false, false, false, kLean>
+                            : classify_kernel<kIdx, false, false, false, kFixed>);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "classify (index) launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+int launch_tiled_lookup(const TileArgs& a, void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(tile_bucket_kernel, dim3((a.n_pkts + kBucketPkts - 1) / kBucketPkts), dim3(kBucketNT),
+                     a.n_tiles * 4, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "tile bucket launch: %s", hipGetErrorString(e));
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(tile_lookup_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kTileEntries * 2) != hipSuccess)
+      return set_error(NBG_EIO, "tile lookup: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+    attr = true;
+  }
+  hipLaunchKernelGGL(tile_lookup_kernel, dim3((a.n_pkts + kLookupChunk - 1) / kLookupChunk, a.n_tiles),
+                     dim3(kLookupNT), kTileEntries * 2, s, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "tile lookup launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+uint32_t lut_tiles(uint64_t m) { return static_cast<uint32_t>((m + kTileEntries - 1) / kTileEntries); }
+
 size_t small_lds(uint32_t nb) { return (kSmallW * (((nb + 1) + 3) & ~3u)) * 4u + kSmallMax * 4u; }
 
 int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream) {
-  auto fn = wide_lut ? (a.m == 65537u ? small_kernel<kGlobalU16, true> : small_kernel<kGlobalU16, false>)
-                     : (a.m == 65537u ? small_kernel<kGlobalU8, true> : small_kernel<kGlobalU8, false>);
+  const bool b7 = a.nb + 1 <= 128;
+  auto fn = wide_lut ? (a.m == 65537u ? (b7 ? small_kernel<kGlobalU16, true, 7> : small_kernel<kGlobalU16, true, 10>)
+                                      : (b7 ? small_kernel<kGlobalU16, false, 7> : small_kernel<kGlobalU16, false, 10>))
+                     : (a.m == 65537u ? (b7 ? small_kernel<kGlobalU8, true, 7> : small_kernel<kGlobalU8, true, 10>)
+                                      : (b7 ? small_kernel<kGlobalU8, false, 7> : small_kernel<kGlobalU8, false, 10>));
   const size_t lds = small_lds(a.nb);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                           static_cast<int>(lds)) != hipSuccess)
     return set_error(NBG_EIO, "small: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
-  hipLaunchKernelGGL(fn, dim3(1), dim3(kSmallNT), lds, static_cast<hipStream_t>(stream), a, g);
+  const uint32_t waves = (a.n_pkts + 255u) / 256u;  // 1..16: a wave per 256 packets
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64 * waves), lds, static_cast<hipStream_t>(stream), a, g);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "small launch: %s", hipGetErrorString(e));
   return NBG_OK;

@@ -82,6 +82,12 @@ struct nbg_maglev {
   hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
   int grid_lds = 0, grid_global = 0;
   uint32_t tiles_per_wave = 1;        // L2-LUT classify: 64-packet tiles per wave (NBG_TPW)
+  // NBG_LUT_TILED scratch (grown on demand, outside graph capture): per-packet LUT indices, bucket
+  // fill counts, and one bucket of (packet, index in tile) per 64-KiB LUT tile
+  uint32_t* d_idx = nullptr;
+  uint32_t* d_cursor = nullptr;
+  uint64_t* d_bucket = nullptr;
+  uint64_t tiled_cap = 0;
   // descriptor mode without lengths: a fixed_len-filled u16[] (the kernel reads off[] and len[])
   uint16_t* d_fixed_len = nullptr;
   uint64_t fixed_len_cap = 0;
@@ -164,6 +170,12 @@ int order_after_last(nbg_maglev* h, hipStream_t s) {
 }
 
 void free_scratch(nbg_maglev* h) {
+  (void)hipFree(h->d_idx);
+  (void)hipFree(h->d_cursor);
+  (void)hipFree(h->d_bucket);
+  h->d_idx = h->d_cursor = nullptr;
+  h->d_bucket = nullptr;
+  h->tiled_cap = 0;
   (void)hipFree(h->d_fixed_len);
   h->d_fixed_len = nullptr;
   h->fixed_len_cap = 0;
@@ -266,14 +278,17 @@ bool use_stream(const nbg_maglev* h, uint64_t n_pkts) {
   return on && !h->wide && h->m <= 65537 && n_pkts >= 262144;
 }
 
-// Batches of at most one partition take the single-launch small kernel; NBG_SMALL=0 disables it
-// (A/B measurements).
+// Batches of at most 2048 packets take the single-launch small kernel (one block: 3.5 us per call
+// back to back at 32 packets and 6.9 us at 1024, against 9.5 and 10.6 us for classify + group; at
+// 4096 packets one CU is too little: 14.1 against 11.0 us, profiles/r02_small_batches.json).
+// NBG_SMALL=0 disables it (A/B measurements).
 bool use_small(uint64_t n_pkts, uint32_t nbins, uint32_t flags, const uint8_t* d_pkts) {
   static const bool on = [] {
     const char* e = std::getenv("NBG_SMALL");
     return !e || std::atoi(e) != 0;
   }();
-  return on && n_pkts <= small_max() && nbins <= kMaxGroupBins && !(flags & (NBG_DEFER_GROUP | NBG_LUT_LDS)) &&
+  return on && n_pkts <= std::min<uint32_t>(small_max(), 2048) && nbins <= kMaxGroupBins &&
+         !(flags & (NBG_DEFER_GROUP | NBG_LUT_LDS | NBG_LUT_TILED)) &&
          (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0;
 }
 
@@ -480,6 +495,9 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const bool capturing = cap != hipStreamCaptureStatusNone;
   if (capturing && (flags & NBG_DEFER_GROUP))
     return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP cannot be captured in a graph");
+  if (capturing && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
+    return set_error(NBG_EINVAL, "classify: only single-launch batches (<= 2048 packets, <= %u backends, 16-B aligned) "
+                     "can be captured in a graph", kMaxGroupBins - 1);
   int rc = capturing ? NBG_OK : order_after_last(h, static_cast<hipStream_t>(stream));
   if (rc) return rc;
   const bool lds = use_lds_lut(h, flags);
@@ -567,7 +585,37 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     g.counts = d_counts ? d_counts : (d_perm ? h->d_counts : nullptr);
     return launch_small(a, g, h->wide, stream);
   }
-  if (a.lean && !lds && !lpm && use_stream(h, n_pkts)) {
+  const bool tiled = (flags & NBG_LUT_TILED) && h->wide && !lpm;
+  if (tiled) {
+    const uint32_t n_tiles = lut_tiles(h->m);
+    if (h->tiled_cap < n_pkts) {
+      if (capturing) return set_error(NBG_EINVAL, "classify: NBG_LUT_TILED scratch cannot grow in a graph");
+      (void)hipFree(h->d_idx);
+      (void)hipFree(h->d_cursor);
+      (void)hipFree(h->d_bucket);
+      h->d_idx = h->d_cursor = nullptr;
+      h->d_bucket = nullptr;
+      h->tiled_cap = 0;
+      NBG_HIP(hipMalloc(&h->d_idx, n_pkts * 4));
+      NBG_HIP(hipMalloc(&h->d_cursor, n_tiles * 4));
+      NBG_HIP(hipMalloc(&h->d_bucket, static_cast<size_t>(n_tiles) * n_pkts * 8));
+      h->tiled_cap = n_pkts;
+    }
+    a.idx_out = h->d_idx;
+    if ((rc = launch_classify_idx(a, grid, stream))) return rc;
+    NBG_HIP(hipMemsetAsync(h->d_cursor, 0, n_tiles * 4, static_cast<hipStream_t>(stream)));
+    TileArgs ta{};
+    ta.idx = h->d_idx;
+    ta.n_pkts = static_cast<uint32_t>(n_pkts);
+    ta.n_tiles = n_tiles;
+    ta.m = static_cast<uint32_t>(h->m);
+    ta.lut = h->d_lut;
+    ta.cursor = h->d_cursor;
+    ta.bucket = h->d_bucket;
+    ta.bucket_cap = static_cast<uint32_t>(h->tiled_cap);
+    ta.backend = d_backend;
+    rc = launch_tiled_lookup(ta, stream);
+  } else if (a.lean && !lds && !lpm && use_stream(h, n_pkts)) {
     const uint64_t waves = static_cast<uint64_t>(h->cus) * stream_waves_per_block();
     a.tiles_per_wave = static_cast<uint32_t>((n_tiles64 + waves - 1) / waves);
     a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);

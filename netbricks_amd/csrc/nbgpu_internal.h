@@ -66,6 +66,20 @@ struct ClassifyArgs {
   const uint16_t* tbl_long;
   uint32_t lpm_groups;
   uint16_t* gate;
+  uint32_t* idx_out;        // NBG_LUT_TILED: per-packet LUT index (0xffffffff = would panic)
+};
+
+// NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
+struct TileArgs {
+  const uint32_t* idx;      // [n_pkts] from the classify kernel (kIdx)
+  uint32_t n_pkts;
+  uint32_t n_tiles;
+  uint32_t m;               // LUT entries
+  const void* lut;          // u16 entries (padded to whole 16-B vectors)
+  uint32_t* cursor;         // [n_tiles] bucket fill counts (zeroed before the bucket kernel)
+  uint64_t* bucket;         // [n_tiles][bucket_cap] (packet << 32 | index in tile)
+  uint32_t bucket_cap;
+  uint16_t* backend;
 };
 
 struct HistArgs {
@@ -124,6 +138,9 @@ int launch_group_wide(const GroupArgs& a, void* stream);  // nb + 1 > kMaxGroupB
 // and (when g.perm / g.counts) group.  The batch base must be 16-B aligned.
 int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream);
 uint32_t small_max();
+int launch_classify_idx(const ClassifyArgs& a, int grid, void* stream);  // kIdx classify (tile per wave)
+int launch_tiled_lookup(const TileArgs& a, void* stream);
+uint32_t lut_tiles(uint64_t m);
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan);
 int pick_group_scan(uint32_t nbins, uint32_t n_parts);
 int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid);

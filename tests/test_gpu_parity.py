@@ -161,9 +161,11 @@ def test_imix_descriptors(torch_cuda, nb, m, lut_lds):
     mg.close()
 
 
-def test_c3_full_1m(torch_cuda):
+@pytest.mark.parametrize("tiled", [False, True])
+def test_c3_full_1m(torch_cuda, tiled):
     """BASELINE config C3 size: 1,048,576 IMIX frames (64-B aligned descriptors, in-place swap over
-    owned windows), 1000 backends, M = 655373 (u16 LUT, hist_kernel + scan_kernel grouping)."""
+    owned windows), 1000 backends, M = 655373 (u16 LUT, hist_kernel + scan_kernel grouping); with
+    the L2-gathered LUT and with the LDS-tiled lookup (NBG_LUT_TILED: 21 tiles of 64 KiB)."""
     from netbricks_amd import Maglev, make_trace
 
     names = [f"be{i}" for i in range(1000)]
@@ -175,7 +177,7 @@ def test_c3_full_1m(torch_cuda):
     d_buf = torch_cuda.from_numpy(buf.copy()).to(dev)
     d_off = torch_cuda.from_numpy(off.view(np.int32)).to(dev).view(torch_cuda.uint32)
     d_len = torch_cuda.from_numpy(ln.view(np.int16)).to(dev).view(torch_cuda.uint16)
-    r = mg.group_by(d_buf, n, offsets=d_off, lens=d_len, owned_windows=True)
+    r = mg.group_by(d_buf, n, offsets=d_off, lens=d_len, owned_windows=True, lut_tiled=tiled)
     torch_cuda.cuda.synchronize()
     mg.check()
     got = (d_buf.cpu().numpy(), r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16),
@@ -216,6 +218,33 @@ def _pack(frames, align):
     for o, f in zip(offs, frames):
         buf[o:o + len(f)] = np.frombuffer(bytes(f), dtype=np.uint8)
     return buf, np.array(offs, dtype=np.uint32), np.array(lens, dtype=np.uint16)
+
+
+@pytest.mark.parametrize("n,mode,nb,m", [(1, 0, 300, 65537), (5000, 0, 300, 65537), (70000, 1, 1000, 655373),
+                                        (300000, 0, 4096, 655373)])
+def test_lut_tiled_variants(torch_cuda, n, mode, nb, m):
+    """NBG_LUT_TILED at several sizes, layouts and table sizes (a LUT of 2 to 21 tiles)."""
+    from netbricks_amd import Maglev, make_trace
+
+    names = [f"t{i}" for i in range(nb)]
+    mg = Maglev(names, m)
+    lut = orc.lut_build(names, m)
+    buf, off, ln = make_trace(n, mode, seed=n + nb)
+    dev = torch_cuda.device("cuda:0")
+    d_buf = torch_cuda.from_numpy(buf.copy()).to(dev)
+    kw = {}
+    if mode:
+        kw = dict(offsets=torch_cuda.from_numpy(off.view(np.int32)).to(dev).view(torch_cuda.uint32),
+                  lens=torch_cuda.from_numpy(ln.view(np.int16)).to(dev).view(torch_cuda.uint16))
+    r = mg.group_by(d_buf, n, lut_tiled=True, **kw)
+    torch_cuda.cuda.synchronize()
+    mg.check()
+    got = (d_buf.cpu().numpy(), r.backend.view(torch_cuda.int16).cpu().numpy().view(np.uint16),
+           r.perm.view(torch_cuda.int32).cpu().numpy().view(np.uint32)[:n],
+           r.counts.view(torch_cuda.int32).cpu().numpy().view(np.uint32))
+    okw = dict(stride=64, fixed_len=60) if mode == 0 else dict(offs=off, lens=ln)
+    _assert_same(got, _oracle(buf, n, lut, nb, **okw))
+    mg.close()
 
 
 @pytest.mark.parametrize("align", [1, 4, 64])

@@ -41,7 +41,7 @@ def main():
     dev = torch.device("cuda:0")
     routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
     for cfg in args.config.split(","):
-        if cfg == "c3":
+        if cfg in ("c3", "c3t"):  # c3t: the LDS-tiled lookup (NBG_LUT_TILED) instead of the L2 gather
             names, m, nbk = [f"be{i}" for i in range(1000)], 655373, 1000
             bytes_pkt, classify_bytes = 88, 84
         elif cfg == "c5":
@@ -74,7 +74,7 @@ def main():
                                     defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream, **outs[j])
             else:
                 mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, swap_macs=True,
-                                defer_group=defer, stream=sts[j].cuda_stream, **outs[j])
+                                defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream, **outs[j])
 
         for i in range(args.warmup):
             step(i)
