@@ -537,6 +537,17 @@ template <int MODE>
 constexpr uint32_t row_of() { return MODE == 1 ? 64u : 48u; }
 constexpr uint32_t kLutLds = 65536;            // LUT bytes staged in LDS
 
+#ifdef NBG_SPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch:
+                   // [0] entry, [1] LUT visible (after the barrier), [2 + k] tile k landed, [11] exit
+constexpr uint32_t kSProbeWaves = 4096, kSProbeSlots = 12;
+__device__ unsigned long long g_sprobe[kSProbeWaves * kSProbeSlots];
+#define SPROBE(slot)                                                                              \
+  if (lane == 0 && blockIdx.x * kStreamW + wave < kSProbeWaves && (slot) < kSProbeSlots)          \
+    g_sprobe[(blockIdx.x * kStreamW + wave) * kSProbeSlots + (slot)] = wall_clock64();
+#else
+#define SPROBE(slot)
+#endif
+
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) void*)(p)));
@@ -696,6 +707,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
   const uint32_t n_tiles = (a.n_pkts + 63u) >> 6;
+  SPROBE(0)
   // Interleaved units: unit u = tiles [u*W, u*W + W), one per wave; block b takes units b, b + G,
   // b + 2G, ...  At any moment the grid reads consecutive units: one sequential sweep of the batch
   // (contiguous per-wave runs read ~3k streams at a fixed stride and measured 10 % slower:
@@ -714,9 +726,11 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 #else
   const uint32_t pieces = a.lut_lds_bytes >> 10;
 #endif
+  const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
+  // the LUT pieces first, then the first tiles (measured: tiles first, or the LUT through registers
+  // off the LDS-DMA path, are both ~0.8 us slower per launch)
   for (uint32_t q = wave; q < pieces; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
-  const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
   for (uint32_t k = 0; k < first; ++k) issue_tile<kRow>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
   if constexpr (HIST)
     for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
@@ -724,11 +738,13 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // makes every wave's pieces visible to every wave
   wait_tile(first);
   lds_sync();
+  SPROBE(1)
 
   for (uint32_t k = 0; k < nt; ++k) {
     const uint32_t t = tile_of(k);
     const uint32_t tb = t * 64u;
     wait_tile(min(nt - 1u - k, static_cast<uint32_t>(kStreamAhead)));
+    SPROBE(2 + k)
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
@@ -755,6 +771,10 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       }
     }
   }
+#ifdef NBG_SPROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores retired
+#endif
+  SPROBE(11)
 }
 
 // Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
@@ -1740,6 +1760,13 @@ int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int
 
 }  // namespace nbg
 
+#ifdef NBG_SPROBE
+// Diagnostic builds only (not part of include/nbgpu.h): the streaming kernel's per-wave timestamps.
+extern "C" int nbg_debug_sprobe(unsigned long long* out, uint64_t n) {
+  if (n > nbg::kSProbeWaves * nbg::kSProbeSlots) n = nbg::kSProbeWaves * nbg::kSProbeSlots;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_sprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
+}
+#endif
 #ifdef NBG_CPROBE
 // Diagnostic builds only (not part of include/nbgpu.h): the per-wave timestamps of the last launch.
 extern "C" int nbg_debug_cprobe(unsigned long long* out, uint64_t n) {
