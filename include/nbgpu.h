@@ -57,6 +57,10 @@ extern "C" {
 #define NBG_LUT_TILED 0x20u     /* u16 LUTs (> 256 backends): instead of gathering from L2, bucket the
                                    packets by 64-KiB LUT tile and look them up per tile in LDS
                                    (BASELINE config C3's named variant; measured slower) */
+#define NBG_STREAM_DESC 0x40u   /* descriptor layouts with NBG_OWNED_WINDOWS, >= 262144 packets: the
+                                   streaming classify kernel (one block per CU, everything fetched by
+                                   LDS-DMA).  Faster on one stream (C5 classify -5 %), slower when
+                                   several streams share the GPU (it cannot co-run): DESIGN.md §4 */
 
 typedef struct nbg_maglev nbg_maglev;
 
@@ -93,7 +97,8 @@ int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts);
  *   d_off      nullable u32 byte offsets (descriptor mode, e.g. IMIX)
  *   d_len      nullable u16 frame lengths (mbuf data_len); NULL => every frame is fixed_len
  *   n_pkts     packets in the batch, < 2^30
- *   flags      NBG_SWAP_MACS | NBG_LUT_LDS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP | NBG_LUT_TILED
+ *   flags      NBG_SWAP_MACS | NBG_LUT_LDS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP | NBG_LUT_TILED |
+ *              NBG_STREAM_DESC
  *   d_backend  out, n_pkts u16: backend index, or NBG_SENTINEL
  *   d_perm     out (nullable), n_pkts u32: packet indices grouped by backend 0..n-1 then the
  *              sentinel group, ascending index inside each group (per-group FIFO order)

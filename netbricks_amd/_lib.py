@@ -29,6 +29,7 @@ NBG_OWNED_WINDOWS = 0x4
 NBG_WB_PARTIAL = 0x8
 NBG_DEFER_GROUP = 0x10
 NBG_LUT_TILED = 0x20
+NBG_STREAM_DESC = 0x40
 NBG_HOST_SLOTS = 3
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1

@@ -777,6 +777,313 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   SPROBE(11)
 }
 
+// ---- streaming classify for descriptor layouts (IMIX: u32 offsets + u16 lengths, owned windows) ----
+//
+// Configs C5 (the lpm -> maglev chain: u8 LUT in LDS, tbl24 gathered) and the IMIX read-only /
+// record layouts (u8 LUT in LDS or the u16 LUT gathered).  Same block structure as
+// classify_stream_kernel (one block per CU, interleaved units, per-unit block histogram).  Per wave,
+// everything global arrives by LDS-DMA: the descriptors of a tile (off[64], len[64]) issued four
+// tiles ahead, the packet windows of a tile from its descriptors three tiles ahead, and the per-packet
+// gather (tbl24 or LUT entry, 2 B per lane) one tile ahead — so iteration k hashes tile k+1 and
+// issues its gather, then finishes tile k, whose gather had a whole iteration to land.
+//
+// vmcnt retires in issue order and hipcc does not count these loads, so the kernel keeps its own
+// wave-uniform count of issued VM operations (`seq`): each load group records the count after it,
+// and waiting for one is vmcnt(seq - recorded).  Every store instruction is issued by every lane
+// (lanes with nothing to store write to a scratch sink), so the count of stores per tile is a
+// known lower bound; uncounted operations (byte-wise path, histogram flush) only ever make a wait
+// stricter.
+// A 1- or 2-B LDS-DMA load still fills one dword per lane (measured: lane i's value at 4i), so the
+// u16 lengths and gathered entries take 4 B of LDS per lane.
+constexpr uint32_t kDescRing = 4;                   // descriptor slots per wave: tiles k+1 .. k+4
+constexpr uint32_t kDescLds = 64u * 4u + 64u * 4u;  // off[64] then len[64] (dword per lane)
+constexpr uint32_t kGatherLds = 64u * 4u;           // one dword per lane, two tiles
+
+template <int MODE>
+__host__ __device__ constexpr uint32_t desc_ring_tiles() { return MODE == 1 ? 4u : 3u; }
+
+template <int MODE>
+__host__ __device__ constexpr uint32_t desc_wave_lds() {
+  return desc_ring_tiles<MODE>() * 64u * row_of<MODE>() + kDescRing * kDescLds + 3u * kGatherLds;
+}
+
+// 4 or 2 B per lane from `src` into LDS at m0 + lane * 4.
+__device__ __forceinline__ void glds4(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+__device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_ushort %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+
+// Wait until at most n VM operations are outstanding (n above 31 waits for 31: stricter, still right).
+__device__ __forceinline__ void wait_vm_n(uint32_t n) {
+#define NBG_VMC(i) \
+  case i:          \
+    wait_vm<i>();  \
+    break;
+  switch (n) {
+    NBG_VMC(0) NBG_VMC(1) NBG_VMC(2) NBG_VMC(3) NBG_VMC(4) NBG_VMC(5) NBG_VMC(6) NBG_VMC(7)
+    NBG_VMC(8) NBG_VMC(9) NBG_VMC(10) NBG_VMC(11) NBG_VMC(12) NBG_VMC(13) NBG_VMC(14) NBG_VMC(15)
+    NBG_VMC(16) NBG_VMC(17) NBG_VMC(18) NBG_VMC(19) NBG_VMC(20) NBG_VMC(21) NBG_VMC(22) NBG_VMC(23)
+    NBG_VMC(24) NBG_VMC(25) NBG_VMC(26) NBG_VMC(27) NBG_VMC(28) NBG_VMC(29) NBG_VMC(30)
+    default:
+      wait_vm<31>();
+      break;
+  }
+#undef NBG_VMC
+}
+
+// A hashed tile waiting for its gather.
+struct DescTile {
+  uint32_t fast;   // packet on the fast path (valid, 16-B aligned, >= 48 B, IHL 5)
+  uint32_t bin;    // u8 LUT: the entry (LDS lookup)
+  uint32_t iplo;   // chain: low byte of the source address (tbl_long index)
+  uint32_t r0, r1, r2;  // records: the swapped MAC words
+};
+
+#ifndef NBG_DABL  // diagnostic ablations (wrong results): 1 no gathers, 2 no packet loads, 3 both
+#define NBG_DABL 0
+#endif
+
+// LUTM: kLdsU8Tail (u8 LUT staged in LDS) or kGlobalU16 (u16 LUT gathered from L2).
+// MODE: 0 = read only (always with CHAIN), 1 = in place (whole owned windows), 2 = 12-B records.
+template <int LUTM, bool F4, bool HIST, int MODE, bool CHAIN>
+__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(ClassifyArgs a) {
+  constexpr uint32_t kRow = row_of<MODE>(), kTileLds = 64u * kRow;
+  constexpr uint32_t kLut = LUTM == kLdsU8Tail ? kLutLds : 0u;
+  constexpr uint32_t kPR = desc_ring_tiles<MODE>();
+  constexpr bool kG = (CHAIN || LUTM == kGlobalU16) && !(NBG_DABL & 1);  // one 2-B gather per packet
+  // store instructions per tile (a lower bound: the compiler may not split them further)
+  constexpr uint32_t kS = 1u + (CHAIN ? 1u : 0u) + (MODE == 1 ? 4u : 0u) + (MODE == 2 ? 1u : 0u);
+  extern __shared__ __align__(16) uint8_t smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nbins = a.nb + 1;
+  uint8_t* lut = smem;
+  uint8_t* wbase = smem + kLut + wave * desc_wave_lds<MODE>();
+  uint8_t* ring = wbase;
+  uint8_t* dring = wbase + kPR * kTileLds;
+  uint8_t* gbuf = dring + kDescRing * kDescLds;
+  uint8_t* tlbuf = gbuf + 2u * kGatherLds;  // chain: tbl_long entries of the tile being finished
+  const uint32_t hstride = (nbins + 3) & ~3u;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(smem + kLut + kStreamW * desc_wave_lds<MODE>());
+  const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint32_t dring_lds = __builtin_amdgcn_readfirstlane(lds_addr(dring));
+  const uint32_t gbuf_lds = __builtin_amdgcn_readfirstlane(lds_addr(gbuf));
+  const uint32_t tl_lds = __builtin_amdgcn_readfirstlane(lds_addr(tlbuf));
+  const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
+  const uint32_t n_tiles = (a.n_pkts + 63u) >> 6;
+  const uint32_t n_units = (n_tiles + kStreamW - 1) / kStreamW;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t nt = b < n_units ? (n_units - b + G - 1) / G : 0u;
+  auto tile_of = [&](uint32_t k) { return (b + k * G) * kStreamW + wave; };
+  auto doff = [&](uint32_t k) {
+    return reinterpret_cast<const uint32_t*>(dring + (k % kDescRing) * kDescLds);
+  };
+  auto dlen = [&](uint32_t k) {
+    return reinterpret_cast<const uint32_t*>(dring + (k % kDescRing) * kDescLds + 256u);
+  };
+  uint8_t* sink = a.sink + lane * 16u;
+  uint32_t seq = 0;  // VM operations this wave issued (counted ones)
+  auto wait_seq = [&](uint32_t after) { wait_vm_n(seq - after); };
+  // descriptors of step k: lane i fetches off/len of packet tile_of(k)*64 + i (clamped)
+  auto issue_desc = [&](uint32_t k) {
+    const uint32_t p = min(tile_of(k) * 64u + lane, a.n_pkts - 1u);
+    const uint32_t d = dring_lds + (k % kDescRing) * kDescLds;
+    glds4(a.off + p, d);
+    glds2(a.len + p, d + 256u);
+    seq += 2;
+    return seq;
+  };
+  // packet windows of step k from its landed descriptors; a window off the 16-B grid is fetched
+  // from the batch base (its lane takes the byte-wise path)
+  auto issue_pk = [&](uint32_t k) {
+    constexpr uint32_t kCh = kRow / 16u;
+    const uint32_t* o = doff(k);
+    const uint32_t buf = ring_lds + (k % kPR) * kTileLds;
+    const uint32_t tb = tile_of(k) * 64u;
+    if ((kCh == 4u || lane < 16u * kCh) && !(NBG_DABL & 2)) {
+      const uint32_t pk = lane / kCh, ch = lane - pk * kCh;
+      uint32_t off[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) off[j] = o[j * 16u + pk];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t q = j * 16u + pk;
+        const uint8_t* src = (tb + q < a.n_pkts && (off[j] & 15u) == 0) ? a.pkts + off[j] + ch * 16u : a.pkts;
+        glds16(src, buf + j * (16u * kRow));
+      }
+    }
+    if (!(NBG_DABL & 2)) seq += 4;
+    return seq;
+  };
+  // hash step k's packets (landed) and issue their gather; returns the count after the gather
+  auto hash = [&](uint32_t k, DescTile& st) {
+    const uint32_t p = tile_of(k) * 64u + lane;
+    const uint8_t* x = ring + (k % kPR) * kTileLds + lane * kRow;
+    const uint4 c0 = *reinterpret_cast<const uint4*>(x);
+    const uint4 c1 = *reinterpret_cast<const uint4*>(x + 16);
+    const uint2 c2 = *reinterpret_cast<const uint2*>(x + 32);
+    const uint32_t off = doff(k)[lane], len = dlen(k)[lane] & 0xffffu;
+    const bool fast = p < a.n_pkts && (off & 15u) == 0 && len >= 48u && ((c0.w >> 16) & 0xfu) == 5u;
+    st.fast = fast;
+    // frame bytes: src 26..29, dst 30..33, ports 34..37, proto 23
+    const uint32_t src = (c1.z >> 16) | (c1.w << 16);
+    const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
+    const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
+    uint32_t lo, hi;
+    fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+    const uint32_t idx = F4 ? mod_f4(lo, hi) : mod_barrett(lo, hi, a.m, a.mu);
+    if constexpr (LUTM == kLdsU8Tail) st.bin = (idx >> 16) ? a.lut_tail : lut[idx & 0xffffu];
+    if constexpr (MODE == 2) {
+      st.r0 = (c0.y >> 16) | (c0.z << 16);
+      st.r1 = (c0.z >> 16) | (c0.x << 16);
+      st.r2 = (c0.x >> 16) | (c0.y << 16);
+    }
+    const uint32_t g = gbuf_lds + (k & 1u) * kGatherLds;
+    if constexpr (CHAIN) {
+      const uint32_t ip = __builtin_bswap32(src);
+      st.iplo = ip & 0xffu;
+      if (kG) glds2(a.tbl24 + (fast ? (ip >> 8) : 0u), g);
+    } else if constexpr (LUTM == kGlobalU16 && kG) {
+      glds2(static_cast<const uint16_t*>(a.lut) + (fast ? idx : 0u), g);
+    }
+    if constexpr (kG) ++seq;
+    return seq;
+  };
+
+  if constexpr (kLut) {
+    const uint32_t pieces = a.lut_lds_bytes >> 10;
+    for (uint32_t q = wave; q < pieces; q += kStreamW)
+      glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
+  }
+  if constexpr (HIST)
+    for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
+  // prologue: D(0..2) landed, P(0..2) and D(3) in flight
+  uint32_t sP1 = 0, sP2 = 0, sP3 = 0, sD3 = 0, sD4 = 0, sG0 = 0, sG1 = 0, sP0 = 0;
+  if (nt > 0) {
+    for (uint32_t j = 0; j < 3 && j < nt; ++j) issue_desc(j);
+    wait_vm<0>();  // the LUT pieces too
+    sP0 = issue_pk(0);
+    if (nt > 1) sP1 = issue_pk(1);
+    if (nt > 2) sP2 = issue_pk(2);
+    if (nt > 3) sD3 = issue_desc(3);
+  }
+  lds_sync();  // LUT and zeroed histograms visible to every wave
+  DescTile cur{}, nxt{};
+  if (nt > 0) {
+    wait_seq(sP0);
+    sG0 = hash(0, cur);
+  }
+  for (uint32_t k = 0; k < nt; ++k) {
+    const uint32_t tb = tile_of(k) * 64u;
+    const uint32_t p = tb + lane;
+    const bool valid = p < a.n_pkts;
+    // tile k's gather (issued one iteration ago)
+    uint32_t gv = 0;
+    if constexpr (kG) {
+      wait_seq(sG0);
+      gv = reinterpret_cast<const uint32_t*>(gbuf + (k & 1u) * kGatherLds)[lane] & 0xffffu;
+    }
+    uint32_t bin = LUTM == kLdsU8Tail ? cur.bin : gv;
+    uint32_t gate = kSentinel;
+    // chain: routes longer than /24 need a second, dependent gather (tbl_long); issued here, before
+    // the next tile's work, and waited for after it, so it does not drain the prefetches
+    bool lng = false, any_lng = false;
+    uint32_t sTL = 0;
+    if constexpr (CHAIN) {
+      gate = gv;
+      lng = cur.fast && (gv & 0x8000u);
+      any_lng = kG && __builtin_amdgcn_ballot_w64(lng) != 0;
+      if (any_lng) {
+        glds2(a.tbl_long + (lng ? ((gv & 0x7fffu) << 8) + cur.iplo : 0u), tl_lds);
+        sTL = ++seq;
+      }
+    }
+    if (k + 1 < nt) {
+      wait_seq(sP1);
+      sG1 = hash(k + 1, nxt);
+    }
+    if (k + 3 < nt) {
+      wait_seq(sD3);
+      sP3 = issue_pk(k + 3);
+    }
+    if constexpr (CHAIN) {
+      if (any_lng) {
+        wait_seq(sTL);
+        const uint32_t t = reinterpret_cast<const uint32_t*>(tlbuf)[lane] & 0xffffu;
+        if (lng) gate = t;
+      }
+    }
+    if constexpr (MODE == 1) {
+      // whole owned windows back from LDS: lane (quad, part) stores chunk `part` of packet
+      // 16j + quad, chunk 0 with the MACs swapped; lanes of other packets store to the sink
+      const uint8_t* tile = ring + (k % kPR) * kTileLds;
+      const uint32_t part = lane & 3u, quad = lane >> 2;
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t q = j * 16u + quad;
+        uint4 v = *reinterpret_cast<const uint4*>(tile + q * kRow + part * 16u);
+        const uint32_t qo = doff(k)[q], ql = dlen(k)[q] & 0xffffu;
+        const uint32_t w3 =
+            static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v.w), 0x00, 0xf, 0xf, false));
+        const bool qfast = tb + q < a.n_pkts && (qo & 15u) == 0 && ql >= 48u && ((w3 >> 16) & 0xfu) == 5u;
+        if (part == 0u)
+          v = make_uint4((v.y >> 16) | (v.z << 16), (v.z >> 16) | (v.x << 16), (v.x >> 16) | (v.y << 16), v.w);
+        stg16_nt(qfast ? a.pkts + qo + part * 16u : sink, v);
+      }
+    } else if constexpr (MODE == 2) {
+      uint32_t* mo = reinterpret_cast<uint32_t*>(cur.fast ? a.mac_out + static_cast<size_t>(p) * 12u : sink);
+      mo[0] = cur.r0;
+      mo[1] = cur.r1;
+      mo[2] = cur.r2;
+    }
+    if (valid && !cur.fast) {
+      // byte-wise loads: their waits stay inside this branch
+      bin = classify_slow<LUTM, F4, CHAIN>(a, lut, a.pkts + doff(k)[lane], dlen(k)[lane] & 0xffffu, p, gate);
+      asm volatile("" : "+v"(bin), "+v"(gate)::"memory");
+    }
+    if constexpr (CHAIN) {
+      if (cur.fast && gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
+      *(valid ? a.gate + p : reinterpret_cast<uint16_t*>(sink)) = static_cast<uint16_t>(gate);
+    }
+    *(valid ? a.backend + p : reinterpret_cast<uint16_t*>(sink)) = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+    seq += kS;
+    if constexpr (HIST) {
+      if (valid) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
+      lds_sync();
+      if (wave == k % kStreamW) {
+        uint32_t* h = hist + (k & 1u) * hstride;
+        stream_flush<HIST>(a, h, nbins, ((b + k * G) * kStreamW * 64u) / a.part_pkts, lane);
+      }
+    }
+    if (k + 4 < nt) sD4 = issue_desc(k + 4);  // into tile k's descriptor slot, now free
+    cur = nxt;
+    sP1 = sP2;
+    sP2 = sP3;
+    sD3 = sD4;
+    sG0 = sG1;
+  }
+}
+
 // Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
 // SGPR-base + 32-bit VGPR-offset form (one VGPR per address instead of two).
 __device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t byte_off) {
@@ -1543,6 +1850,47 @@ int launch_stream_mode(const ClassifyArgs& a, int mode, int grid, size_t lds, hi
   return NBG_OK;
 }
 
+template <int LUTM, bool F4, bool HIST, int MODE, bool CHAIN>
+int launch_desc_v(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
+  auto fn = classify_stream_desc_kernel<LUTM, F4, HIST, MODE, CHAIN>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return set_error(NBG_EIO, "streaming classify (descriptors): LDS attribute: %s",
+                       hipGetErrorString(hipGetLastError()));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "streaming classify (descriptors) launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+template <int LUTM, bool F4, bool HIST>
+int launch_desc_mode(const ClassifyArgs& a, int mode, int grid, size_t lds, hipStream_t s) {
+  if (a.tbl24) {
+    if constexpr (LUTM == kLdsU8Tail) return launch_desc_v<LUTM, F4, HIST, 0, true>(a, grid, lds, s);
+    return set_error(NBG_EINVAL, "streaming classify (descriptors): chain needs the u8 LUT");
+  }
+  if (mode == 2) return launch_desc_v<LUTM, F4, HIST, 2, false>(a, grid, lds, s);
+  if (mode == 1) {
+    if constexpr (LUTM == kGlobalU16) return launch_desc_v<LUTM, F4, HIST, 1, false>(a, grid, lds, s);
+    return set_error(NBG_EINVAL, "streaming classify (descriptors): in place needs the u16 LUT");
+  }
+  return launch_desc_v<LUTM, F4, HIST, 0, false>(a, grid, lds, s);
+}
+
+template <int LUTM>
+int launch_desc_lut(const ClassifyArgs& a, int mode, int grid, size_t lds, hipStream_t s) {
+  const bool hist = a.part_hist != nullptr;
+  if (a.m == 65537u)
+    return hist ? launch_desc_mode<LUTM, true, true>(a, mode, grid, lds, s)
+                : launch_desc_mode<LUTM, true, false>(a, mode, grid, lds, s);
+  return hist ? launch_desc_mode<LUTM, false, true>(a, mode, grid, lds, s)
+              : launch_desc_mode<LUTM, false, false>(a, mode, grid, lds, s);
+}
+
 size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
   const uint32_t waves = (lut_lds_bytes ? kLdsBlock : kBlock) / 64;
   return static_cast<size_t>(lut_lds_bytes) + waves * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
@@ -1557,6 +1905,20 @@ size_t stream_lds(uint32_t nb, int mode) {
 }
 
 int stream_waves_per_block() { return kStreamW; }
+
+size_t stream_desc_lds(uint32_t nb, int mode, bool wide_lut) {
+  const size_t hwords = 2 * (((nb + 1) + 3) & ~3u);
+  const size_t wave = mode == 1 ? desc_wave_lds<1>() : (mode == 2 ? desc_wave_lds<2>() : desc_wave_lds<0>());
+  return (wide_lut ? 0u : kLutLds) + static_cast<size_t>(kStreamW) * wave + hwords * 4u;
+}
+
+int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, void* stream) {
+  const int mode = a.tbl24 || !a.swap ? 0 : (a.mac_out ? 2 : 1);
+  const size_t lds = stream_desc_lds(a.nb, mode, wide_lut);
+  if (lds > 160u * 1024u) return set_error(NBG_EINVAL, "streaming classify (descriptors): %zu B of LDS", lds);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  return wide_lut ? launch_desc_lut<kGlobalU16>(a, mode, grid, lds, s) : launch_desc_lut<kLdsU8Tail>(a, mode, grid, lds, s);
+}
 
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;

@@ -67,6 +67,7 @@ struct nbg_maglev {
   uint32_t* d_part_prefix = nullptr;  // [kMaxParts][nb+1] (scan-kernel fallback)
   uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
   uint32_t* d_bin_base = nullptr;     // [nb+1]            (wide grouping path)
+  uint8_t* d_sink = nullptr;          // [1 KiB] stores of idle lanes (descriptor streaming kernel)
   uint32_t parity = 0;
   uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
@@ -184,12 +185,14 @@ void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_part_prefix);
   (void)hipFree(h->d_totals);
   (void)hipFree(h->d_bin_base);
+  (void)hipFree(h->d_sink);
   (void)hipFree(h->d_counts);
   h->d_part_hist = nullptr;
   h->d_part_graph = nullptr;
   h->d_part_prefix = nullptr;
   h->d_totals = nullptr;
   h->d_bin_base = nullptr;
+  h->d_sink = nullptr;
   h->d_counts = nullptr;
 }
 
@@ -243,6 +246,7 @@ int upload(nbg_maglev* h) {
   NBG_HIP(hipMalloc(&h->d_part_prefix, kMaxParts * nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_bin_base, nbins * sizeof(uint32_t)));
+  NBG_HIP(hipMalloc(&h->d_sink, 1024));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
   SetupStream st;  // complete before the handle is returned: any caller stream may use it next
   (void)st.h2d(h->d_lut, buf.data(), h->lut_alloc);
@@ -276,6 +280,18 @@ bool use_stream(const nbg_maglev* h, uint64_t n_pkts) {
     return !e || std::atoi(e) != 0;
   }();
   return on && !h->wide && h->m <= 65537 && n_pkts >= 262144;
+}
+
+// NBG_STREAM_DESC: descriptor layouts (IMIX offsets + lengths) with owned windows take the
+// streaming kernel too: the u8 LUT staged in LDS (read only, records, or the lpm chain), or the u16
+// LUT gathered from L2 (any mode, no chain).  The in-place mode with the u8 LUT does not fit LDS.
+// Opt-in: one stream, it classifies C5 in 27.1 us against 28.7 for the tile-per-wave kernel, but it
+// holds all LDS of every CU, so with three streams the tile-per-wave kernels co-running beat it
+// (profiles/r02_stream_desc_ab.txt).
+bool use_stream_desc(const nbg_maglev* h, uint64_t n_pkts, uint32_t flags, bool chain, int mode) {
+  if (!(flags & NBG_STREAM_DESC) || n_pkts < 262144) return false;
+  if (h->wide) return !chain;
+  return h->m <= 65537 && mode != 1;
 }
 
 // Batches of at most 2048 packets take the single-launch small kernel (one block: 3.5 us per call
@@ -623,6 +639,16 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     if (capturing && a.part_hist)
       NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
     rc = launch_classify_stream(a, h->cus, stream);
+  } else if (d_off && d_len && a.win_owned && !lds && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
+             use_stream_desc(h, n_pkts, flags, lpm != nullptr, lpm || !a.swap ? 0 : (a.mac_out ? 2 : 1))) {
+    if (!h->wide) {
+      a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
+      a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+    }
+    if (capturing && a.part_hist)
+      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
+    a.sink = h->d_sink;
+    rc = launch_classify_stream_desc(a, h->wide, h->cus, stream);
   } else {
     if (capturing && a.part_hist)
       NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));

@@ -67,6 +67,7 @@ struct ClassifyArgs {
   uint32_t lpm_groups;
   uint16_t* gate;
   uint32_t* idx_out;        // NBG_LUT_TILED: per-packet LUT index (0xffffffff = would panic)
+  uint8_t* sink;            // descriptor streaming kernel: 1 KiB scratch for stores of lanes with none
 };
 
 // NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
@@ -127,6 +128,10 @@ int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid
 // CU; a.tiles_per_wave = the contiguous 64-packet tiles of each of the grid's waves.
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream);
 int stream_waves_per_block();
+// Streaming classify for descriptor layouts with owned windows (u8 LUT in LDS, or the u16 LUT
+// gathered from L2); stream_desc_lds: its dynamic LDS bytes (mode 0 read only, 1 in place, 2 records).
+int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, void* stream);
+size_t stream_desc_lds(uint32_t nb, int mode, bool wide_lut);
 int launch_scan(const ScanArgs& a, void* stream);
 int launch_hist(const HistArgs& a, void* stream);
 bool hist_in_classify(uint32_t nbins);

@@ -15,7 +15,7 @@ from typing import Iterable, Tuple, Union
 import numpy as np
 
 from . import _lib
-from ._lib import NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, check, lib
+from ._lib import NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_STREAM_DESC, check, lib
 from .maglev import GroupedBatch, Maglev, _ptr
 
 __all__ = ["Lpm", "build_lpm", "chain_lpm_maglev", "LpmResult"]
@@ -88,7 +88,8 @@ class Lpm:
 
 def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int = 3, stride: int = 64,
                      frame_len: int = 60, offsets=None, lens=None, owned_windows: bool = False,
-                     defer_group: bool = False, group: bool = True, lut_lds: bool = False, gate=None,
+                     defer_group: bool = False, group: bool = True, lut_lds: bool = False,
+                     stream_desc: bool = False, gate=None,
                      backend=None, perm=None,
                      counts=None, stream=None) -> LpmResult:
     """lpm(...) -> maglev(...) over a device-resident batch (packet layout as Maglev.group_by)."""
@@ -106,7 +107,7 @@ def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int
     if stream is None:
         stream = torch.cuda.current_stream(dev).cuda_stream
     flags = ((NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_DEFER_GROUP if defer_group else 0)
-             | (NBG_LUT_LDS if lut_lds else 0))
+             | (NBG_LUT_LDS if lut_lds else 0) | (NBG_STREAM_DESC if stream_desc else 0))
     rc = lib.nbg_chain_lpm_maglev_device(mg._h, lpm._h, lpm_groups, _ptr(pkts), _ptr(offsets), _ptr(lens), stride,
                                          frame_len, n_pkts, flags, _ptr(gate), _ptr(backend),
                                          _ptr(perm) if group else None, _ptr(counts) if group else None, stream)

@@ -17,6 +17,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (NBG_DEFER_GROUP, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_OWNED_WINDOWS, NBG_SENTINEL,
+                   NBG_STREAM_DESC,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
@@ -135,7 +136,7 @@ class Maglev:
     def group_by(self, pkts, n_pkts: int, *, stride: int = 64, frame_len: int = 60, offsets=None, lens=None,
                  swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_lds: bool = False,
                  owned_windows: bool = False, wb_partial: bool = False,
-                 defer_group: bool = False, lut_tiled: bool = False,
+                 defer_group: bool = False, lut_tiled: bool = False, stream_desc: bool = False,
                  backend=None, perm=None, counts=None, mac_out=None, stream=None) -> GroupedBatch:
         """Classify a device-resident batch (torch uint8 tensor on this device).
 
@@ -168,7 +169,8 @@ class Maglev:
             stream = torch.cuda.current_stream(dev).cuda_stream
         flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_LUT_LDS if lut_lds else 0)
                  | (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_WB_PARTIAL if wb_partial else 0)
-                 | (NBG_DEFER_GROUP if defer_group else 0) | (NBG_LUT_TILED if lut_tiled else 0))
+                 | (NBG_DEFER_GROUP if defer_group else 0) | (NBG_LUT_TILED if lut_tiled else 0)
+                 | (NBG_STREAM_DESC if stream_desc else 0))
         rc = lib.nbg_maglev_classify_device_ex(self._h, _ptr(pkts), _ptr(offsets), _ptr(lens), stride, frame_len,
                                                n_pkts, flags, _ptr(backend), _ptr(perm) if scatter else None,
                                                _ptr(counts) if group else None, _ptr(mac_out), stream)

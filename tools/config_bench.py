@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--stream-desc", action="store_true", help="NBG_STREAM_DESC: the streaming classify kernel")
     args = ap.parse_args()
     import torch
 
@@ -71,10 +72,12 @@ def main():
             k = i % N_BATCHES
             if cfg == "c5":
                 nb.chain_lpm_maglev(mgs[j], lpm, bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
-                                    defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream, **outs[j])
+                                    defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream,
+                                    stream_desc=args.stream_desc, **outs[j])
             else:
                 mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, swap_macs=True,
-                                defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream, **outs[j])
+                                defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream,
+                                stream_desc=args.stream_desc, **outs[j])
 
         for i in range(args.warmup):
             step(i)
