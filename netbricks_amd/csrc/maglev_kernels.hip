@@ -523,13 +523,17 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
 #ifndef NBG_SW
 #define NBG_SW 8
 #endif
+#ifndef NBG_SEQWAIT  // 0: the round-2 tile-count waits (A/B)
+#define NBG_SEQWAIT 1
+#endif
 #ifndef NBG_SRING
 #define NBG_SRING 2
 #endif
 constexpr int kStreamNT = 64 * NBG_SW;         // threads per block (8 waves)
 constexpr int kStreamW = kStreamNT / 64;
 constexpr int kRing = NBG_SRING;               // LDS tile buffers per wave
-constexpr int kStreamAhead = kRing - 1;        // tiles in flight while one is classified
+[[maybe_unused]] constexpr int kStreamAhead = kRing - 1;  // tiles in flight while one is classified
+static_assert(kRing >= 2 && kRing <= 3, "classify_stream_kernel tracks the counts of three tiles at most");
 // LDS bytes per packet: 48 (chunks 0..2, all the classify reads) for read-only and records; 64 (the
 // whole slot) for the in-place swap, which then writes every line back whole from LDS (measured:
 // 48-B rows read faster, whole-line write-back beats 16-B partial-line stores)
@@ -580,6 +584,24 @@ __device__ __forceinline__ void wait_tile(uint32_t ahead) {
   else if (ahead == 2) wait_vm<8>();
   else if (ahead == 1) wait_vm<4>();
   else wait_vm<0>();
+}
+
+// Wait until at most n VM operations are outstanding (n above 31 waits for 31: stricter, still right).
+__device__ __forceinline__ void wait_vm_n(uint32_t n) {
+#define NBG_VMC(i) \
+  case i:          \
+    wait_vm<i>();  \
+    break;
+  switch (n) {
+    NBG_VMC(0) NBG_VMC(1) NBG_VMC(2) NBG_VMC(3) NBG_VMC(4) NBG_VMC(5) NBG_VMC(6) NBG_VMC(7)
+    NBG_VMC(8) NBG_VMC(9) NBG_VMC(10) NBG_VMC(11) NBG_VMC(12) NBG_VMC(13) NBG_VMC(14) NBG_VMC(15)
+    NBG_VMC(16) NBG_VMC(17) NBG_VMC(18) NBG_VMC(19) NBG_VMC(20) NBG_VMC(21) NBG_VMC(22) NBG_VMC(23)
+    NBG_VMC(24) NBG_VMC(25) NBG_VMC(26) NBG_VMC(27) NBG_VMC(28) NBG_VMC(29) NBG_VMC(30)
+    default:
+      wait_vm<31>();
+      break;
+  }
+#undef NBG_VMC
 }
 
 // Issue tile `t` (64 packets from tile base `tb`) into the LDS buffer at `buf`: instruction k
@@ -731,7 +753,15 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // off the LDS-DMA path, are both ~0.8 us slower per launch)
   for (uint32_t q = wave; q < pieces; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
-  for (uint32_t k = 0; k < first; ++k) issue_tile<kRow>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
+  // VM operations this wave issued after the LUT pieces (tile loads, and a lower bound of its
+  // stores): waiting for tile k is vmcnt(seq - its count), so the stores issued after a tile do not
+  // make the wait for it stricter (vmcnt counts stores too)
+  uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
+  for (uint32_t k = 0; k < first; ++k) {
+    issue_tile<kRow>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
+    seq += 4;
+    (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
+  }
   if constexpr (HIST)
     for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
   // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
@@ -743,7 +773,11 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   for (uint32_t k = 0; k < nt; ++k) {
     const uint32_t t = tile_of(k);
     const uint32_t tb = t * 64u;
+#if NBG_SEQWAIT
+    wait_vm_n(seq - sA);  // kStreamAhead tiles (and their stores) stay in flight
+#else
     wait_tile(min(nt - 1u - k, static_cast<uint32_t>(kStreamAhead)));
+#endif
     SPROBE(2 + k)
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
@@ -752,13 +786,24 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
                                                                  p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
+    uint32_t sN = 0;
     if (k + kRing < nt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       issue_tile<kRow>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
+      seq += 4;
+      sN = seq;
     }
     if (valid) {
       bin = stream_finish<F4>(a, lut, p, bin, slow);
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
+    }
+    if (t < n_tiles) ++seq;  // the backend store (lane 0 has a packet)
+    sA = sB;
+    if constexpr (kRing == 2) {
+      sB = sN;
+    } else {
+      sB = sC;
+      sC = sN;
     }
     if constexpr (HIST) {
       // every wave's counts of unit k are in hist[k & 1]; one wave flushes it into the unit's
@@ -833,23 +878,6 @@ __device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
       : "memory");
 }
 
-// Wait until at most n VM operations are outstanding (n above 31 waits for 31: stricter, still right).
-__device__ __forceinline__ void wait_vm_n(uint32_t n) {
-#define NBG_VMC(i) \
-  case i:          \
-    wait_vm<i>();  \
-    break;
-  switch (n) {
-    NBG_VMC(0) NBG_VMC(1) NBG_VMC(2) NBG_VMC(3) NBG_VMC(4) NBG_VMC(5) NBG_VMC(6) NBG_VMC(7)
-    NBG_VMC(8) NBG_VMC(9) NBG_VMC(10) NBG_VMC(11) NBG_VMC(12) NBG_VMC(13) NBG_VMC(14) NBG_VMC(15)
-    NBG_VMC(16) NBG_VMC(17) NBG_VMC(18) NBG_VMC(19) NBG_VMC(20) NBG_VMC(21) NBG_VMC(22) NBG_VMC(23)
-    NBG_VMC(24) NBG_VMC(25) NBG_VMC(26) NBG_VMC(27) NBG_VMC(28) NBG_VMC(29) NBG_VMC(30)
-    default:
-      wait_vm<31>();
-      break;
-  }
-#undef NBG_VMC
-}
 
 // A hashed tile waiting for its gather.
 struct DescTile {
