@@ -258,7 +258,12 @@ typedef struct {
     uint64_t checksum;
     double seconds;
     double t_start, t_end; /* CLOCK_MONOTONIC seconds around the thread's loop */
+    /* chain (config C5): test/lpm's stage before maglev when tbl24 is set */
+    const uint16_t *tbl24, *tbl_long;
+    uint32_t lpm_groups;
 } orc_shard_t;
+
+static inline uint16_t lpm_lookup(const uint16_t *tbl24, const uint16_t *tbl_long, uint32_t ip);
 
 #define RING 1024
 #define BURST 32
@@ -290,11 +295,64 @@ static void *shard_main(void *arg) {
     memo_t memo;
     memo_init(&memo, 1 << 12);
     uint64_t sum = 0;
+    /* chain: test/lpm's group_by(lpm_groups) rings of packet indices */
+    uint32_t nl = s->tbl24 ? s->lpm_groups : 0;
+    uint64_t **lring = (uint64_t **)calloc(nl ? nl : 1, sizeof(uint64_t *));
+    uint64_t *lhead = (uint64_t *)calloc(nl ? nl : 1, sizeof(uint64_t));
+    uint64_t *ltail = (uint64_t *)calloc(nl ? nl : 1, sizeof(uint64_t));
+    for (uint32_t g = 0; g < nl; g++) lring[g] = (uint64_t *)malloc(RING * sizeof(uint64_t));
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (uint32_t rep = 0; rep < s->reps; rep++)
     for (uint64_t b = s->begin; b < s->end; b += BURST) {
         uint64_t e = b + BURST < s->end ? b + BURST : s->end;
+        if (nl) {
+            /* test/lpm (nf.rs:212-221): parse Mac + Ip, lookup_entry on the source address,
+             * transform (MAC swap), group_by(lpm_groups); a packet the reference would panic on
+             * (runt, gate >= lpm_groups) gets the sentinel and goes no further */
+            for (uint64_t i = b; i < e; i++) {
+                uint8_t *f = s->buf + pkt_off(s->offs, s->stride, i);
+                uint32_t len = pkt_len(s->lens, s->fixed_len, i);
+                uint32_t gate = ORC_SENTINEL;
+                if (len >= ORC_ETH + 20) {
+                    const uint8_t *ip = f + ORC_ETH;
+                    gate = lpm_lookup(s->tbl24, s->tbl_long,
+                                      (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15]);
+                }
+                if (gate >= nl) {
+                    if (s->backend) s->backend[i] = ORC_SENTINEL;
+                    continue;
+                }
+                mac_swap(f);
+                if (lhead[gate] - ltail[gate] < RING - 1) lring[gate][lhead[gate]++ & (RING - 1)] = i;
+            }
+            /* test/maglev over the lpm groups in order: MAC swap back, group_fn, enqueue */
+            for (uint32_t lg = 0; lg < nl; lg++) {
+                while (ltail[lg] != lhead[lg]) {
+                    uint64_t i = lring[lg][ltail[lg]++ & (RING - 1)];
+                    uint8_t *f = s->buf + pkt_off(s->offs, s->stride, i);
+                    uint32_t len = pkt_len(s->lens, s->fixed_len, i);
+                    mac_swap(f);
+                    uint64_t h;
+                    uint32_t g;
+                    if (!flow_hash_of(f, len, &h))
+                        g = s->nb;
+                    else
+                        g = s->use_cache ? memo_get(&memo, h, s->lut, s->m) : s->lut[h % s->m];
+                    if (s->backend) s->backend[i] = g == s->nb ? ORC_SENTINEL : (uint16_t)g;
+                    meta[0][0] = (uint64_t)(uintptr_t)f;
+                    meta[0][1] = ORC_ETH;
+                    if (head[g] - tail[g] < RING - 1) ring[g][head[g]++ & (RING - 1)] = f;
+                }
+            }
+            for (uint32_t g = 0; g < ng; g++) {
+                while (tail[g] != head[g]) {
+                    uint8_t *f = ring[g][tail[g]++ & (RING - 1)];
+                    sum += (uint64_t)f[0] * (g + 1) + meta[0][1];
+                }
+            }
+            continue;
+        }
         /* transform: MAC swap over the burst */
         for (uint64_t i = b; i < e; i++) {
             uint8_t *f = s->buf + pkt_off(s->offs, s->stride, i);
@@ -329,6 +387,10 @@ static void *shard_main(void *arg) {
     s->t_end = (double)t1.tv_sec + 1e-9 * (double)t1.tv_nsec;
     s->checksum = sum;
     memo_free(&memo);
+    for (uint32_t g = 0; g < nl; g++) free(lring[g]);
+    free(lring);
+    free(lhead);
+    free(ltail);
     for (uint32_t g = 0; g < ng; g++) free(ring[g]);
     free(ring);
     free(head);
@@ -340,16 +402,18 @@ static void *shard_main(void *arg) {
 /* Runs `threads` pinned threads, each `reps` times over a contiguous shard of [0, n).
  * Returns wall seconds from the first thread's loop start to the last thread's loop end (thread
  * start-up excluded; threads that do not run concurrently, e.g. under a CPU quota, count in full). */
-double orc_cpu_baseline_reps(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
-                             uint32_t fixed_len, uint64_t n, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache,
-                             int threads, uint32_t reps, uint16_t *backend) {
+static double run_shards(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
+                         uint32_t fixed_len, uint64_t n, const uint16_t *tbl24, const uint16_t *tbl_long,
+                         uint32_t lpm_groups, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache, int threads,
+                         uint32_t reps, uint16_t *backend) {
     if (threads < 1) threads = 1;
     if (reps < 1) reps = 1;
     orc_shard_t *sh = (orc_shard_t *)calloc(threads, sizeof(orc_shard_t));
     pthread_t *tid = (pthread_t *)calloc(threads, sizeof(pthread_t));
     for (int t = 0; t < threads; t++) {
         sh[t] = (orc_shard_t){buf, offs, stride, lens, fixed_len, n * t / threads, n * (t + 1) / threads,
-                              lut, m, nb, use_cache, threads > 1 ? t : -1, reps, backend, 0, 0.0, 0.0, 0.0};
+                              lut, m, nb, use_cache, threads > 1 ? t : -1, reps, backend, 0, 0.0, 0.0, 0.0,
+                              tbl24, tbl_long, lpm_groups};
         pthread_create(&tid[t], NULL, shard_main, &sh[t]);
     }
     double first = 0.0, last = 0.0;
@@ -361,6 +425,23 @@ double orc_cpu_baseline_reps(uint8_t *buf, const uint64_t *offs, uint64_t stride
     free(sh);
     free(tid);
     return last - first;
+}
+
+double orc_cpu_baseline_reps(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
+                             uint32_t fixed_len, uint64_t n, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache,
+                             int threads, uint32_t reps, uint16_t *backend) {
+    return run_shards(buf, offs, stride, lens, fixed_len, n, NULL, NULL, 0, lut, m, nb, use_cache, threads, reps,
+                      backend);
+}
+
+/* The chained lpm -> maglev loop (config C5): per 32-packet burst test/lpm's stage (lookup,
+ * swap, group_by(lpm_groups) rings), then test/maglev's over those groups in order. */
+double orc_cpu_baseline_chain_reps(uint8_t *buf, const uint64_t *offs, uint64_t stride, const uint16_t *lens,
+                                   uint32_t fixed_len, uint64_t n, const uint16_t *tbl24, const uint16_t *tbl_long,
+                                   uint32_t lpm_groups, const uint32_t *lut, uint64_t m, uint32_t nb, int use_cache,
+                                   int threads, uint32_t reps, uint16_t *backend) {
+    return run_shards(buf, offs, stride, lens, fixed_len, n, tbl24, tbl_long, lpm_groups ? lpm_groups : 1, lut, m, nb,
+                      use_cache, threads, reps, backend);
 }
 
 /* One pass per thread (the round-1 entry point). */

@@ -44,6 +44,9 @@ def lib():
         L.orc_cpu_baseline_reps.restype = C.c_double
         L.orc_cpu_baseline_reps.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, C.c_uint64,
                                             C.c_uint32, C.c_int, C.c_int, C.c_uint32, _P]
+        L.orc_cpu_baseline_chain_reps.restype = C.c_double
+        L.orc_cpu_baseline_chain_reps.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, _P, C.c_uint32,
+                                                  _P, C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_uint32, _P]
         L.orc_lpm_build.restype = C.c_int
         L.orc_lpm_build.argtypes = [_P, _P, _P, C.c_uint64, _P, _P, C.POINTER(C.c_uint64)]
         L.orc_lpm_lookup.restype = None
@@ -139,3 +142,25 @@ def chain_classify(buf, n, t24, tl, lut, *, offs=None, stride=64, lens=None, fix
                              None if lens16 is None else lens16.ctypes.data, fixed_len, n, t24.ctypes.data,
                              tl.ctypes.data, lpm_groups, lut.ctypes.data, lut.size, gate.ctypes.data, be.ctypes.data)
     return gate[:n], be[:n]
+
+
+def cpu_baseline(buf, n, lut, nb, *, offs=None, stride=64, lens=None, fixed_len=60, chain=None, lpm_groups=3,
+                 cache=True, threads=1, reps=1):
+    """The reference's producer loop restated in C (the CPU baseline).  `chain` = (tbl24, tbl_long)
+    runs test/lpm's stage first (config C5).  Modifies `buf` (MAC swaps).  -> (wall seconds, backend)."""
+    lut = np.ascontiguousarray(lut, dtype=np.uint32)
+    offs64 = None if offs is None else np.ascontiguousarray(offs, dtype=np.uint64)
+    lens16 = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    be = np.empty(max(n, 1), dtype=np.uint16)
+    o = None if offs64 is None else offs64.ctypes.data
+    ln = None if lens16 is None else lens16.ctypes.data
+    if chain is None:
+        t = lib().orc_cpu_baseline_reps(buf.ctypes.data, o, stride, ln, fixed_len, n, lut.ctypes.data, lut.size, nb,
+                                        1 if cache else 0, threads, reps, be.ctypes.data)
+    else:
+        t24, tl = chain
+        tl = tl if tl.size else np.zeros(1, dtype=np.uint16)
+        t = lib().orc_cpu_baseline_chain_reps(buf.ctypes.data, o, stride, ln, fixed_len, n, t24.ctypes.data,
+                                              tl.ctypes.data, lpm_groups, lut.ctypes.data, lut.size, nb,
+                                              1 if cache else 0, threads, reps, be.ctypes.data)
+    return t, be[:n]

@@ -235,6 +235,42 @@ def test_trace_generator_deterministic_and_wellformed():
     assert np.all(ln0 == 60) and np.array_equal(off0, np.arange(100) * 64)
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_cpu_baseline_loop_matches_oracle(cfg):
+    """The CPU baseline (the reference's producer loop restated: bursts, memo map, rings; for C5
+    test/lpm's stage and its group rings first) computes the oracle's backends, on 2 threads, with
+    and without the memo map."""
+    import netbricks_amd as nb
+
+    n = 3000
+    if cfg == "c2":
+        names, m, mode = [f"backend-{i}" for i in range(65)], 65537, 0
+    elif cfg == "c3":
+        names, m, mode = [f"be{i}" for i in range(1000)], 655373, 1
+    else:
+        names, m, mode = [f"backend-{i}" for i in range(65)], 65537, 1
+    lut = orc.lut_build(names, m)
+    buf, off, ln = nb.make_trace(n, mode, seed=5)
+    kw = dict(stride=64, fixed_len=60) if mode == 0 else dict(offs=off, lens=ln)
+    if cfg == "c5":
+        routes = json.load(open(os.path.join(GOLD, "lpm_routes.json")))
+        rc, t24, tl = orc.lpm_build(routes["reference"] + routes["mixed"])
+        assert rc == 0
+        _, exp = orc.chain_classify(buf, n, t24, tl, lut, **kw)
+        chain = (t24, tl)
+    else:
+        exp = orc.classify(buf.copy(), n, lut, **kw)
+        chain = None
+    for cache in (True, False):
+        work = buf.copy()
+        t, got = orc.cpu_baseline(work, n, lut, len(names), chain=chain, cache=cache, threads=2, **kw)
+        assert t > 0
+        np.testing.assert_array_equal(got, exp)
+        if cfg == "c5":
+            np.testing.assert_array_equal(work, buf)  # lpm's and maglev's swaps cancel
+    assert (exp != 0xFFFF).any()
+
+
 def _header_symbols():
     txt = open(os.path.join(ROOT, "include", "nbgpu.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)

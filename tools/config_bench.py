@@ -27,6 +27,42 @@ BATCH = 1 << 20
 N_BATCHES = 8
 
 
+def cpu_baseline(cfg, names, m, routes, cpu_s=4.0):
+    """The reference's per-core loop restated in C (oracle/, kind "port"; for C5 test/lpm's stage and
+    group rings first), over one BATCH-packet trace of this config: all allowed cores, one core,
+    and without the memo map.  Test infrastructure used as the baseline only."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import orc
+    from bench import cpu_inventory
+
+    import netbricks_amd as nb
+
+    affinity, quota, model = cpu_inventory()
+    cores = max(1, min(affinity, int(quota))) if quota else affinity
+    lut = orc.lut_build(names, m)
+    buf, off, ln = nb.make_trace(BATCH, 1, seed=1000)
+    chain = None
+    if cfg == "c5":
+        rc, t24, tl = orc.lpm_build(routes["reference"] + routes["mixed"])
+        chain = (t24, tl)
+
+    def measure(threads, cache, budget):
+        t, _ = orc.cpu_baseline(buf, BATCH, lut, len(names), offs=off, lens=ln, chain=chain, cache=cache,
+                                threads=threads)
+        reps = int(min(max(1, budget / max(t * threads, 1e-6)), 10000))
+        t, _ = orc.cpu_baseline(buf, BATCH, lut, len(names), offs=off, lens=ln, chain=chain, cache=cache,
+                                threads=threads, reps=reps)
+        return round(BATCH * reps / t / 1e6, 1), reps
+
+    allc, ra = measure(cores, True, cpu_s)
+    single, r1 = measure(1, True, cpu_s / 4)
+    nocache, rn = measure(cores, False, cpu_s / 2)
+    return {"value": allc, "unit": "Mpps", "cores": cores, "kind": "port", "single_core_mpps": single,
+            "no_cache_mpps": nocache, "cpu_model": model,
+            "sample": f"one {BATCH:,}-packet IMIX trace of this config: {cores} pinned threads x {ra} passes, "
+                      f"1 thread x {r1} passes, no memo map {rn} passes"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3,c5")
@@ -34,6 +70,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--stream-desc", action="store_true", help="NBG_STREAM_DESC: the streaming classify kernel")
+    ap.add_argument("--cpu-baseline", action="store_true",
+                    help="also time the C port of the reference loop (oracle/) on this host's cores, same traces")
     args = ap.parse_args()
     import torch
 
@@ -116,6 +154,8 @@ def main():
         if cfg == "c5":
             g = gates[0].view(torch.int16).cpu().numpy().view(np.uint16)
             line["gate_hist"] = {str(k): int(v) for k, v in zip(*np.unique(g, return_counts=True))}
+        if args.cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(cfg, names, m, routes)
         print(json.dumps(line), flush=True)
         for mg in mgs:
             mg.close()
