@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 9
 mkdir -p gpurun_out
 for pass in 1 2; do
-  for L in a_seq b_warm; do
+  for L in a_dyn b_static; do
     only="classify noswap nogroup,classify inplace nogroup,classify mac_out nogroup"
     [ $L = c_seq_r3 ] && only="classify noswap nogroup,classify mac_out nogroup"
     echo "== $L (pass $pass)"
