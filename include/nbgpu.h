@@ -161,6 +161,19 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
                            uint64_t* ticket);
 int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket);
 
+/*
+ * Zero-copy host path: register a host memory region (a DPDK mempool's hugepage memory, as
+ * rte_extmem_register / rte_dev_dma_map would map it for a NIC) once, so that the GPU reads the
+ * header windows straight out of the mbufs and writes the MAC swap back into them over PCIe.
+ * Then nbg_maglev_classify_device_ex(h, dev_base, d_off, d_len, ...) classifies a burst with
+ * d_off[i] = (mbuf data address - base) (u32: regions below 4 GiB) and d_len[i] = data_len, both
+ * in HBM; pass NBG_OWNED_WINDOWS (mbuf data rooms are >= 2 KiB) and NBG_WB_PARTIAL (only the
+ * 16 B holding the MACs cross PCIe back).  No host thread touches a packet.  *dev_base receives
+ * the device address of base.  nbg_host_unregister(base) before the memory is freed.
+ */
+int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base);
+int nbg_host_unregister(void* base, int device);
+
 
 /* ---- chained NF: test/lpm -> test/maglev (BASELINE config C5) ------------- */
 

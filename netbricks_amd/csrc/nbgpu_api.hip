@@ -127,6 +127,17 @@ struct nbg_maglev {
 
 namespace {
 
+// NBG_OK, or NBG_ENODEV with the reason (no device: the path has no CPU fallback).
+int check_device(int device) {
+  int ndev = 0;
+  const hipError_t ce = hipGetDeviceCount(&ndev);
+  if (ce != hipSuccess || ndev <= 0)
+    return set_error(NBG_ENODEV, "no HIP device available (no CPU fallback): %s, %d devices", hipGetErrorString(ce),
+                     ndev);
+  if (device < 0 || device >= ndev) return set_error(NBG_ENODEV, "device %d out of range (%d devices)", device, ndev);
+  return NBG_OK;
+}
+
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -941,6 +952,31 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   NBG_HIP(hipEventRecord(t.done, hs));
   t.busy = true;
   *ticket = tk;
+  return NBG_OK;
+}
+
+int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base) {
+  if (!base || !bytes || !dev_base) return set_error(NBG_EINVAL, "host_register: null argument");
+  int rc = check_device(device);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  NBG_HIP(hipHostRegister(base, bytes, hipHostRegisterMapped));
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, base, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister(base);
+    return set_error(NBG_EIO, "host_register: hipHostGetDevicePointer: %s", hipGetErrorString(e));
+  }
+  *dev_base = static_cast<uint8_t*>(d);
+  return NBG_OK;
+}
+
+int nbg_host_unregister(void* base, int device) {
+  if (!base) return set_error(NBG_EINVAL, "host_unregister: null base");
+  int rc = check_device(device);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  NBG_HIP(hipHostUnregister(base));
   return NBG_OK;
 }
 

@@ -133,6 +133,39 @@ class Maglev:
     def check(self) -> None:
         check(lib.nbg_maglev_check(self._h), "nbg_maglev_check")
 
+    def group_by_region(self, region: "HostRegion", n_pkts: int, offsets, lens, *, swap_macs: bool = True,
+                        group: bool = True, backend=None, perm=None, counts=None, stream=None) -> GroupedBatch:
+        """Zero-copy host path: classify n_pkts frames that live in a registered host region
+        (frame i at region offset offsets[i], lens[i] bytes; both u32/u16 tensors on this device).
+        The GPU reads the header windows over PCIe and writes the swapped MACs back into the
+        frames (16 B per frame); mbuf-style owned 64-B windows are assumed."""
+        import torch
+
+        if region.device != self.device or region.dev_ptr is None:
+            raise ValueError("region: not registered on this handle's device")
+        dev = torch.device("cuda", self.device)
+        _check_dev("offsets", offsets, torch.uint32, n_pkts, dev)
+        _check_dev("lens", lens, torch.uint16, n_pkts, dev)
+        if offsets is None or lens is None:
+            raise ValueError("offsets and lens are required")
+        if backend is None:
+            backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
+        if group and perm is None:
+            perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev)
+        if group and counts is None:
+            counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev)
+        _check_dev("backend", backend, torch.uint16, n_pkts, dev)
+        _check_dev("perm", perm, torch.uint32, n_pkts, dev)
+        _check_dev("counts", counts, torch.uint32, self.n_backends + 1, dev)
+        if stream is None:
+            stream = torch.cuda.current_stream(dev).cuda_stream
+        flags = (NBG_SWAP_MACS if swap_macs else 0) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL
+        rc = lib.nbg_maglev_classify_device_ex(self._h, region.dev_ptr, _ptr(offsets), _ptr(lens), 0, 0, n_pkts,
+                                               flags, _ptr(backend), _ptr(perm) if group else None,
+                                               _ptr(counts) if group else None, None, stream)
+        check(rc, "nbg_maglev_classify_device_ex")
+        return GroupedBatch(backend, perm if group else None, counts if group else None)
+
     def group_by(self, pkts, n_pkts: int, *, stride: int = 64, frame_len: int = 60, offsets=None, lens=None,
                  swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_lds: bool = False,
                  owned_windows: bool = False, wb_partial: bool = False,
@@ -237,3 +270,32 @@ class Maglev:
                                           counts.ctypes.data if group else None)
         check(rc, "nbg_maglev_classify_host")
         return backend[:n], (perm[:n] if group else None), counts
+
+
+class HostRegion:
+    """A host memory region registered for zero-copy GPU access (nbg_host_register): the GPU reads
+    frames out of it and writes the MAC swap back over PCIe.  `array` is a writable, C-contiguous
+    numpy uint8 array (e.g. an mbuf pool); keep it alive while registered.  Offsets into it are u32,
+    so the region must stay below 4 GiB."""
+
+    def __init__(self, array: np.ndarray, device: int = 0):
+        if array.dtype != np.uint8 or not array.flags.c_contiguous or not array.flags.writeable:
+            raise ValueError("array: expected a writable C-contiguous uint8 numpy array")
+        if array.nbytes == 0 or array.nbytes > (1 << 32):
+            raise ValueError("array: 1 B .. 4 GiB")
+        self.array = array
+        self.device = device
+        d = C.c_void_p()
+        check(lib.nbg_host_register(array.ctypes.data, array.nbytes, device, C.byref(d)), "nbg_host_register")
+        self.dev_ptr = d.value
+
+    def close(self) -> None:
+        if self.dev_ptr is not None:
+            self.dev_ptr = None
+            check(lib.nbg_host_unregister(self.array.ctypes.data, self.device), "nbg_host_unregister")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

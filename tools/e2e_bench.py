@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--host-n", type=int, default=1 << 20)
     ap.add_argument("--host-batches", type=int, default=12)
+    ap.add_argument("--thp", action="store_true",
+                    help="advise transparent huge pages for the mbuf pool (measured slower for the host gather)")
     args = ap.parse_args()
     import torch
 
@@ -86,9 +88,26 @@ def main():
     # (b) the synchronous host-mbuf entry point and (c) the pipelined one, over 2-KiB mbufs
     hn = args.host_n
     room = 2048
-    mbufs = np.zeros((hn, room), dtype=np.uint8)
+    # DPDK mempools live in hugepages; --thp advises transparent huge pages (2 MiB) for the pool.
+    # Measured on the box: the pipelined host path ran 155 Mpps with THP against 203 with 4-KiB pages
+    import mmap
+
+    pool = mmap.mmap(-1, hn * room, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+    thp = False
+    if args.thp and hasattr(mmap, "MADV_HUGEPAGE"):
+        try:
+            pool.madvise(mmap.MADV_HUGEPAGE)
+            thp = True
+        except OSError:
+            pass
+    mbufs = np.frombuffer(pool, dtype=np.uint8).reshape(hn, room)
     mbufs[:, :64] = np.resize(buf.reshape(n, 64), (hn, 64))
     ptrs = (np.arange(hn, dtype=np.uint64) * room + np.uint64(mbufs.ctypes.data)).astype(np.uint64)
+    try:
+        res["mbuf_pool_pages"] = ("THP advised (" + open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+                                  + ")") if thp else "4 KiB"
+    except OSError:
+        res["mbuf_pool_pages"] = "THP advised" if thp else "4 KiB"
     lens = np.full(hn, 60, dtype=np.uint16)
     outs = [(np.empty(hn, dtype=np.uint16), np.empty(hn, dtype=np.uint32), np.empty(66, dtype=np.uint32))
             for _ in range(2)]
@@ -123,6 +142,47 @@ def main():
                             "batches": args.host_batches, "ms_per_batch": round(dt / args.host_batches * 1e3, 3),
                             "h2d_bytes_per_pkt": 50, "d2h_bytes_per_pkt": 18, "mbuf_data_room": room,
                             "host_threads": "<= 16 (persistent pool)"}
+    # (d) zero-copy: the mbuf pool registered once (nbg_host_register); the GPU reads the header
+    # windows out of the mbufs and writes the MAC swap back over PCIe.  Per batch only offsets and
+    # lengths go H2D (6 B/pkt) and backend / perm / counts come back (6 B/pkt); 2 streams
+    reg = nb.HostRegion(mbufs.reshape(-1))
+    offs = (np.arange(hn, dtype=np.uint64) * room).astype(np.uint32)
+    h_off = torch.from_numpy(offs.view(np.int32)).pin_memory()
+    h_len = torch.from_numpy(lens.view(np.int16)).pin_memory()
+    ZS = 2
+    zmg = [mg] + [nb.Maglev(names, 65537) for _ in range(ZS - 1)]
+    zst = [torch.cuda.Stream(dev) for _ in range(ZS)]
+    zb = [dict(off=torch.empty(hn, dtype=torch.int32, device=dev), ln=torch.empty(hn, dtype=torch.int16, device=dev),
+               be=torch.empty(hn, dtype=torch.uint16, device=dev), pm=torch.empty(hn, dtype=torch.uint32, device=dev),
+               ct=torch.empty(66, dtype=torch.uint32, device=dev), h_be=torch.empty(hn, dtype=torch.int16).pin_memory(),
+               h_pm=torch.empty(hn, dtype=torch.int32).pin_memory(), h_ct=torch.empty(66, dtype=torch.int32).pin_memory())
+          for _ in range(ZS)]
+
+    def zbatch(i):
+        j = i % ZS
+        b, st = zb[j], zst[j]
+        with torch.cuda.stream(st):
+            b["off"].copy_(h_off, non_blocking=True)
+            b["ln"].copy_(h_len, non_blocking=True)
+            zmg[j].group_by_region(reg, hn, b["off"].view(torch.uint32), b["ln"].view(torch.uint16), backend=b["be"],
+                                   perm=b["pm"], counts=b["ct"], stream=st.cuda_stream)
+            b["h_be"].copy_(b["be"].view(torch.int16), non_blocking=True)
+            b["h_pm"].copy_(b["pm"].view(torch.int32), non_blocking=True)
+            b["h_ct"].copy_(b["ct"].view(torch.int32), non_blocking=True)
+
+    for i in range(2 * ZS):
+        zbatch(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.host_batches):
+        zbatch(i)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    res["zero_copy"] = {"mpps": round(hn * args.host_batches / dt / 1e6, 1), "batch_pkts": hn,
+                        "batches": args.host_batches, "ms_per_batch": round(dt / args.host_batches * 1e3, 3),
+                        "h2d_bytes_per_pkt": 6, "d2h_bytes_per_pkt": 6, "pcie_read_bytes_per_pkt": 64,
+                        "pcie_write_bytes_per_pkt": 16, "mbuf_data_room": room, "streams": ZS, "host_threads": 0}
+    reg.close()
     print(json.dumps(res))
     _ = C
 
