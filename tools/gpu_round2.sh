@@ -9,7 +9,7 @@ timeout -k 10 120 ./tools/small_bench > gpurun_out/small_new.json || exit $?
 NBG_SMALL=0 timeout -k 10 120 ./tools/small_bench > gpurun_out/small_old.json || exit $?
 cat gpurun_out/small_new.json gpurun_out/small_old.json
 echo "== configs"
-timeout -k 10 400 python -u tools/config_bench.py > gpurun_out/configs.json 2> gpurun_out/configs.err
+timeout -k 10 500 python -u tools/config_bench.py --cpu-baseline > gpurun_out/configs.json 2> gpurun_out/configs.err
 rc=$?; cat gpurun_out/configs.json; [ $rc -ne 0 ] && { tail -5 gpurun_out/configs.err; exit $rc; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R0/gpurun_out/prof/cfg" -o run --output-format csv -- python "$R0/tools/config_bench.py" --streams 1 --steps 50 --warmup 5 > "$R0/gpurun_out/prof/cfg.json" 2> "$R0/gpurun_out/prof/cfg.err"
