@@ -23,7 +23,7 @@ def _run(n):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("n", [1, 2, 4])
 def test_launcher_spawns_ranks(n):
     line = _run(n)
     assert line["n_gpus"] == n
