@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--stream-desc", action="store_true", help="NBG_STREAM_DESC: the streaming classify kernel")
+    ap.add_argument("--lut-lds", action="store_true", help="NBG_LUT_LDS: stage the LUT in LDS (u8/u16 LUT <= 72 KiB)")
     ap.add_argument("--cpu-baseline", action="store_true",
                     help="also time the C port of the reference loop (oracle/) on this host's cores, same traces")
     args = ap.parse_args()
@@ -111,11 +112,11 @@ def main():
             if cfg == "c5":
                 nb.chain_lpm_maglev(mgs[j], lpm, bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
                                     defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream,
-                                    stream_desc=args.stream_desc, **outs[j])
+                                    stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])
             else:
                 mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, swap_macs=True,
                                 defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream,
-                                stream_desc=args.stream_desc, **outs[j])
+                                stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])
 
         for i in range(args.warmup):
             step(i)
