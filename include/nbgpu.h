@@ -170,6 +170,8 @@ int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket);
  * in HBM; pass NBG_OWNED_WINDOWS (mbuf data rooms are >= 2 KiB) and NBG_WB_PARTIAL (only the
  * 16 B holding the MACs cross PCIe back).  No host thread touches a packet.  *dev_base receives
  * the device address of base.  nbg_host_unregister(base) before the memory is freed.
+ * nbg_maglev_host_submit / nbg_maglev_classify_host take this path by themselves when every frame
+ * of a batch (and the 64 B from its start) lies in one registered region of the handle's device.
  */
 int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base);
 int nbg_host_unregister(void* base, int device);

@@ -127,6 +127,28 @@ struct nbg_maglev {
 
 namespace {
 
+// Host regions registered with nbg_host_register: host_submit batches whose frames all lie in one
+// of them take the zero-copy path (the GPU reads and rewrites the frames over PCIe).
+struct HostRegionRec {
+  uintptr_t base;
+  uint64_t bytes;
+  uint8_t* dev;
+  int device;
+};
+std::mutex g_regions_mu;
+std::vector<HostRegionRec> g_regions;
+
+bool find_region(const void* p, int device, HostRegionRec* out) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::lock_guard<std::mutex> g(g_regions_mu);
+  for (const auto& r : g_regions)
+    if (r.device == device && a >= r.base && a - r.base < r.bytes) {
+      *out = r;
+      return true;
+    }
+  return false;
+}
+
 // NBG_OK, or NBG_ENODEV with the reason (no device: the path has no CPU fallback).
 int check_device(int device) {
   int ndev = 0;
@@ -928,6 +950,42 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     *ticket = tk;
     return NBG_OK;
   }
+  // zero-copy: every frame (and the 64 B the kernel may read from its start) lies in one registered
+  // region below 4 GiB: only offsets and lengths cross PCIe; the kernel reads the frames and writes
+  // the MAC chunk back in host memory, and no host thread touches a packet
+  HostRegionRec reg{};
+  if (n <= t.cap && find_region(pkt_ptrs[0], h->device, &reg) && reg.bytes <= (1ull << 32)) {
+    std::atomic<bool> inside{true};
+    uint32_t* h_off = reinterpret_cast<uint32_t*>(t.h_win);
+    parallel_for(n, [&](uint64_t b, uint64_t e) {
+      bool ok = true;
+      for (uint64_t i = b; i < e; ++i) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(pkt_ptrs[i]);
+        ok &= a >= reg.base && a + 64 <= reg.base + reg.bytes;
+        h_off[i] = static_cast<uint32_t>(a - reg.base);
+        t.h_len[i] = lens[i];
+      }
+      if (!ok) inside.store(false);
+    });
+    if (inside.load()) {
+      hipStream_t hs = h->host_compute;
+      t.swap = false;  // the kernel rewrites the frames itself
+      NBG_HIP(hipMemcpyAsync(t.d_win, h_off, n * 4, hipMemcpyHostToDevice, hs));
+      NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
+      const bool group = perm_out || counts_out;
+      rc = nbg_maglev_classify_device_ex(h, reg.dev, reinterpret_cast<const uint32_t*>(t.d_win), t.d_len, 0, 0, n,
+                                         (flags & ~NBG_DEFER_GROUP) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL, t.d_backend,
+                                         perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr, nullptr, hs);
+      if (rc) return rc;
+      NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, hs));
+      if (perm_out) NBG_HIP(hipMemcpyAsync(t.h_perm, t.d_perm, n * 4, hipMemcpyDeviceToHost, hs));
+      if (counts_out) NBG_HIP(hipMemcpyAsync(t.h_counts, t.d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, hs));
+      NBG_HIP(hipEventRecord(t.done, hs));
+      t.busy = true;
+      *ticket = tk;
+      return NBG_OK;
+    }
+  }
   // gather at 48-B windows; a batch with longer IP headers is staged again at the stride it needs
   uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len);
   if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len);
@@ -968,6 +1026,8 @@ int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base
     return set_error(NBG_EIO, "host_register: hipHostGetDevicePointer: %s", hipGetErrorString(e));
   }
   *dev_base = static_cast<uint8_t*>(d);
+  std::lock_guard<std::mutex> lk(g_regions_mu);
+  g_regions.push_back({reinterpret_cast<uintptr_t>(base), bytes, *dev_base, device});
   return NBG_OK;
 }
 
@@ -976,6 +1036,14 @@ int nbg_host_unregister(void* base, int device) {
   int rc = check_device(device);
   if (rc) return rc;
   DeviceGuard g(device);
+  {
+    std::lock_guard<std::mutex> lk(g_regions_mu);
+    for (size_t i = 0; i < g_regions.size(); ++i)
+      if (g_regions[i].base == reinterpret_cast<uintptr_t>(base) && g_regions[i].device == device) {
+        g_regions.erase(g_regions.begin() + static_cast<std::ptrdiff_t>(i));
+        break;
+      }
+  }
   NBG_HIP(hipHostUnregister(base));
   return NBG_OK;
 }

@@ -79,3 +79,35 @@ def test_region_rejects_closed_and_bad_arrays(torch_cuda):
     with pytest.raises(ValueError):
         nb.HostRegion(np.zeros((4, 16), dtype=np.uint8)[:, :8])
     mg.close()
+
+
+def test_host_submit_takes_zero_copy_for_registered_pool(torch_cuda):
+    """nbg_maglev_host_submit over mbufs inside a registered region: the GPU rewrites the frames
+    itself (the swap is in host memory once the device is idle, before host_wait), results
+    bit-exact; the same batch from an unregistered pool takes the gather path (swap at wait)."""
+    import netbricks_amd as nb
+
+    torch = torch_cuda
+    n = 20000
+    pool, offs, lens = _pool(n, seed=11)
+    ref = pool.copy()
+    be = orc.classify(ref, n, orc.lut_build(NAMES, 65537), offs=offs, lens=lens)
+    perm, counts = orc.group(be, 65)
+    mg = nb.Maglev(NAMES, 65537)
+    for registered in (True, False):
+        work = pool.copy()
+        ptrs = (offs.astype(np.uint64) + np.uint64(work.ctypes.data)).astype(np.uint64)
+        reg = nb.HostRegion(work) if registered else None
+        out_be, out_pm, out_ct = np.empty(n, np.uint16), np.empty(n, np.uint32), np.empty(66, np.uint32)
+        tk = mg.host_submit(ptrs, lens, out_be, out_pm, out_ct)
+        torch.cuda.synchronize()
+        swapped_before_wait = np.array_equal(work, ref)
+        mg.host_wait(tk)
+        np.testing.assert_array_equal(out_be, be)
+        np.testing.assert_array_equal(out_pm, perm)
+        np.testing.assert_array_equal(out_ct, counts)
+        np.testing.assert_array_equal(work, ref)
+        assert swapped_before_wait == registered
+        if reg is not None:
+            reg.close()
+    mg.close()
