@@ -2,11 +2,12 @@
 // path, driven from a pcap port (the eth_pcap PMD of the reference's example tests).
 //
 //   nb_maglev --rx in.pcap --tx out.pcap [--backends N | --names a,b,c] [--table 65537]
-//             [--batch 4096] [--order order.txt]
+//             [--batch 4096] [--order order.txt] [--zero-copy 1]
 //
 // Default backends are the reference's ["Larry", "Curly", "Moe"] (main.rs:36).  Prints one
 // JSON line with rx/tx/dropped counts and the per-group packet counts; --order writes the rx
-// index of every transmitted frame (one per line) for order checks.
+// index of every transmitted frame (one per line) for order checks.  --zero-copy 1 registers the
+// port's mempool (nbg_host_register), so the GPU reads and rewrites the frames in place over PCIe.
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -21,6 +22,7 @@ int main(int argc, char** argv) {
   std::vector<std::string> names = {"Larry", "Curly", "Moe"};
   uint64_t table = 65537;
   uint32_t batch = 4096;
+  bool zero_copy = false;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
     if (k == "--rx") rx = v;
@@ -28,6 +30,7 @@ int main(int argc, char** argv) {
     else if (k == "--order") order = v;
     else if (k == "--table") table = std::strtoull(v.c_str(), nullptr, 10);
     else if (k == "--batch") batch = static_cast<uint32_t>(std::strtoul(v.c_str(), nullptr, 10));
+    else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
       names.clear();
       for (int b = 0, n = std::atoi(v.c_str()); b < n; ++b) names.push_back("backend-" + std::to_string(b));
@@ -46,6 +49,11 @@ int main(int argc, char** argv) {
   }
   try {
     auto port = std::make_shared<nb::PcapPort>(rx);
+    auto pool = port->mempool();
+    if (zero_copy && pool.second) {
+      uint8_t* dev = nullptr;
+      nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
+    }
     nb::StandaloneScheduler sched;
     auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch);
     // run until the capture is consumed and every group queue has drained
@@ -61,10 +69,12 @@ int main(int argc, char** argv) {
       for (size_t i : port->tx_index()) std::fprintf(f, "%zu\n", i);
       std::fclose(f);
     }
-    std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"would_panic\": %llu, \"backends\": %zu}\n",
+    if (zero_copy && pool.second) nb::check(nbg_host_unregister(pool.first, 0), "nbg_host_unregister");
+    std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"would_panic\": %llu, \"backends\": %zu, "
+                "\"zero_copy\": %s}\n",
                 port->rx_total(), static_cast<unsigned long long>(pipe.tx->sent),
                 static_cast<unsigned long long>(pipe.groups->dropped()),
-                static_cast<unsigned long long>(pipe.groups->would_panic()), names.size());
+                static_cast<unsigned long long>(pipe.groups->would_panic()), names.size(), zero_copy ? "true" : "false");
   } catch (const nb::NbError& e) {
     std::fprintf(stderr, "nb_maglev: %s\n", e.what());
     return e.code == NBG_ENODEV ? 3 : 1;

@@ -37,11 +37,12 @@ namespace nb {
 constexpr size_t kHeaderSlot = 0, kOffsetSlot = 1;
 struct MBuf {
   std::vector<uint8_t> storage;  // data room (DPDK: >= 2 KiB, so 64-B windows are owned)
+  uint8_t* room = nullptr;       // or a data room inside a port's mempool (then storage is empty)
   uint16_t data_len = 0;
   uintptr_t meta[2] = {0, 0};    // HEADER_SLOT, OFFSET_SLOT
   uint64_t port_seq = 0;         // position in the receiving port's stream (bookkeeping)
-  uint8_t* data() { return storage.data(); }
-  uint8_t* data_address(size_t off) { return storage.data() + off; }  // native/zcsi/mbuf.rs:34-37
+  uint8_t* data() { return room ? room : storage.data(); }
+  uint8_t* data_address(size_t off) { return data() + off; }  // native/zcsi/mbuf.rs:34-37
   // native/zcsi/mbuf.rs:8-21
   static uintptr_t read_metadata_slot(const MBuf* m, size_t slot) { return m->meta[slot]; }
   static void write_metadata_slot(MBuf* m, size_t slot, uintptr_t v) { m->meta[slot] = v; }

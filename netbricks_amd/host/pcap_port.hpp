@@ -57,17 +57,27 @@ inline void write_pcap(const std::string& path, const std::vector<PcapRecord>& r
 // One port with an rx capture (consumed once) and a tx capture (collected in send order).
 class PcapPort : public PacketRx, public PacketTx {
  public:
+  // The frames live in one contiguous mempool of fixed data rooms (as a DPDK mempool's do), so the
+  // pool can be registered for zero-copy GPU access (mempool() + nbg_host_register).
   explicit PcapPort(const std::string& rx_path, uint32_t data_room = 2048) {
-    for (auto& r : read_pcap(rx_path)) {
+    auto recs = read_pcap(rx_path);
+    room_ = data_room;
+    for (auto& r : recs) room_ = std::max<size_t>(room_, (r.data.size() + 63) & ~size_t{63});
+    mem_.assign(recs.size() * room_ + 4096, 0);
+    base_ = mem_.data() + ((4096 - reinterpret_cast<uintptr_t>(mem_.data()) % 4096) % 4096);  // page-aligned
+    uint8_t* base = base_;
+    for (auto& r : recs) {
       auto m = std::make_unique<MBuf>();
-      m->storage.assign(std::max<size_t>(data_room, r.data.size()), 0);
-      std::memcpy(m->storage.data(), r.data.data(), r.data.size());
+      m->room = base + pool_.size() * room_;
+      std::memcpy(m->room, r.data.data(), r.data.size());
       m->data_len = static_cast<uint16_t>(r.data.size());
       m->port_seq = pool_.size();
       ts_.push_back({r.ts_sec, r.ts_usec});
       pool_.push_back(std::move(m));
     }
   }
+  // the mempool's memory: every frame's data room lies in [data, data + bytes)
+  std::pair<uint8_t*, size_t> mempool() { return {base_, pool_.size() * room_}; }
   uint32_t recv(MBuf** pkts, uint32_t cap) override {
     uint32_t n = 0;
     while (n < cap && next_ < pool_.size()) pkts[n++] = pool_[next_++].get();
@@ -88,6 +98,9 @@ class PcapPort : public PacketRx, public PacketTx {
   const std::vector<size_t>& tx_index() const { return tx_index_; }  // rx position of each sent frame
 
  private:
+  std::vector<uint8_t> mem_;
+  uint8_t* base_ = nullptr;
+  size_t room_ = 2048;
   std::vector<std::unique_ptr<MBuf>> pool_;
   std::vector<std::pair<uint32_t, uint32_t>> ts_;
   size_t next_ = 0;
