@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--stream-desc", action="store_true", help="NBG_STREAM_DESC: the streaming classify kernel")
     ap.add_argument("--lut-lds", action="store_true", help="NBG_LUT_LDS: stage the LUT in LDS (u8/u16 LUT <= 72 KiB)")
+    ap.add_argument("--c3-variant", default="in_place", choices=["in_place", "records", "read_only"],
+                    help="C3's MAC handling: in place (default), 12-B records, or none (parse + hash + lookup)")
     ap.add_argument("--cpu-baseline", action="store_true",
                     help="also time the C port of the reference loop (oracle/) on this host's cores, same traces")
     args = ap.parse_args()
@@ -101,6 +103,11 @@ def main():
         mgs = [nb.Maglev(names, m) for _ in range(S)]
         lpm = nb.Lpm(routes["reference"] + routes["mixed"]) if cfg == "c5" else None
         sts = [torch.cuda.Stream(dev) for _ in range(S)]
+        recs = [torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) for _ in range(S)]
+        c3v = args.c3_variant
+        if cfg.startswith("c3") and c3v != "in_place":
+            classify_bytes = 84 if c3v == "records" else 72  # 64 + 6 descriptor + 2 backend (+ 12 record)
+            bytes_pkt = classify_bytes + 4
         outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
                      perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
                      counts=torch.empty(nbk + 1, dtype=torch.uint32, device=dev)) for _ in range(S)]
@@ -114,7 +121,8 @@ def main():
                                     defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream,
                                     stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])
             else:
-                mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, swap_macs=True,
+                mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
+                                swap_macs=c3v != "read_only", mac_out=recs[j] if c3v == "records" else None,
                                 defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream,
                                 stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])
 
@@ -146,7 +154,7 @@ def main():
         kus = float(kt.ms().mean()) * 1e3
         kt.close()
         mpps = BATCH * args.steps / elapsed / 1e6
-        line = {"config": cfg, "mpps": round(mpps, 1), "us_per_batch": round(elapsed / args.steps * 1e6, 2),
+        line = {"config": cfg + ("" if cfg == "c5" or c3v == "in_place" else f"_{c3v}"), "mpps": round(mpps, 1), "us_per_batch": round(elapsed / args.steps * 1e6, 2),
                 "streams": S, "batch_pkts": BATCH, "backends": nbk, "table_size": m,
                 "path_bytes_per_pkt": bytes_pkt, "path_gbps": round(mpps * bytes_pkt / 1e3, 1),
                 "classify_us": round(kus, 2), "classify_bytes_per_pkt": classify_bytes,
