@@ -830,7 +830,10 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 // everything global arrives by LDS-DMA: the descriptors of a tile (off[64], len[64]) issued four
 // tiles ahead, the packet windows of a tile from its descriptors three tiles ahead, and the per-packet
 // gather (tbl24 or LUT entry, 2 B per lane) one tile ahead — so iteration k hashes tile k+1 and
-// issues its gather, then finishes tile k, whose gather had a whole iteration to land.
+// issues its gather, then finishes tile k, whose gather had a whole iteration to land.  The chain's
+// second, dependent gather (tbl_long, routes longer than /24) is issued at the start of iteration k
+// and waited for after tile k+1's hash and prefetches, so it never drains them.  Opt-in
+// (NBG_STREAM_DESC): one block per CU holds all LDS, so several streams' kernels cannot co-run.
 //
 // vmcnt retires in issue order and hipcc does not count these loads, so the kernel keeps its own
 // wave-uniform count of issued VM operations (`seq`): each load group records the count after it,
@@ -840,7 +843,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 // stricter.
 // A 1- or 2-B LDS-DMA load still fills one dword per lane (measured: lane i's value at 4i), so the
 // u16 lengths and gathered entries take 4 B of LDS per lane.
-constexpr uint32_t kDescRing = 4;                   // descriptor slots per wave: tiles k+1 .. k+4
+constexpr uint32_t kDescRing = 4;                   // descriptor slots per wave: tiles k .. k+3, then k+4 into k's
 constexpr uint32_t kDescLds = 64u * 4u + 64u * 4u;  // off[64] then len[64] (dword per lane)
 constexpr uint32_t kGatherLds = 64u * 4u;           // one dword per lane, two tiles
 
