@@ -1,0 +1,39 @@
+"""CPU tests of bench.py's helpers that the GPU runs depend on: the rocprofv3 --pmc CSV reader that
+turns counter rows into per-launch bytes (only the classify kernels, in dispatch order, KB -> B),
+and the CPU inventory used to size the CPU baseline."""
+import csv
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_pmc_rows_filters_and_orders(tmp_path):
+    d = tmp_path / "pass" / "host" / "1234"
+    d.mkdir(parents=True)
+    rows = [
+        (7, "void nbg::(anonymous namespace)::classify_stream_kernel<true, true, 1>(nbg::ClassifyArgs)", "FETCH_SIZE", 3.0),
+        (3, "void nbg::(anonymous namespace)::classify_stream_kernel<true, true, 1>(nbg::ClassifyArgs)", "FETCH_SIZE", 1.5),
+        (5, "void nbg::(anonymous namespace)::group_kernel<2, 7>(nbg::GroupArgs)", "FETCH_SIZE", 99.0),
+        (6, "void nbg::(anonymous namespace)::classify_kernel<2, true, true, false, 2, 0, 256>(nbg::ClassifyArgs)",
+         "FETCH_SIZE", 2.0),
+        (8, "void nbg::(anonymous namespace)::classify_stream_kernel<true, true, 1>(nbg::ClassifyArgs)", "WRITE_SIZE", 9.0),
+    ]
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        for r in rows:
+            w.writerow(r)
+    got = bench._pmc_rows(str(tmp_path / "pass"), "FETCH_SIZE")
+    assert got == [1.5 * 1024, 2.0 * 1024, 3.0 * 1024]
+    assert bench._pmc_rows(str(tmp_path / "pass"), "WRITE_SIZE") == [9.0 * 1024]
+
+
+def test_cpu_inventory_is_sane():
+    affinity, quota, model = bench.cpu_inventory()
+    assert affinity >= 1
+    assert quota is None or quota > 0
+    assert isinstance(model, str) and model
