@@ -592,7 +592,11 @@ def run_rank(args) -> None:
                                 "group_kernel_avg_us": roof["group_kernel_avg_us"],
                                 "timing": "single-stream pass, HIP events around each classify launch (grouping "
                                           "deferred); `value` is the multi-stream rate, where the grouping of one "
-                                          "batch overlaps the classify of the next"}
+                                          "batch overlaps the classify of the next",
+                                "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts), "
+                                        "so the physical traffic is ~1.7x the 78 algorithmic bytes and this variant's "
+                                        "frac is capped near 0.40 by the measured read+rewrite ceiling (DESIGN.md "
+                                        "section 5); variants.read_only is north_star's parse + hash + lookup"}
         if variants:
             line["variants"] = variants
         line["cpu_baseline"] = cpu
