@@ -22,6 +22,7 @@ def pct(x, qs=(0, 10, 50, 90, 100)):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--group", action="store_true", help="with grouping (the kernel's per-unit histogram barriers)")
     args = ap.parse_args()
     import torch
 
@@ -42,7 +43,7 @@ def main():
         if variant == "records":
             kw["mac_out"] = rec
         for i in range(20):
-            mg.group_by(bufs[i % 8], n, group=False, backend=be, **kw)
+            mg.group_by(bufs[i % 8], n, group=args.group, backend=be, **kw)
         torch.cuda.synchronize()
         waves = 256 * 8
         raw = np.zeros(4096 * 12, dtype=np.uint64)
@@ -58,6 +59,17 @@ def main():
         print(f"   exit         {pct(us[:, 11])}")
         steady = np.diff(us[:, 2:10], axis=1)
         print(f"   tile interval (k -> k+1) median {np.median(steady):.2f} us, p90 {np.percentile(steady, 90):.2f}")
+        # where the exit spread comes from: per block (max over its waves), grouped by XCD (blocks
+        # are dealt round-robin to the 8 XCDs), and against the block's first-tile arrival
+        blk_exit = us[:, 11].reshape(256, 8).max(axis=1)
+        blk_t0 = us[:, 2].reshape(256, 8).max(axis=1)
+        xcd = np.arange(256) % 8
+        per_x = [blk_exit[xcd == x] for x in range(8)]
+        print("   exit by XCD (median / max):", " ".join(f"{np.median(e):.2f}/{e.max():.2f}" for e in per_x))
+        within = np.mean([e.max() - e.min() for e in per_x])
+        print(f"   block exit spread {blk_exit.max() - blk_exit.min():.2f} us; mean within-XCD spread {within:.2f} us; "
+              f"XCD median range {max(np.median(e) for e in per_x) - min(np.median(e) for e in per_x):.2f} us; "
+              f"corr(first tile, exit) {np.corrcoef(blk_t0, blk_exit)[0, 1]:.2f}")
     mg.close()
 
 
