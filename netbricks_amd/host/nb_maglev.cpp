@@ -8,6 +8,7 @@
 // JSON line with rx/tx/dropped counts and the per-group packet counts; --order writes the rx
 // index of every transmitted frame (one per line) for order checks.  --zero-copy 1 registers the
 // port's mempool (nbg_host_register), so the GPU reads and rewrites the frames in place over PCIe.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
@@ -55,15 +56,18 @@ int main(int argc, char** argv) {
       nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
     }
     nb::StandaloneScheduler sched;
+    sched.set_timed(true);
     auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch);
     // run until the capture is consumed and every group queue has drained
+    const auto t0 = std::chrono::steady_clock::now();
     for (int idle = 0; idle < 2 * static_cast<int>(names.size() + 2);) {
       const uint64_t before = pipe.tx->sent + pipe.groups->processed();
       sched.execute_round();
       const bool progress = pipe.tx->sent + pipe.groups->processed() != before;
       idle = (port->rx_done() && !progress) ? idle + 1 : 0;
     }
-    if (!tx.empty()) nb::write_pcap(tx, port->tx());
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!tx.empty()) port->write_tx(tx);
     if (!order.empty()) {
       FILE* f = std::fopen(order.c_str(), "w");
       for (size_t i : port->tx_index()) std::fprintf(f, "%zu\n", i);
@@ -71,10 +75,12 @@ int main(int argc, char** argv) {
     }
     if (zero_copy && pool.second) nb::check(nbg_host_unregister(pool.first, 0), "nbg_host_unregister");
     std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"would_panic\": %llu, \"backends\": %zu, "
-                "\"zero_copy\": %s}\n",
+                "\"zero_copy\": %s, \"seconds\": %.6f, \"mpps\": %.2f, \"group_by_seconds\": %.6f, "
+                "\"merge_send_seconds\": %.6f}\n",
                 port->rx_total(), static_cast<unsigned long long>(pipe.tx->sent),
                 static_cast<unsigned long long>(pipe.groups->dropped()),
-                static_cast<unsigned long long>(pipe.groups->would_panic()), names.size(), zero_copy ? "true" : "false");
+                static_cast<unsigned long long>(pipe.groups->would_panic()), names.size(), zero_copy ? "true" : "false",
+                secs, secs > 0 ? port->rx_total() / secs / 1e6 : 0.0, sched.task_seconds(0), sched.task_seconds(1));
   } catch (const nb::NbError& e) {
     std::fprintf(stderr, "nb_maglev: %s\n", e.what());
     return e.code == NBG_ENODEV ? 3 : 1;

@@ -19,6 +19,7 @@
 // order — exactly what GroupByProducer::execute (group_by.rs:43-55) does packet by packet.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -132,11 +133,25 @@ class StandaloneScheduler {
     return tasks_.size() - 1;
   }
   void execute_round() {
-    for (auto& t : tasks_) t->execute();
+    if (!timed_) {
+      for (auto& t : tasks_) t->execute();
+      return;
+    }
+    seconds_.resize(tasks_.size());
+    for (size_t i = 0; i < tasks_.size(); ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      tasks_[i]->execute();
+      seconds_[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
   }
+  // per-task wall time accumulated over execute_round() (for throughput breakdowns; off by default)
+  void set_timed(bool on) { timed_ = on; }
+  double task_seconds(size_t i) const { return i < seconds_.size() ? seconds_[i] : 0.0; }
 
  private:
   std::vector<std::shared_ptr<Executable>> tasks_;
+  std::vector<double> seconds_;
+  bool timed_ = false;
 };
 
 // ---- batches ------------------------------------------------------------------------------

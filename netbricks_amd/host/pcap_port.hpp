@@ -3,6 +3,7 @@
 // out the capture's frames in bursts; send() appends frames to the output capture.
 #pragma once
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -66,6 +67,7 @@ class PcapPort : public PacketRx, public PacketTx {
     mem_.assign(recs.size() * room_ + 4096, 0);
     base_ = mem_.data() + ((4096 - reinterpret_cast<uintptr_t>(mem_.data()) % 4096) % 4096);  // page-aligned
     uint8_t* base = base_;
+    size_t tx_room = 0;
     for (auto& r : recs) {
       auto m = std::make_unique<MBuf>();
       m->room = base + pool_.size() * room_;
@@ -74,7 +76,10 @@ class PcapPort : public PacketRx, public PacketTx {
       m->port_seq = pool_.size();
       ts_.push_back({r.ts_sec, r.ts_usec});
       pool_.push_back(std::move(m));
+      tx_room += 16 + r.data.size();
     }
+    tx_bytes_.assign(tx_room, 0);
+    tx_index_.reserve(pool_.size());
   }
   // the mempool's memory: every frame's data room lies in [data, data + bytes)
   std::pair<uint8_t*, size_t> mempool() { return {base_, pool_.size() * room_}; }
@@ -83,18 +88,36 @@ class PcapPort : public PacketRx, public PacketTx {
     while (n < cap && next_ < pool_.size()) pkts[n++] = pool_[next_++].get();
     return n;
   }
+  // Appends each frame, with its pcap record header, to one dump buffer (the pcap PMD's
+  // pcap_dump into a stdio buffer); write_tx() puts the buffer behind a pcap file header.
   uint32_t send(MBuf** pkts, uint32_t n) override {
+    // The buffer is sized and touched for one copy of the rx capture up front (outside any timed
+    // loop); sending more than that grows it.
+    size_t add = 0;
+    for (uint32_t i = 0; i < n; ++i) add += 16 + pkts[i]->data_len;
+    if (tx_used_ + add > tx_bytes_.size()) tx_bytes_.resize(std::max(2 * tx_bytes_.size(), tx_used_ + add));
+    uint8_t* out = tx_bytes_.data() + tx_used_;
     for (uint32_t i = 0; i < n; ++i) {
-      PcapRecord r;
-      r.data.assign(pkts[i]->data(), pkts[i]->data() + pkts[i]->data_len);
-      tx_.push_back(std::move(r));
+      const uint32_t len = pkts[i]->data_len;
+      const uint32_t rh[4] = {0, 0, len, len};
+      std::memcpy(out, rh, 16);
+      std::memcpy(out + 16, pkts[i]->data(), len);
+      out += 16 + len;
       tx_index_.push_back(pkts[i]->port_seq);
     }
+    tx_used_ += add;
     return n;
+  }
+  void write_tx(const std::string& path) const {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("cannot create " + path);
+    const uint32_t gh[6] = {0xA1B2C3D4u, 0x00040002u, 0, 0, 65535, 1 /* LINKTYPE_ETHERNET */};
+    std::fwrite(gh, 4, 6, f);
+    std::fwrite(tx_bytes_.data(), 1, tx_used_, f);
+    std::fclose(f);
   }
   bool rx_done() const { return next_ >= pool_.size(); }
   size_t rx_total() const { return pool_.size(); }
-  const std::vector<PcapRecord>& tx() const { return tx_; }
   const std::vector<size_t>& tx_index() const { return tx_index_; }  // rx position of each sent frame
 
  private:
@@ -104,7 +127,8 @@ class PcapPort : public PacketRx, public PacketTx {
   std::vector<std::unique_ptr<MBuf>> pool_;
   std::vector<std::pair<uint32_t, uint32_t>> ts_;
   size_t next_ = 0;
-  std::vector<PcapRecord> tx_;
+  std::vector<uint8_t> tx_bytes_;
+  size_t tx_used_ = 0;
   std::vector<size_t> tx_index_;
 };
 
