@@ -2115,7 +2115,10 @@ int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
   }();
   if (forced == kScanKernel || forced == kScanDirect) return forced;
   if (forced == kScanLds && group_lds(nbins, n_parts, kScanLds) <= 100 * 1024) return kScanLds;
-  return static_cast<size_t>(nbins) * n_parts <= 32 * 1024 ? kScanDirect : kScanKernel;
+#ifndef NBG_SCAN_DIRECT_MAX
+#define NBG_SCAN_DIRECT_MAX (32 * 1024)
+#endif
+  return static_cast<size_t>(nbins) * n_parts <= NBG_SCAN_DIRECT_MAX ? kScanDirect : kScanKernel;
 }
 
 int launch_group(const GroupArgs& a, int scan, void* stream) {

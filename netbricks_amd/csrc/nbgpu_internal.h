@@ -31,9 +31,15 @@ constexpr int kLoadPrio = NBG_LOAD_PRIO;  // s_setprio while a classify wave iss
 #define NBG_GBLOCK 512
 #endif
 constexpr int kGBlock = NBG_GBLOCK;  // group kernel threads per workgroup (8 waves: overlaps classify better)
-constexpr int kChunk = 4096;         // packets per group-kernel chunk
+#ifndef NBG_KCHUNK  // measurement builds only (tools/build_ab.sh): group-kernel chunk size
+#define NBG_KCHUNK 4096
+#endif
+#ifndef NBG_KMAXPARTS
+#define NBG_KMAXPARTS 256
+#endif
+constexpr int kChunk = NBG_KCHUNK;   // packets per group-kernel chunk
 constexpr int kGRounds = kChunk / kGBlock;  // group kernel rounds of 64 packets per wave per chunk
-constexpr uint32_t kMaxParts = 256;  // partitions per batch (part_pkts is a multiple of kChunk)
+constexpr uint32_t kMaxParts = NBG_KMAXPARTS;  // partitions per batch (part_pkts is a multiple of kChunk)
 constexpr uint32_t kMaxGroupBins = 1024;  // multisplit group kernel: n_backends + 1 <= 1024
 constexpr uint32_t kMaxWideBins = 32768;  // wide grouping path: n_backends <= 32767 (LUT sentinel bound,
                                           // test/maglev/src/nf.rs:46)

@@ -7,9 +7,10 @@ import csv
 
 
 def short(name):
-    for k in ("classify_kernel", "group_kernel", "scan_kernel", "hist_kernel"):
+    for k in ("classify_stream_desc_kernel", "classify_stream_kernel", "classify_kernel", "group_kernel",
+              "scan_kernel", "hist_kernel"):
         if k in name:
-            return k.replace("_kernel", "")
+            return "classify" if k.startswith("classify") else k.replace("_kernel", "")
     return name[:24]
 
 
