@@ -1511,6 +1511,9 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
 #else
 #define GPROBE(k)
 #endif
+#ifndef NBG_GABL  // diagnostic ablations (wrong results): bit 0 no partition-row reads, bit 1 no
+#define NBG_GABL 0  // multisplit ballots, bit 2 no perm stores
+#endif
 #ifndef NBG_GROUP_WAVES
 #define NBG_GROUP_WAVES 4  // waves per SIMD the group kernel is compiled for: <= 64 VGPRs, so a resident
                            // group block leaves the other streams' classify waves their registers
@@ -1558,7 +1561,9 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
     base[b] = 0;
     tot[b] = 0;
   }
-  if constexpr (SCAN == kScanDirect) {
+  if constexpr (SCAN == kScanDirect && (NBG_GABL & 1)) {
+    lds_sync();
+  } else if constexpr (SCAN == kScanDirect) {
     lds_sync();
     // L threads per row word, each summing a strided subset of the partition rows straight from
     // L2 (consecutive threads read consecutive words of one row: coalesced)
@@ -1732,6 +1737,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
       const uint32_t mv = valid ? ~0u : 0u;
       const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
       uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
+#if !(NBG_GABL & 2)
 #pragma unroll
       for (int bit = 0; bit < BITS; ++bit) {
         const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
@@ -1739,6 +1745,10 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
         elo &= ~(static_cast<uint32_t>(bb) ^ m);
         ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
       }
+#else  // every lane alone: counts under-counted, so every perm index stays inside its bin's range
+      elo &= lane < 32 ? 1u << lane : 0u;
+      ehi &= lane >= 32 ? 1u << (lane - 32) : 0u;
+#endif
       // every lane of a bin stores the same new count (no branch); lanes past the end use the
       // scratch slot
       const uint32_t slot = valid ? bin : nbins;
@@ -1804,7 +1814,11 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
 #ifdef NBG_GUARD  // diagnostic build: a store whose slot comes from inconsistent histograms is dropped
       if (tot[sbin[j]] + j >= a.n_pkts) continue;
 #endif
+#if !(NBG_GABL & 4)
       a.perm[tot[sbin[j]] + j] = sidx[j];
+#else
+      if (sidx[j] == 0xffffffffu) a.perm[0] = tot[sbin[j]];
+#endif
     }
   }
   zero_next();
