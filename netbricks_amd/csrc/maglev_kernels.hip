@@ -571,6 +571,33 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
       : "memory");
 }
 
+// The same with the streaming (non-temporal) policy, for packet windows (read once).  Measured on
+// classify_stream_kernel, 1M packets, one MI355X (tools/gpu_ab_ms.sh, profiles/r02_tile_nt_ab.txt):
+// one stream, read-only 14.6 -> 13.5 us, in place 27.5 -> 25.5, records 17.0 -> 16.6; three streams
+// with grouping, read-only 16.1 -> 15.8, in place neutral, records 17.8 -> 18.9 (slower).  So nt for
+// read-only and in place (NT = true), the default policy for records.  The LUT pieces keep the
+// default policy: every CU of an XCD re-reads them from L2.
+#ifndef NBG_TILE_NT  // 0: default policy everywhere (A/B builds)
+#define NBG_TILE_NT 1
+#endif
+template <bool NT>
+__device__ __forceinline__ void glds16_tile(const void* src, uint32_t lds_base) {
+  if constexpr (NT && NBG_TILE_NT) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(src), "s"(lds_base)
+        : "memory");
+  } else {
+    glds16(src, lds_base);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
@@ -608,7 +635,7 @@ __device__ __forceinline__ void wait_vm_n(uint32_t n) {
 // covers packets 16k..16k+15.  48-B rows: lane l < 48 fetches chunk l % 3 of packet 16k + l / 3;
 // 64-B rows: lane l fetches chunk l % 4 of packet 16k + l / 4 (1 KiB contiguous).  Lanes past the
 // batch end fetch the batch base (their rows are never read).
-template <uint32_t kRow>
+template <uint32_t kRow, bool NT>
 __device__ __forceinline__ void issue_tile(const ClassifyArgs& a, uint32_t tb, uint32_t buf, uint32_t lane) {
   constexpr uint32_t kCh = kRow / 16u;
   if (kCh == 4u || lane < 16u * kCh) {
@@ -617,7 +644,7 @@ __device__ __forceinline__ void issue_tile(const ClassifyArgs& a, uint32_t tb, u
     for (uint32_t k = 0; k < 4; ++k) {
       const uint32_t p = tb + k * 16u + pk;
       const uint8_t* src = p < a.n_pkts ? a.pkts + static_cast<size_t>(p) * a.stride + ch * 16u : a.pkts;
-      glds16(src, buf + k * (16u * kRow));
+      glds16_tile<NT>(src, buf + k * (16u * kRow));
     }
   }
 }
@@ -758,7 +785,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // make the wait for it stricter (vmcnt counts stores too)
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
   for (uint32_t k = 0; k < first; ++k) {
-    issue_tile<kRow>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
+    issue_tile<kRow, MODE != 2>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
     seq += 4;
     (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
   }
@@ -789,7 +816,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     uint32_t sN = 0;
     if (k + kRing < nt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue_tile<kRow>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
+      issue_tile<kRow, MODE != 2>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
       seq += 4;
       sN = seq;
     }
@@ -960,7 +987,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
       for (uint32_t j = 0; j < 4; ++j) {
         const uint32_t q = j * 16u + pk;
         const uint8_t* src = (tb + q < a.n_pkts && (off[j] & 15u) == 0) ? a.pkts + off[j] + ch * 16u : a.pkts;
-        glds16(src, buf + j * (16u * kRow));
+        glds16_tile<MODE != 2>(src, buf + j * (16u * kRow));
       }
     }
     if (!(NBG_DABL & 2)) seq += 4;

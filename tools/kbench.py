@@ -84,16 +84,17 @@ def main():
                  torch.empty(args.nb + 1, dtype=torch.uint32, device=dev),
                  torch.empty(n * 12, dtype=torch.uint8, device=dev)) for _ in range(S)]
 
-        def ms(i, S=S, mgs=mgs, sts=sts, outs=outs, mac=True, group=True, scatter=True):
+        def ms(i, S=S, mgs=mgs, sts=sts, outs=outs, mac=True, group=True, scatter=True, swap=True):
             j = i % S
             be, pm, ct, mo = outs[j]
             mgs[j].group_by(bufs[i % 8], n, backend=be, perm=pm if scatter else None, counts=ct, group=group,
-                            scatter=scatter,
+                            scatter=scatter, swap_macs=swap,
                             mac_out=mo if mac else None, stream=sts[j].cuda_stream, **kw(i))
 
         extra[f"full path l2 mac_out x{S} streams"] = ms
         extra[f"full path l2 inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False))
         extra[f"classify only inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False, group=False))
+        extra[f"full path l2 noswap x{S} streams"] = (lambda i, f=ms: f(i, mac=False, swap=False))
         extra[f"classify only mac_out x{S} streams"] = (lambda i, f=ms: f(i, group=False))
         extra[f"counts only inplace x{S} streams"] = (lambda i, f=ms: f(i, mac=False, scatter=False))
         extra[f"_keep{S}"] = (mgs, sts, outs)
