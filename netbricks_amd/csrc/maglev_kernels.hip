@@ -741,43 +741,6 @@ __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const u
   return bin;
 }
 
-// Dynamic tail (round 2, session 3).  With static interleaved units every block has the same work,
-// but blocks whose first tiles queue behind the startup burst finish up to 2 us (read-only) / 4.7 us
-// (in place) after the first ones (profiles/r02_stream_kernel_timeline_nt.txt: corr(first tile,
-// exit) 0.6-0.85).  So the last kDynRounds units of every block go into 8 pools (pool c = every 8th
-// of those units, claimed by the blocks b with b % 8 == c: one XCD's blocks when dispatch deals
-// blocks round-robin over the 8 XCDs, which is only a speed matter) and blocks claim them one unit at
-// a time from the pool's device-scope counter.  A claim for position p is issued at iteration p - 5
-// by wave (p - 5) % 8, before that wave's tile p - 3 goes out, so waiting for tile p - 3 also covers
-// the claim; at iteration p - 3 that wave publishes the unit (or kNoUnit) in an LDS queue, and the
-// unit barrier of that iteration makes it visible before tile p is issued at iteration p - 2.  The
-// first failed claim ends the block at that position + 3 (claims for the two positions after it may
-// already be out, and may still win units: they are processed).
-#ifndef NBG_DYN  // rounds of units per block claimed dynamically (0: static assignment only)
-#define NBG_DYN 0
-#endif
-constexpr uint32_t kDynRounds = NBG_DYN;
-constexpr uint32_t kClaimLead = 5;
-constexpr uint32_t kNoUnit = 0xffffffffu;
-constexpr uint32_t kClaimStride = 32;  // counters 128 B apart
-
-// One returning device-scope add of 1 by lane 0 (exec narrowed inside the asm, so the result register
-// is not the value of a divergent branch for the compiler): the caller reads it only after a vmcnt
-// wait that covers this operation.
-__device__ __forceinline__ uint32_t claim_issue(uint32_t* counter) {
-  uint32_t ret;
-  uint64_t save;
-  asm volatile(
-      "s_mov_b64 %1, exec\n\t"
-      "s_mov_b64 exec, 1\n\t"
-      "global_atomic_add %0, %2, %3, off sc0\n\t"
-      "s_mov_b64 exec, %1"
-      : "=&v"(ret), "=&s"(save)
-      : "v"(counter), "v"(1u)
-      : "memory");
-  return ret;
-}
-
 // MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
 template <bool F4, bool HIST, int MODE>
 __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a) {
@@ -790,7 +753,6 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   uint8_t* ring = smem + kLutLds + wave * (kRing * kTileLds);
   const uint32_t hstride = (nbins + 3) & ~3u;
   uint32_t* hist_base = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);
-  uint32_t* queue = hist_base + 2 * hstride;  // [8] units of dynamic positions, [8] the first failed position
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
   const uint32_t n_tiles = (a.n_pkts + 63u) >> 6;
@@ -802,19 +764,8 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // wave behind one LDS-only barrier; a unit (W tiles = 512 packets) never straddles a partition.
   const uint32_t n_units = (n_tiles + kStreamW - 1) / kStreamW;
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t full = n_units / G;
-  const bool dyn = HIST && kDynRounds > 0 && a.claim != nullptr && (G & 7u) == 0 && full >= kDynRounds + kClaimLead;
-  // static positions of this block (block-uniform); with dyn the units from S*G on are pooled
-  const uint32_t S = dyn ? full - kDynRounds : (b < n_units ? (n_units - b + G - 1) / G : 0u);
-  const uint32_t pc = b & 7u;
-  const uint32_t pool_n = dyn ? n_units - S * G : 0u;
-  const uint32_t pool_sz = pool_n > pc ? (pool_n - pc + 7u) >> 3 : 0u;
-  const uint32_t cap = S + pool_sz + 8u;  // positions never reach this (safety bound)
-  auto unit_at = [&](uint32_t k) -> uint32_t {
-    if (k < S) return b + k * G;
-    if (!dyn) return kNoUnit;
-    return queue[k & 7u];
-  };
+  const uint32_t nt = b < n_units ? (n_units - b + G - 1) / G : 0u;  // units of this block (block-uniform)
+  auto tile_of = [&](uint32_t k) { return (b + k * G) * kStreamW + wave; };
   uint32_t* hist = hist_base;  // [2][hstride]
 
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
@@ -824,88 +775,56 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 #else
   const uint32_t pieces = a.lut_lds_bytes >> 10;
 #endif
-  const uint32_t first = min(S, static_cast<uint32_t>(kRing));  // dyn: S >= kClaimLead > kRing
+  const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
   // the LUT pieces first, then the first tiles (measured: tiles first, or the LUT through registers
   // off the LDS-DMA path, are both ~0.8 us slower per launch)
   for (uint32_t q = wave; q < pieces; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
-  // VM operations this wave issued after the LUT pieces (tile loads, its claims, and a lower bound
-  // of its stores): waiting for tile k is vmcnt(seq - its count), so the stores issued after a tile
-  // do not make the wait for it stricter (vmcnt counts stores too)
+  // VM operations this wave issued after the LUT pieces (tile loads, and a lower bound of its
+  // stores): waiting for tile k is vmcnt(seq - its count), so the stores issued after a tile do not
+  // make the wait for it stricter (vmcnt counts stores too)
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
   for (uint32_t k = 0; k < first; ++k) {
-    issue_tile<kRow, MODE != 2>(a, (unit_at(k) * kStreamW + wave) * 64u, ring_lds + k * kTileLds, lane);
+    issue_tile<kRow, MODE != 2>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
     seq += 4;
     (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
   }
   if constexpr (HIST)
     for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
-  if (dyn) {
-    if (tid < 16) queue[tid] = kNoUnit;
-    // the next launch's counters (this handle's other set): written through to memory
-    if (b == 0 && tid < 8) __hip_atomic_store(a.claim_next + tid * kClaimStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
   // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
   // makes every wave's pieces visible to every wave
   wait_tile(first);
   lds_sync();
   SPROBE(1)
 
-  uint32_t claim_ret = 0, claim_pos = kNoUnit;  // this wave's claim in flight (at most one)
-  for (uint32_t k = 0;; ++k) {
-    if (k >= S) {
-      if (!dyn || k >= cap) break;
-      const uint32_t f = queue[8];
-      if (f != kNoUnit && k >= f + 3u) break;
-    }
-    const uint32_t u = unit_at(k);
+  for (uint32_t k = 0; k < nt; ++k) {
+    const uint32_t t = tile_of(k);
+    const uint32_t tb = t * 64u;
 #if NBG_SEQWAIT
     wait_vm_n(seq - sA);  // kStreamAhead tiles (and their stores) stay in flight
 #else
-    wait_tile(min(S - 1u - k, static_cast<uint32_t>(kStreamAhead)));
+    wait_tile(min(nt - 1u - k, static_cast<uint32_t>(kStreamAhead)));
 #endif
     SPROBE(2 + k)
-    if (dyn && claim_pos == k + 3u) {
-      // the claim issued at iteration k - 2 was issued before tile k's loads: covered by the wait above
-      uint32_t j;
-      asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(j) : "v"(claim_ret));
-      const uint32_t nu = j < pool_sz ? S * G + pc + 8u * j : kNoUnit;
-      if (lane == 0) {
-        queue[claim_pos & 7u] = nu;
-        if (nu == kNoUnit && queue[8] == kNoUnit) queue[8] = claim_pos;
-      }
-      claim_pos = kNoUnit;
-    }
-    const uint32_t t = u * kStreamW + wave;
-    const uint32_t tb = t * 64u;
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
-    const bool valid = u != kNoUnit && t < n_tiles &&
-                       stream_classify<F4, MODE>(a, lut, ring + (k % kRing) * kTileLds + lane * kRow, p, bin, slow);
-    if (dyn && wave == k % kStreamW && k + kClaimLead >= S) {
-      // claim the unit of position k + 5 unless the pool ran dry at least three positions earlier
-      const uint32_t q = k + kClaimLead, f = queue[8];
-      if (q < cap && (f == kNoUnit || q < f + 3u)) {
-        claim_ret = claim_issue(a.claim + pc * kClaimStride);
-        claim_pos = q;
-        ++seq;
-      }
-    }
+    const bool valid = t < n_tiles && stream_classify<F4, MODE>(a, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+                                                                 p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
-    const uint32_t u2 = unit_at(k + kRing);
-    if (u2 != kNoUnit) {
+    uint32_t sN = 0;
+    if (k + kRing < nt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue_tile<kRow, MODE != 2>(a, (u2 * kStreamW + wave) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
+      issue_tile<kRow, MODE != 2>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
       seq += 4;
+      sN = seq;
     }
-    const uint32_t sN = seq;  // no tile: waiting for it waits for everything issued before (stricter)
     if (valid) {
       bin = stream_finish<F4>(a, lut, p, bin, slow);
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
-    if (u != kNoUnit && t < n_tiles) ++seq;  // the backend store (lane 0 has a packet)
+    if (t < n_tiles) ++seq;  // the backend store (lane 0 has a packet)
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -918,9 +837,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       // partition row and zeroes it.  The next barrier (unit k + 1) orders that before unit k + 2
       // counts into the same buffer.
       lds_sync();
-      if (wave == k % kStreamW && u != kNoUnit) {
+      if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
-        stream_flush<HIST>(a, h, nbins, (u * kStreamW * 64u) / a.part_pkts, lane);
+        stream_flush<HIST>(a, h, nbins, ((b + k * G) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
   }
@@ -2054,7 +1973,7 @@ size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
 size_t stream_lds(uint32_t nb, int mode) {
   const size_t hwords = 2 * (((nb + 1) + 3) & ~3u);
   const size_t tile = 64u * (mode == 1 ? row_of<1>() : row_of<0>());
-  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + hwords * 4u + 16u * 4u;  // + the claim queue
+  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + hwords * 4u;
 }
 
 int stream_waves_per_block() { return kStreamW; }

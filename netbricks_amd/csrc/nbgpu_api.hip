@@ -68,8 +68,6 @@ struct nbg_maglev {
   uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
   uint32_t* d_bin_base = nullptr;     // [nb+1]            (wide grouping path)
   uint8_t* d_sink = nullptr;          // [1 KiB] stores of idle lanes (descriptor streaming kernel)
-  uint32_t* d_claim = nullptr;        // [2][8 x 32] unit-claim counters of the streaming kernel (ping-pong)
-  uint32_t claim_parity = 0;
   uint32_t parity = 0;
   uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
@@ -221,7 +219,6 @@ void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_totals);
   (void)hipFree(h->d_bin_base);
   (void)hipFree(h->d_sink);
-  (void)hipFree(h->d_claim);
   (void)hipFree(h->d_counts);
   h->d_part_hist = nullptr;
   h->d_part_graph = nullptr;
@@ -229,7 +226,6 @@ void free_scratch(nbg_maglev* h) {
   h->d_totals = nullptr;
   h->d_bin_base = nullptr;
   h->d_sink = nullptr;
-  h->d_claim = nullptr;
   h->d_counts = nullptr;
 }
 
@@ -284,12 +280,10 @@ int upload(nbg_maglev* h) {
   NBG_HIP(hipMalloc(&h->d_totals, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_bin_base, nbins * sizeof(uint32_t)));
   NBG_HIP(hipMalloc(&h->d_sink, 1024));
-  NBG_HIP(hipMalloc(&h->d_claim, kClaimBytes));
   NBG_HIP(hipMalloc(&h->d_counts, nbins * sizeof(uint32_t)));
   SetupStream st;  // complete before the handle is returned: any caller stream may use it next
   (void)st.h2d(h->d_lut, buf.data(), h->lut_alloc);
   (void)st.zero(h->d_part_hist, 2 * kMaxParts * nbins * sizeof(uint32_t));
-  (void)st.zero(h->d_claim, kClaimBytes);
   NBG_HIP(st.finish());  // reports the first failure of the sequence
   if (const char* e = std::getenv("NBG_TPW")) {
     const int v = std::atoi(e);
@@ -677,12 +671,6 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
     if (capturing && a.part_hist)
       NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
-    if (a.part_hist && !capturing) {
-      // this launch claims from one counter set and zeroes the other for the next streaming launch
-      a.claim = h->d_claim + h->claim_parity * (kClaimBytes / 8);
-      a.claim_next = h->d_claim + (h->claim_parity ^ 1u) * (kClaimBytes / 8);
-      h->claim_parity ^= 1u;
-    }
     rc = launch_classify_stream(a, h->cus, stream);
   } else if (d_off && d_len && a.win_owned && !lds && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
              use_stream_desc(h, n_pkts, flags, lpm != nullptr, lpm || !a.swap ? 0 : (a.mac_out ? 2 : 1))) {

@@ -39,8 +39,7 @@ constexpr int kGBlock = NBG_GBLOCK;  // group kernel threads per workgroup (8 wa
 #endif
 constexpr int kChunk = NBG_KCHUNK;   // packets per group-kernel chunk
 constexpr int kGRounds = kChunk / kGBlock;  // group kernel rounds of 64 packets per wave per chunk
-constexpr uint32_t kMaxParts = NBG_KMAXPARTS;
-constexpr size_t kClaimBytes = 2 * 8 * 32 * sizeof(uint32_t);  // streaming kernel: two sets of 8 counters 128 B apart  // partitions per batch (part_pkts is a multiple of kChunk)
+constexpr uint32_t kMaxParts = NBG_KMAXPARTS;  // partitions per batch (part_pkts is a multiple of kChunk)
 constexpr uint32_t kMaxGroupBins = 1024;  // multisplit group kernel: n_backends + 1 <= 1024
 constexpr uint32_t kMaxWideBins = 32768;  // wide grouping path: n_backends <= 32767 (LUT sentinel bound,
                                           // test/maglev/src/nf.rs:46)
@@ -75,11 +74,6 @@ struct ClassifyArgs {
   uint16_t* gate;
   uint32_t* idx_out;        // NBG_LUT_TILED: per-packet LUT index (0xffffffff = would panic)
   uint8_t* sink;            // descriptor streaming kernel: 1 KiB scratch for stores of lanes with none
-  // streaming kernel, dynamic tail (NBG_DYN): 8 unit-claim counters (one per 128-B line) of this
-  // launch, zero at launch start, and the other set of the handle's pair, zeroed by this launch for
-  // the next one.  nullptr: static assignment only.
-  uint32_t* claim;
-  uint32_t* claim_next;
 };
 
 // NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
