@@ -49,6 +49,8 @@ BATCH = 1 << 20
 SLOT = 64
 FRAME = 60
 N_BATCHES = 8
+MULTI_K = 4        # batches per launch of the multi-batch variants
+MULTI_STREAMS = 2  # their streams (distinct batch groups in flight)
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet of the classify kernel per variant:
 #   in place: 64 B packet read + 12 B MAC write + 2 B backend write
@@ -477,6 +479,66 @@ def run_rank(args) -> None:
         return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
                 "frac": round(ach / HBM_PEAK_GBPS, 4), "group_kernel_avg_us": round(g_ms.mean() * 1e3, 2)}
 
+    # ---- several batches per launch (nbg_maglev_classify_device_multi): MULTI_K batches of 1M in
+    #      one streaming-classify launch and one group launch, each batch with its own outputs
+    m_arrs = {}
+    if gpu and world == 1 and not args.no_variants and N_BATCHES % MULTI_K == 0:
+        from netbricks_amd._lib import NbgBatch, lib as clib
+        m_outs = [(torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                   torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(N_BATCHES)]
+        for g0 in range(N_BATCHES // MULTI_K):
+            arr = (NbgBatch * MULTI_K)()
+            for q in range(MULTI_K):
+                be, pm, ct = m_outs[g0 * MULTI_K + q]
+                arr[q] = NbgBatch(dbufs[g0 * MULTI_K + q].data_ptr(), BATCH, be.data_ptr(), pm.data_ptr(), ct.data_ptr(),
+                                  None)
+            m_arrs[g0] = arr
+
+    def mcall(i, variant, stream, defer=False, j=0):
+        flags = (1 if variant == "in_place" else 0) | (0x10 if defer else 0)  # NBG_SWAP_MACS, NBG_DEFER_GROUP
+        rc = clib.nbg_maglev_classify_device_multi(mgs[j]._h, m_arrs[i % len(m_arrs)], MULTI_K, SLOT, FRAME, flags,
+                                                   stream)
+        if rc:
+            raise RuntimeError(f"nbg_maglev_classify_device_multi: {rc}")
+
+    def multi_pass(variant, calls, warmup):
+        """Whole-job rate with MULTI_K batches per call on MULTI_STREAMS streams (distinct batch
+        groups in flight), then the multi classify kernel alone (events, grouping deferred)."""
+        ms = min(MULTI_STREAMS, len(m_arrs), args.streams)
+        for i in range(warmup):
+            mcall(i, variant, streams[i % ms].cuda_stream, j=i % ms)
+        sync_all()
+        start_ev = torch.cuda.Event()
+        start_ev.record(torch.cuda.current_stream(dev))
+        for st in streams[:ms]:
+            st.wait_event(start_ev)
+        t1 = time.perf_counter()
+        for i in range(calls):
+            mcall(i, variant, streams[i % ms].cuda_stream, j=i % ms)
+        sync_all()
+        el = time.perf_counter() - t1
+        st = streams[0]
+        kt = KernelTimer(calls)
+        for i in range(calls):
+            kt.start(i, st.cuda_stream)
+            mcall(i, variant, st.cuda_stream, defer=True)
+            kt.stop(i, st.cuda_stream)
+            mgs[0].finish_group(st.cuda_stream)
+        sync_all()
+        c_ms = kt.ms()
+        kt.close()
+        for m in mgs:
+            m.check()
+        ach = MULTI_K * BATCH * CLASSIFY_BYTES[variant] / (c_ms.mean() / 1e3) / 1e9
+        return {"value": round(MULTI_K * BATCH * calls / el / 1e6, 1), "unit": "Mpps",
+                "ms_per_batch": round(el / (calls * MULTI_K) * 1e3, 5), "batches_per_launch": MULTI_K,
+                "streams": ms, "classify_bytes_per_pkt": CLASSIFY_BYTES[variant],
+                "pkts_per_launch": MULTI_K * BATCH, "avg_launch_us": round(c_ms.mean() * 1e3, 2),
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "what": f"{MULTI_K} batches of 1M (one per RX-queue pipeline) per launch of the streaming classify "
+                        "kernel and one group launch (nbg_maglev_classify_device_multi); every batch keeps its own "
+                        "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
+
     if args.pmc_child:  # under rocprofv3 --pmc: each variant's launches in a fixed order
         for v in PMC_VARIANTS:
             for i in range(PMC_WARMUP + PMC_STEPS):
@@ -550,6 +612,10 @@ def run_rank(args) -> None:
                                            "+ grouping, same streams")
             variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + grouping, "
                                              "same streams")
+            if m_arrs:
+                calls = max(args.steps // MULTI_K, 10)
+                for v in ("read_only", "in_place"):
+                    variants[f"{v}_multi{MULTI_K}"] = multi_pass(v, calls, max(args.warmup // MULTI_K, 3))
 
     if rank == 0:
         cpu = None

@@ -125,6 +125,32 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
                                   uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
                                   void* stream);
 
+/*
+ * Several device-resident batches in one launch of each kernel: what NetBricks does with the
+ * batches of several RX queues, one pipeline each (scheduler/context.rs:241-255), when they are
+ * classified together.  Every batch keeps its own outputs, exactly as if it were passed alone to
+ * nbg_maglev_classify_device_ex with the same stride / fixed_len / flags: backend[], the MAC swap
+ * (in place, or records in d_mac_out), and its own perm / counts (grouped per batch, never across
+ * batches).  Fused (one streaming-classify launch + one group launch over all batches) for fixed
+ * 64-B-aligned slots (stride % 16 == 0, stride >= 64, fixed_len >= 48, 16-B aligned d_pkts), at
+ * most 255 backends, M <= 65537 and at least 262144 packets in all; otherwise the batches are run
+ * one after another through nbg_maglev_classify_device_ex on `stream`.  1 <= n_batches <=
+ * NBG_MAX_MULTI.  Flags: NBG_SWAP_MACS, and NBG_DEFER_GROUP on the fused path (nbg_maglev_finish_group
+ * then launches the one group kernel of all batches); others are NBG_EINVAL.
+ * Either every batch has d_perm (or d_counts) or none has.
+ */
+#define NBG_MAX_MULTI 8u
+typedef struct nbg_batch {
+  uint8_t* d_pkts;
+  uint64_t n_pkts;
+  uint16_t* d_backend;
+  uint32_t* d_perm;    /* nullable */
+  uint32_t* d_counts;  /* nullable unless d_perm set (then n_backends + 1 u32) */
+  uint8_t* d_mac_out;  /* nullable: 12-B swapped-MAC records instead of the in-place swap */
+} nbg_batch;
+int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, uint32_t n_batches, uint32_t stride,
+                                     uint16_t fixed_len, uint32_t flags, void* stream);
+
 /* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP on
  * `stream` (which must be ordered after that classify).  No-op when nothing is pending. */
 int nbg_maglev_finish_group(nbg_maglev* h, void* stream);

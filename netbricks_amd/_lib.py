@@ -31,11 +31,21 @@ NBG_DEFER_GROUP = 0x10
 NBG_LUT_TILED = 0x20
 NBG_STREAM_DESC = 0x40
 NBG_HOST_SLOTS = 3
+NBG_MAX_MULTI = 8
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
 # every symbol include/nbgpu.h declares: name -> (restype, argtypes)
 _P = C.c_void_p
+
+
+class NbgBatch(C.Structure):
+    """struct nbg_batch (include/nbgpu.h): one batch of nbg_maglev_classify_device_multi."""
+    _fields_ = [("d_pkts", C.c_void_p), ("n_pkts", C.c_uint64), ("d_backend", C.c_void_p),
+                ("d_perm", C.c_void_p), ("d_counts", C.c_void_p), ("d_mac_out", C.c_void_p)]
+
+
+
 SIGNATURES = {
     "nbg_maglev_create": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_uint64,
                                     C.c_int, C.POINTER(_P)]),
@@ -49,6 +59,7 @@ SIGNATURES = {
                                              _P, _P, _P, _P]),
     "nbg_maglev_classify_device_ex": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64, C.c_uint32,
                                                 _P, _P, _P, _P, _P]),
+    "nbg_maglev_classify_device_multi": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint32, _P]),
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
@@ -82,7 +93,11 @@ def _load() -> C.CDLL:
             "(there is no CPU fallback for the Maglev path)")
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if os.environ.get("NBG_LIB_OVERRIDE"):  # an older diagnostic build (A/B timing)
+                continue
+            raise ImportError(f"{LIB_PATH}: missing {name}")
         fn.restype = res
         fn.argtypes = args
     return lib

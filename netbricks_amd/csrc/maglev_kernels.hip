@@ -742,8 +742,11 @@ __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const u
 }
 
 // MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
+// sb: the batches of this launch (one for nbg_maglev_classify_device; up to kMaxMulti for
+// nbg_maglev_classify_device_multi).  `a` carries what they share; per unit, the unit's batch
+// supplies pkts, n_pkts, backend, mac_out and part_hist (a view of `a`).
 template <bool F4, bool HIST, int MODE>
-__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a) {
+__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a, StreamBatches sb) {
   constexpr uint32_t kRow = row_of<MODE>(), kTileLds = 64u * kRow;
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -755,17 +758,32 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   uint32_t* hist_base = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
-  const uint32_t n_tiles = (a.n_pkts + 63u) >> 6;
   SPROBE(0)
   // Interleaved units: unit u = tiles [u*W, u*W + W), one per wave; block b takes units b, b + G,
   // b + 2G, ...  At any moment the grid reads consecutive units: one sequential sweep of the batch
   // (contiguous per-wave runs read ~3k streams at a fixed stride and measured 10 % slower:
   // HBM channel imbalance).  The block's histogram is double-buffered per unit and flushed by one
   // wave behind one LDS-only barrier; a unit (W tiles = 512 packets) never straddles a partition.
-  const uint32_t n_units = (n_tiles + kStreamW - 1) / kStreamW;
+  const uint32_t n_units = sb.unit_base[sb.n];
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t nt = b < n_units ? (n_units - b + G - 1) / G : 0u;  // units of this block (block-uniform)
-  auto tile_of = [&](uint32_t k) { return (b + k * G) * kStreamW + wave; };
+  // position k: global unit b + k*G; its batch j (scalar search, block-uniform) and the unit's
+  // first packet within the batch
+  auto batch_of = [&](uint32_t u) {
+    uint32_t j = 0;
+    while (j + 1 < sb.n && u >= sb.unit_base[j + 1]) ++j;
+    return j;
+  };
+  auto view = [&](uint32_t j) {
+    ClassifyArgs v = a;
+    v.pkts = sb.pkts[j];
+    v.n_pkts = sb.n_pkts[j];
+    v.backend = sb.backend[j];
+    v.mac_out = sb.mac_out[j];
+    v.part_hist = sb.part_hist[j];
+    return v;
+  };
+  auto first_pkt = [&](uint32_t u, uint32_t j) { return ((u - sb.unit_base[j]) * kStreamW + wave) * 64u; };
   uint32_t* hist = hist_base;  // [2][hstride]
 
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
@@ -785,7 +803,8 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // make the wait for it stricter (vmcnt counts stores too)
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
   for (uint32_t k = 0; k < first; ++k) {
-    issue_tile<kRow, MODE != 2>(a, tile_of(k) * 64u, ring_lds + k * kTileLds, lane);
+    const uint32_t u = b + k * G, j = batch_of(u);
+    issue_tile<kRow, MODE != 2>(view(j), first_pkt(u, j), ring_lds + k * kTileLds, lane);
     seq += 4;
     (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
   }
@@ -798,8 +817,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   SPROBE(1)
 
   for (uint32_t k = 0; k < nt; ++k) {
-    const uint32_t t = tile_of(k);
-    const uint32_t tb = t * 64u;
+    const uint32_t u = b + k * G, j = batch_of(u);
+    const ClassifyArgs aj = view(j);
+    const uint32_t tb = first_pkt(u, j);
 #if NBG_SEQWAIT
     wait_vm_n(seq - sA);  // kStreamAhead tiles (and their stores) stay in flight
 #else
@@ -809,22 +829,23 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
-    const bool valid = t < n_tiles && stream_classify<F4, MODE>(a, lut, ring + (k % kRing) * kTileLds + lane * kRow,
-                                                                 p, bin, slow);
+    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+                                                                    p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
     uint32_t sN = 0;
     if (k + kRing < nt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue_tile<kRow, MODE != 2>(a, tile_of(k + kRing) * 64u, ring_lds + (k % kRing) * kTileLds, lane);
+      const uint32_t u2 = u + kRing * G, j2 = batch_of(u2);
+      issue_tile<kRow, MODE != 2>(view(j2), first_pkt(u2, j2), ring_lds + (k % kRing) * kTileLds, lane);
       seq += 4;
       sN = seq;
     }
     if (valid) {
-      bin = stream_finish<F4>(a, lut, p, bin, slow);
+      bin = stream_finish<F4>(aj, lut, p, bin, slow);
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
-    if (t < n_tiles) ++seq;  // the backend store (lane 0 has a packet)
+    if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -839,7 +860,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       lds_sync();
       if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
-        stream_flush<HIST>(a, h, nbins, ((b + k * G) * kStreamW * 64u) / a.part_pkts, lane);
+        stream_flush<HIST>(aj, h, nbins, ((u - sb.unit_base[j]) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
   }
@@ -1547,16 +1568,29 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
 #endif
 // BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
 template <int SCAN, int BITS>
-__global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupArgs a) {
+// Blocks [j * gm.per, j * gm.per + g[j].n_parts) group batch j (a single batch: j = 0, c = blockIdx.x).
+__global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMulti gm) {
 #ifdef NBG_GPROBE
   uint64_t gpt[12] = {};
 #endif
   extern __shared__ __align__(16) uint32_t gs[];
   __shared__ uint32_t s_wave[kGBlock / 64];
   constexpr uint32_t kW = kGBlock / 64;  // waves
+  const uint32_t bj = blockIdx.x / gm.per;
+  const GroupArgs a = gm.g[bj];
   const uint32_t nbins = a.nb + 1;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-  const uint32_t c = blockIdx.x;
+  const uint32_t c = blockIdx.x - bj * gm.per;  // partition of batch bj
+  // The next call accumulates into the other histogram buffer: every block of the grid zeroes a
+  // slice of it, last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the
+  // first wait for a backend load would also wait for them (the counter retires in issue order).
+  auto zero_next = [&] {
+    for (uint32_t i = blockIdx.x * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
+  };
+  if (c >= a.n_parts) {  // a smaller batch of a multi-batch launch
+    zero_next();
+    return;
+  }
   GPROBE(0)
 #ifdef NBG_GROUP_EMPTY  // measurement build: the launch and its stream boundary only
   return;
@@ -1732,12 +1766,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupAr
   }
   lds_sync();
   GPROBE(3)
-  // The next call accumulates into the other histogram buffer: every block zeroes a slice of it,
-  // last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the first wait
-  // for a backend load would also wait for them (the counter retires in issue order).
-  auto zero_next = [&] {
-    for (uint32_t i = c * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
-  };
   if (!a.perm) {
     zero_next();
     return;
@@ -1906,7 +1934,7 @@ int launch_mode(const ClassifyArgs& a, bool hist, int grid, size_t lds, hipStrea
 }
 
 template <bool F4, bool HIST>
-int launch_stream_mode(const ClassifyArgs& a, int mode, int grid, size_t lds, hipStream_t s) {
+int launch_stream_mode(const ClassifyArgs& a, const StreamBatches& sb, int mode, int grid, size_t lds, hipStream_t s) {
   auto fn = mode == 1 ? classify_stream_kernel<F4, HIST, 1>
                       : (mode == 2 ? classify_stream_kernel<F4, HIST, 2> : classify_stream_kernel<F4, HIST, 0>);
   static bool attr_set[2][2][3] = {};
@@ -1916,7 +1944,7 @@ int launch_stream_mode(const ClassifyArgs& a, int mode, int grid, size_t lds, hi
       return set_error(NBG_EIO, "streaming classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
     attr_set[F4][HIST][mode] = true;
   }
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a, sb);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "streaming classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -1992,14 +2020,29 @@ int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, 
   return wide_lut ? launch_desc_lut<kGlobalU16>(a, mode, grid, lds, s) : launch_desc_lut<kLdsU8Tail>(a, mode, grid, lds, s);
 }
 
-int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
+int launch_classify_stream_multi(const ClassifyArgs& a, const StreamBatches& sb, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;
   const int mode = !a.swap ? 0 : (a.mac_out ? 2 : 1);
   const size_t lds = stream_lds(a.nb, mode);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (a.m == 65537u)
-    return hist ? launch_stream_mode<true, true>(a, mode, grid, lds, s) : launch_stream_mode<true, false>(a, mode, grid, lds, s);
-  return hist ? launch_stream_mode<false, true>(a, mode, grid, lds, s) : launch_stream_mode<false, false>(a, mode, grid, lds, s);
+    return hist ? launch_stream_mode<true, true>(a, sb, mode, grid, lds, s)
+                : launch_stream_mode<true, false>(a, sb, mode, grid, lds, s);
+  return hist ? launch_stream_mode<false, true>(a, sb, mode, grid, lds, s)
+              : launch_stream_mode<false, false>(a, sb, mode, grid, lds, s);
+}
+
+int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
+  StreamBatches sb{};
+  sb.pkts[0] = a.pkts;
+  sb.backend[0] = a.backend;
+  sb.mac_out[0] = a.mac_out;
+  sb.part_hist[0] = a.part_hist;
+  sb.n_pkts[0] = a.n_pkts;
+  sb.unit_base[0] = 0;
+  sb.unit_base[1] = (((a.n_pkts + 63u) >> 6) + kStreamW - 1) / kStreamW;
+  sb.n = 1;
+  return launch_classify_stream_multi(a, sb, grid, stream);
 }
 
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream) {
@@ -2176,9 +2219,29 @@ int launch_group(const GroupArgs& a, int scan, void* stream) {
                             static_cast<int>(lds)) != hipSuccess)
       (void)hipGetLastError();
   }
-  hipLaunchKernelGGL(fn, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
+  GroupMulti gm{};
+  gm.g[0] = a;
+  gm.per = a.n_parts;
+  hipLaunchKernelGGL(fn, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), gm);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "group launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream) {
+  const GroupArgs& a = gm.g[0];
+  if (n == 0 || n > kMaxMulti || scan == kScanKernel) return set_error(NBG_EINVAL, "group (multi): %u batches", n);
+  const size_t lds = group_lds(a.nb + 1, gm.per, scan);
+  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7> : group_kernel<kScanLds, 7>)
+                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10> : group_kernel<kScanLds, 10>);
+  if (lds > 64 * 1024) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            static_cast<int>(lds)) != hipSuccess)
+      (void)hipGetLastError();
+  }
+  hipLaunchKernelGGL(fn, dim3(gm.per * n), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), gm);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "group launch (multi): %s", hipGetErrorString(e));
   return NBG_OK;
 }
 

@@ -68,6 +68,8 @@ struct nbg_maglev {
   uint32_t* d_totals = nullptr;       // [nb+1]            (scan-kernel fallback)
   uint32_t* d_bin_base = nullptr;     // [nb+1]            (wide grouping path)
   uint8_t* d_sink = nullptr;          // [1 KiB] stores of idle lanes (descriptor streaming kernel)
+  uint32_t* d_part_multi = nullptr;   // [2][kMaxMulti][kMaxParts][nb+1] (nbg_maglev_classify_device_multi, on first use)
+  uint32_t mparity = 0;
   uint32_t parity = 0;
   uint32_t* d_counts = nullptr;       // used when the caller passes no counts buffer
   // deferred grouping (NBG_DEFER_GROUP): the group kernel's arguments, launched by finish_group
@@ -78,6 +80,8 @@ struct nbg_maglev {
   HistArgs pending_hist_args{};
   GroupArgs pending_args{};
   ScanArgs pending_scan{};
+  uint32_t pending_multi = 0;         // > 0: the deferred group is a multi-batch group launch
+  GroupMulti pending_gm{};
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
   bool issued = false;                // a launch has been issued on last_stream
   hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
@@ -219,6 +223,7 @@ void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_totals);
   (void)hipFree(h->d_bin_base);
   (void)hipFree(h->d_sink);
+  (void)hipFree(h->d_part_multi);
   (void)hipFree(h->d_counts);
   h->d_part_hist = nullptr;
   h->d_part_graph = nullptr;
@@ -226,6 +231,7 @@ void free_scratch(nbg_maglev* h) {
   h->d_totals = nullptr;
   h->d_bin_base = nullptr;
   h->d_sink = nullptr;
+  h->d_part_multi = nullptr;
   h->d_counts = nullptr;
 }
 
@@ -750,6 +756,135 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
                          d_mac_out, nullptr, 0, nullptr, stream);
 }
 
+int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, uint32_t n_batches, uint32_t stride,
+                                     uint16_t fixed_len, uint32_t flags, void* stream) {
+  if (!h) return set_error(NBG_EINVAL, "classify (multi): null handle");
+  if (!batches || n_batches == 0 || n_batches > NBG_MAX_MULTI)
+    return set_error(NBG_EINVAL, "classify (multi): 1..%u batches", NBG_MAX_MULTI);
+  if (flags & ~(NBG_SWAP_MACS | NBG_DEFER_GROUP))
+    return set_error(NBG_EINVAL, "classify (multi): flags other than NBG_SWAP_MACS and NBG_DEFER_GROUP");
+  if (h->pending) return set_error(NBG_EINVAL, "classify (multi): a deferred group is pending (nbg_maglev_finish_group)");
+  const bool group = batches[0].d_perm || batches[0].d_counts;
+  uint64_t total = 0, max_n = 0;
+  bool lean = stride >= 64 && stride % 16 == 0 && fixed_len >= 48 && stride < (1u << 24);
+  for (uint32_t j = 0; j < n_batches; ++j) {
+    const nbg_batch& x = batches[j];
+    if ((x.d_perm || x.d_counts) != group)
+      return set_error(NBG_EINVAL, "classify (multi): batch %u: every batch or none has perm/counts", j);
+    if (x.n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify (multi): batch %u: n_pkts must be < 2^30", j);
+    if (x.n_pkts && (!x.d_pkts || !x.d_backend))
+      return set_error(NBG_EINVAL, "classify (multi): batch %u: null packet or backend buffer", j);
+    if (x.n_pkts == 0 || (reinterpret_cast<uintptr_t>(x.d_pkts) & 15u)) lean = false;
+    total += x.n_pkts;
+    max_n = std::max<uint64_t>(max_n, x.n_pkts);
+  }
+  const uint32_t nbins = h->nb + 1;
+  const uint64_t per = (max_n + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
+  const uint32_t part_pkts = static_cast<uint32_t>(std::max<uint64_t>(per, 1) * kChunk);
+  const uint32_t n_parts_max = static_cast<uint32_t>((max_n + part_pkts - 1) / part_pkts);
+  const int scan = group ? pick_group_scan(nbins, n_parts_max) : kScanDirect;
+  const bool fused = lean && !h->wide && h->m <= 65537 && total >= 262144 && nbins <= 256 && use_stream(h, total) &&
+                     (!group || (hist_in_classify(nbins) && scan != kScanKernel));
+  if (!fused && (flags & NBG_DEFER_GROUP))
+    return set_error(NBG_EINVAL, "classify (multi): NBG_DEFER_GROUP needs the fused path (fixed 64-B slots, >= 262144 "
+                     "packets in all, <= 255 backends)");
+  if (!fused) {
+    // one batch after another on the same stream (same results, one launch sequence each)
+    for (uint32_t j = 0; j < n_batches; ++j) {
+      const nbg_batch& x = batches[j];
+      const int rc = classify_common(h, x.d_pkts, nullptr, nullptr, stride, fixed_len, x.n_pkts, flags, x.d_backend,
+                                     x.d_perm, x.d_counts, x.d_mac_out, nullptr, 0, nullptr, stream);
+      if (rc) return rc;
+    }
+    return NBG_OK;
+  }
+  DeviceGuard g(h->device);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  NBG_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap));
+  if (cap != hipStreamCaptureStatusNone)
+    return set_error(NBG_EINVAL, "classify (multi): multi-launch batches cannot be captured in a graph");
+  const size_t set_words = static_cast<size_t>(kMaxMulti) * kMaxParts * nbins;
+  if (group && !h->d_part_multi) {
+    NBG_HIP(hipMalloc(&h->d_part_multi, 2 * set_words * sizeof(uint32_t)));
+    SetupStream st;
+    (void)st.zero(h->d_part_multi, 2 * set_words * sizeof(uint32_t));
+    NBG_HIP(st.finish());
+  }
+  int rc = order_after_last(h, static_cast<hipStream_t>(stream));
+  if (rc) return rc;
+  uint32_t* set_cur = group ? h->d_part_multi + static_cast<size_t>(h->mparity) * set_words : nullptr;
+  uint32_t* set_next = group ? h->d_part_multi + static_cast<size_t>(h->mparity ^ 1u) * set_words : nullptr;
+  ClassifyArgs a{};
+  a.stride = stride;
+  a.fixed_len = fixed_len;
+  a.lut = h->d_lut;
+  a.m = static_cast<uint32_t>(h->m);
+  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);
+  a.nb = h->nb;
+  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  a.win_owned = 1u;
+  a.wb_full = 1u;
+  a.lean = 1u;
+  a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
+  a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+  a.part_pkts = part_pkts;
+  a.hist16 = group && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
+  const bool records = batches[0].d_mac_out != nullptr;
+  StreamBatches sb{};
+  GroupMulti gm{};
+  uint32_t units = 0;
+  for (uint32_t j = 0; j < n_batches; ++j) {
+    const nbg_batch& x = batches[j];
+    if ((x.d_mac_out != nullptr) != records)
+      return set_error(NBG_EINVAL, "classify (multi): batch %u: every batch or none has d_mac_out", j);
+    sb.pkts[j] = x.d_pkts;
+    sb.backend[j] = x.d_backend;
+    sb.mac_out[j] = x.d_mac_out;
+    sb.part_hist[j] = group ? set_cur + static_cast<size_t>(j) * kMaxParts * nbins : nullptr;
+    sb.n_pkts[j] = static_cast<uint32_t>(x.n_pkts);
+    sb.unit_base[j] = units;
+    units += static_cast<uint32_t>((((x.n_pkts + 63) >> 6) + stream_waves_per_block() - 1) / stream_waves_per_block());
+    GroupArgs& ga = gm.g[j];
+    ga.backend = x.d_backend;
+    ga.n_pkts = static_cast<uint32_t>(x.n_pkts);
+    ga.nb = h->nb;
+    uint32_t bits = 0;
+    while ((1u << bits) < nbins) ++bits;
+    ga.bits = bits;
+    ga.n_parts = static_cast<uint32_t>((x.n_pkts + part_pkts - 1) / part_pkts);
+    ga.part_pkts = part_pkts;
+    ga.part_hist = sb.part_hist[j];
+    ga.hist16 = a.hist16;
+    ga.part_hist_next = set_next;
+    ga.next_words = static_cast<uint32_t>(set_words);
+    ga.counts = x.d_counts ? x.d_counts : h->d_counts;
+    ga.perm = x.d_perm;
+  }
+  sb.unit_base[n_batches] = units;
+  sb.n = n_batches;
+  a.mac_out = sb.mac_out[0];  // selects the records mode; per-batch pointers come from sb
+  a.part_hist = sb.part_hist[0];
+  a.pkts = sb.pkts[0];
+  a.n_pkts = sb.n_pkts[0];
+  a.backend = sb.backend[0];
+  h->last_stream = static_cast<hipStream_t>(stream);
+  h->issued = true;
+  if ((rc = launch_classify_stream_multi(a, sb, h->cus, stream))) return rc;
+  if (group) {
+    h->mparity ^= 1u;
+    gm.per = n_parts_max;
+    if (flags & NBG_DEFER_GROUP) {
+      h->pending = true;
+      h->pending_multi = n_batches;
+      h->pending_gm = gm;
+      h->pending_scan_mode = scan;
+      return NBG_OK;
+    }
+    if ((rc = launch_group_multi(gm, n_batches, scan, stream))) return rc;
+  }
+  return NBG_OK;
+}
+
 int nbg_chain_lpm_maglev_device(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_groups, uint8_t* d_pkts,
                                 const uint32_t* d_off, const uint16_t* d_len, uint32_t stride, uint16_t fixed_len,
                                 uint64_t n_pkts, uint32_t flags, uint16_t* d_gate, uint16_t* d_backend,
@@ -817,6 +952,11 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   int rc = order_after_last(h, static_cast<hipStream_t>(stream));  // after the classify, on any stream
   if (rc) return rc;
   h->last_stream = static_cast<hipStream_t>(stream);
+  if (h->pending_multi) {
+    const uint32_t n = h->pending_multi;
+    h->pending_multi = 0;
+    return launch_group_multi(h->pending_gm, n, h->pending_scan_mode, stream);
+  }
   if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;
   if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
   if ((rc = h->pending_wide ? launch_group_wide(h->pending_args, stream)

@@ -76,6 +76,19 @@ struct ClassifyArgs {
   uint8_t* sink;            // descriptor streaming kernel: 1 KiB scratch for stores of lanes with none
 };
 
+// Several batches in one streaming-classify launch (nbg_maglev_classify_device_multi): what differs
+// per batch.  A single-batch launch passes n = 1.  Units (512 packets) never straddle batches.
+constexpr uint32_t kMaxMulti = 8;
+struct StreamBatches {
+  uint8_t* pkts[kMaxMulti];
+  uint16_t* backend[kMaxMulti];
+  uint8_t* mac_out[kMaxMulti];
+  uint32_t* part_hist[kMaxMulti];
+  uint32_t n_pkts[kMaxMulti];
+  uint32_t unit_base[kMaxMulti + 1];  // first unit of batch j; unit_base[n] = all units
+  uint32_t n;
+};
+
 // NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
 struct TileArgs {
   const uint32_t* idx;      // [n_pkts] from the classify kernel (kIdx)
@@ -124,6 +137,13 @@ struct GroupArgs {
   uint32_t* bin_base;         // [nb+1] wide path: first perm slot of every group
 };
 
+// The group kernel over several batches: blocks [j * per, j * per + g[j].n_parts) group batch j.
+// Every g[j] names the same part_hist_next / next_words (zeroed by the whole grid).
+struct GroupMulti {
+  GroupArgs g[kMaxMulti];
+  uint32_t per;
+};
+
 // How the group kernel gets each partition's per-bin prefix: from scan_kernel's output, by
 // summing the partition histograms staged in LDS, or by summing them straight from L2.
 enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
@@ -133,6 +153,8 @@ int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid
 // Streaming classify (lean fixed slots, u8 LUT of <= 65537 entries staged in LDS): one block per
 // CU; a.tiles_per_wave = the contiguous 64-packet tiles of each of the grid's waves.
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream);
+// The same over several batches (sb.n >= 1; a carries what they share)
+int launch_classify_stream_multi(const ClassifyArgs& a, const StreamBatches& sb, int grid, void* stream);
 int stream_waves_per_block();
 // Streaming classify for descriptor layouts with owned windows (u8 LUT in LDS, or the u16 LUT
 // gathered from L2); stream_desc_lds: its dynamic LDS bytes (mode 0 read only, 1 in place, 2 records).
@@ -144,6 +166,8 @@ bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
                       uint16_t* gate, void* stream);
 int launch_group(const GroupArgs& a, int scan, void* stream);
+// one launch grouping gm.g[0 .. n): blocks per batch gm.per (the largest n_parts)
+int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream);
 int launch_group_wide(const GroupArgs& a, void* stream);  // nb + 1 > kMaxGroupBins
 // One launch for a batch of at most small_max() packets and at most kMaxGroupBins bins: classify
 // and (when g.perm / g.counts) group.  The batch base must be 16-B aligned.

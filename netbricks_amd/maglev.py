@@ -16,8 +16,8 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (NBG_DEFER_GROUP, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_OWNED_WINDOWS, NBG_SENTINEL,
-                   NBG_STREAM_DESC,
+from ._lib import (NBG_DEFER_GROUP, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_MAX_MULTI, NBG_OWNED_WINDOWS,
+                   NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
@@ -209,6 +209,42 @@ class Maglev:
                                                _ptr(counts) if group else None, _ptr(mac_out), stream)
         check(rc, "nbg_maglev_classify_device_ex")
         return GroupedBatch(backend, perm if scatter else None, counts if group else None)
+
+    def group_by_multi(self, batches, *, stride: int = 64, frame_len: int = 60, swap_macs: bool = True,
+                       group: bool = True, scatter: bool = True, records: bool = False,
+                       defer_group: bool = False, stream=None) -> list:
+        """Classify several device-resident fixed-slot batches in one launch of each kernel
+        (nbg_maglev_classify_device_multi): `batches` is a list of (pkts, n_pkts) with pkts a
+        contiguous uint8 tensor on this device.  Every batch gets its own backend / perm / counts
+        (and 12-B MAC records with records=True), as group_by would give it alone.  Returns one
+        GroupedBatch per batch."""
+        import torch
+
+        if not 1 <= len(batches) <= NBG_MAX_MULTI:
+            raise ValueError(f"batches: 1..{NBG_MAX_MULTI}")
+        arr = (NbgBatch * len(batches))()
+        out = []
+        for j, (pkts, n_pkts) in enumerate(batches):
+            dev = pkts.device
+            if pkts.dtype != torch.uint8 or not pkts.is_contiguous():
+                raise ValueError(f"batch {j}: expected a contiguous uint8 tensor")
+            if dev.type != "cuda" or dev.index != self.device:
+                raise ValueError(f"batch {j}: on {dev}, expected cuda:{self.device}")
+            if n_pkts and (n_pkts - 1) * stride + min(frame_len, stride) > pkts.numel():
+                raise ValueError(f"batch {j}: smaller than n_pkts fixed slots")
+            backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
+            perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev) if group and scatter else None
+            counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev) if group else None
+            mac = torch.empty(max(12 * n_pkts, 1), dtype=torch.uint8, device=dev) if records else None
+            arr[j] = NbgBatch(_ptr(pkts), n_pkts, _ptr(backend), _ptr(perm), _ptr(counts), _ptr(mac))
+            out.append((GroupedBatch(backend, perm, counts), mac))
+        if stream is None:
+            stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
+        flags = (NBG_SWAP_MACS if swap_macs else 0) | (NBG_DEFER_GROUP if defer_group else 0)
+        check(lib.nbg_maglev_classify_device_multi(self._h, arr, len(batches), stride, frame_len, flags, stream),
+              "nbg_maglev_classify_device_multi")
+        self._multi_keep = arr
+        return [g for g, _ in out] if not records else out
 
     def finish_group(self, stream=None) -> None:
         """Launch the grouping kernel deferred by group_by(..., defer_group=True)."""

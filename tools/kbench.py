@@ -75,6 +75,32 @@ def main():
         "full path mac_out": lambda i: mg.group_by(bufs[i % 8], n, backend=backend, perm=perm, counts=counts,
                                                    mac_out=mac, **kw(i)),
     }
+    # several batches per launch (nbg_maglev_classify_device_multi): per-call time covers K batches
+    from netbricks_amd._lib import NbgBatch, lib as _clib
+    m_outs = [(torch.empty(n, dtype=torch.uint16, device=dev), torch.empty(n, dtype=torch.uint32, device=dev),
+               torch.empty(args.nb + 1, dtype=torch.uint32, device=dev), torch.empty(n * 12, dtype=torch.uint8, device=dev))
+              for _ in range(8)]
+    m_arrs = {}
+    for K in (2, 4):
+        for rec in (False, True):
+            for g0 in range(0, 8, K):
+                arr = (NbgBatch * K)()
+                for j in range(K):
+                    be, pm, ct, mo = m_outs[g0 + j]
+                    arr[j] = NbgBatch(bufs[g0 + j].data_ptr(), n, be.data_ptr(), pm.data_ptr(), ct.data_ptr(),
+                                      mo.data_ptr() if rec else None)
+                m_arrs[(K, rec, g0 // K)] = arr
+
+    def multi(i, K, rec, swap):
+        st = torch.cuda.current_stream(dev).cuda_stream
+        rc = _clib.nbg_maglev_classify_device_multi(mg._h, m_arrs[(K, rec, i % (8 // K))], K, 64, 60,
+                                                    1 if swap else 0, st)
+        assert rc == 0, rc
+
+    for K in (2, 4):
+        for mode, rec, swap in (("noswap", False, False), ("inplace", False, True), ("mac_out", True, True)):
+            variants[f"multi{K} {mode} (per call of {K} batches)"] = (
+                lambda i, K=K, rec=rec, swap=swap: multi(i, K, rec, swap))
     # multi-stream: independent batches in flight on S streams, one handle (scratch) per stream
     extra = {}
     for S in (() if args.no_multistream else tuple(int(x) for x in args.streams.split(","))):
