@@ -539,6 +539,11 @@ def run_rank(args) -> None:
                         "kernel and one group launch (nbg_maglev_classify_device_multi); every batch keeps its own "
                         "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
 
+    if args.multi_only:  # profiling run: only the multi-batch passes
+        print(json.dumps({f"{v}_multi{MULTI_K}": multi_pass(v, max(args.steps // MULTI_K, 10), 3)
+                          for v in ("read_only", "in_place")}), flush=True)
+        return
+
     if args.pmc_child:  # under rocprofv3 --pmc: each variant's launches in a fixed order
         for v in PMC_VARIANTS:
             for i in range(PMC_WARMUP + PMC_STEPS):
@@ -687,6 +692,8 @@ def parse_args(argv):
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip the records / read-only variant passes")
+    ap.add_argument("--multi-only", action="store_true",
+                    help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--inline", action="store_true",
                     help="run as a single rank in this process (no launcher; for running under a profiler)")

@@ -769,21 +769,35 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   const uint32_t nt = b < n_units ? (n_units - b + G - 1) / G : 0u;  // units of this block (block-uniform)
   // position k: global unit b + k*G; its batch j (scalar search, block-uniform) and the unit's
   // first packet within the batch
-  auto batch_of = [&](uint32_t u) {
-    uint32_t j = 0;
-    while (j + 1 < sb.n && u >= sb.unit_base[j + 1]) ++j;
-    return j;
+  // A cursor over the batches: units [lo, hi) are batch j's.  Positions visit increasing units, so
+  // a cursor only moves forward, at most n - 1 times per block: the kernel arguments are read at a
+  // batch change only.  Measured (rocprof, 4 x 1M per launch, profiles/r02_multi_batch_rocprof.txt):
+  // read-only 45.7 us with the cursor against 52.7 us with a per-unit search of the argument arrays.
+  struct Cursor {
+    uint32_t j, lo, hi;
+    ClassifyArgs v;
   };
-  auto view = [&](uint32_t j) {
-    ClassifyArgs v = a;
-    v.pkts = sb.pkts[j];
-    v.n_pkts = sb.n_pkts[j];
-    v.backend = sb.backend[j];
-    v.mac_out = sb.mac_out[j];
-    v.part_hist = sb.part_hist[j];
-    return v;
+  auto load = [&](Cursor& c, uint32_t j) {
+    c.j = j;
+    c.lo = sb.unit_base[j];
+    c.hi = sb.unit_base[j + 1];
+    c.v = a;
+    c.v.pkts = sb.pkts[j];
+    c.v.n_pkts = sb.n_pkts[j];
+    c.v.backend = sb.backend[j];
+    c.v.mac_out = sb.mac_out[j];
+    c.v.part_hist = sb.part_hist[j];
   };
-  auto first_pkt = [&](uint32_t u, uint32_t j) { return ((u - sb.unit_base[j]) * kStreamW + wave) * 64u; };
+  auto seek = [&](Cursor& c, uint32_t u) {
+    if (u < c.hi) return;
+    uint32_t jj = c.j + 1;
+    while (jj + 1 < sb.n && u >= sb.unit_base[jj + 1]) ++jj;
+    load(c, jj);
+  };
+  auto first_pkt = [&](const Cursor& c, uint32_t u) { return ((u - c.lo) * kStreamW + wave) * 64u; };
+  Cursor cur, nxt;  // the unit being classified; the unit whose tile is issued
+  load(cur, 0);
+  load(nxt, 0);
   uint32_t* hist = hist_base;  // [2][hstride]
 
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
@@ -803,8 +817,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   // make the wait for it stricter (vmcnt counts stores too)
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
   for (uint32_t k = 0; k < first; ++k) {
-    const uint32_t u = b + k * G, j = batch_of(u);
-    issue_tile<kRow, MODE != 2>(view(j), first_pkt(u, j), ring_lds + k * kTileLds, lane);
+    const uint32_t u = b + k * G;
+    seek(nxt, u);
+    issue_tile<kRow, MODE != 2>(nxt.v, first_pkt(nxt, u), ring_lds + k * kTileLds, lane);
     seq += 4;
     (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
   }
@@ -817,9 +832,10 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   SPROBE(1)
 
   for (uint32_t k = 0; k < nt; ++k) {
-    const uint32_t u = b + k * G, j = batch_of(u);
-    const ClassifyArgs aj = view(j);
-    const uint32_t tb = first_pkt(u, j);
+    const uint32_t u = b + k * G;
+    seek(cur, u);
+    const ClassifyArgs& aj = cur.v;
+    const uint32_t tb = first_pkt(cur, u);
 #if NBG_SEQWAIT
     wait_vm_n(seq - sA);  // kStreamAhead tiles (and their stores) stay in flight
 #else
@@ -836,8 +852,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     uint32_t sN = 0;
     if (k + kRing < nt) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const uint32_t u2 = u + kRing * G, j2 = batch_of(u2);
-      issue_tile<kRow, MODE != 2>(view(j2), first_pkt(u2, j2), ring_lds + (k % kRing) * kTileLds, lane);
+      const uint32_t u2 = u + kRing * G;
+      seek(nxt, u2);
+      issue_tile<kRow, MODE != 2>(nxt.v, first_pkt(nxt, u2), ring_lds + (k % kRing) * kTileLds, lane);
       seq += 4;
       sN = seq;
     }
@@ -860,7 +877,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       lds_sync();
       if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
-        stream_flush<HIST>(aj, h, nbins, ((u - sb.unit_base[j]) * kStreamW * 64u) / a.part_pkts, lane);
+        stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
   }
