@@ -670,6 +670,12 @@ def run_rank(args) -> None:
                                         "section 5); variants.read_only is north_star's parse + hash + lookup"}
         if variants:
             line["variants"] = variants
+            ro = variants.get(f"read_only_multi{MULTI_K}") or variants.get("read_only")
+            if ro:  # BASELINE.json north_star: parse + hash + lookup at >= 70 % of the HBM roofline
+                line["north_star"] = {"target_frac": 0.70, "frac": float(ro["frac"]), "met": bool(ro["frac"] >= 0.70),
+                                      "variant": f"read_only_multi{MULTI_K}" if f"read_only_multi{MULTI_K}" in variants
+                                      else "read_only",
+                                      "single_batch_frac": variants.get("read_only", {}).get("frac")}
         line["cpu_baseline"] = cpu
         if scatter is not None:
             line["scatter_inclusive"] = scatter
