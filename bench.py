@@ -482,7 +482,7 @@ def run_rank(args) -> None:
     # ---- several batches per launch (nbg_maglev_classify_device_multi): MULTI_K batches of 1M in
     #      one streaming-classify launch and one group launch, each batch with its own outputs
     m_arrs = {}
-    if gpu and world == 1 and not args.no_variants and N_BATCHES % MULTI_K == 0:
+    if gpu and world == 1 and not args.no_variants and not args.no_multi and N_BATCHES % MULTI_K == 0:
         from netbricks_amd._lib import NbgBatch, lib as clib
         m_outs = [(torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
                    torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(N_BATCHES)]
@@ -698,6 +698,7 @@ def parse_args(argv):
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip the records / read-only variant passes")
+    ap.add_argument("--no-multi", action="store_true", help="skip the multi-batch variants")
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")

@@ -149,7 +149,13 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
 }
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-#ifdef NBG_NT_LOADS  // measurement build: packet windows are read once, so try the streaming policy
+// Packet windows are read once: the streaming policy.  Round 1 measured it neutral on C2's 4-stream
+// path (then served by this kernel); round 2, with C2 on the streaming kernel, it cut C3 from 48.9 to
+// 44.8 us and C5 from 28.3 to 26.5 us per batch at 3 streams (profiles/r02_c3_c5_ntloads_ab.txt).
+#ifndef NBG_NT_LOADS
+#define NBG_NT_LOADS 1
+#endif
+#if NBG_NT_LOADS
 __device__ __forceinline__ uint4 ldg16(const uint8_t* p) {
   const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
   return make_uint4(w.x, w.y, w.z, w.w);

@@ -8,5 +8,5 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; [ $rc -ne 0 ] && { tail -
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R0/gpurun_out/prof/multi" -o run --output-format csv -- python "$R0/bench.py" --inline --no-pmc --no-cpu-baseline --multi-only --steps 200 > "$R0/gpurun_out/prof/multi.json" 2> "$R0/gpurun_out/prof/multi.err"
 rc=$?; echo "rocprof multi rc=$rc"; cat "$R0/gpurun_out/prof/multi.json"; python "$R0/tools/kstats.py" "$R0/gpurun_out/prof/multi/run_kernel_stats.csv"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R0/gpurun_out/prof/var" -o run --output-format csv -- python "$R0/bench.py" --inline --no-pmc --no-cpu-baseline --streams 1 --steps 200 --warmup 20 > "$R0/gpurun_out/prof/var.json" 2> "$R0/gpurun_out/prof/var.err"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R0/gpurun_out/prof/var" -o run --output-format csv -- python "$R0/bench.py" --inline --no-pmc --no-cpu-baseline --no-multi --streams 1 --steps 200 --warmup 20 > "$R0/gpurun_out/prof/var.json" 2> "$R0/gpurun_out/prof/var.err"
 rc=$?; echo "rocprof variants rc=$rc"; python "$R0/tools/kstats.py" "$R0/gpurun_out/prof/var/run_kernel_stats.csv"; exit $rc
