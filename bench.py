@@ -62,6 +62,7 @@ PATH_BYTES = {k: v + 4 for k, v in CLASSIFY_BYTES.items()}
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_WARMUP, PMC_STEPS = 10, 40
 PMC_VARIANTS = ("in_place", "records", "read_only")
+PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
 
 
 def log(*a):
@@ -289,6 +290,16 @@ def pmc_traffic(timeout_s: int = 150):
         out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
                      "algorithmic_bytes": BATCH * CLASSIFY_BYTES[name],
                      "ratio": round((rd + wr) / (BATCH * CLASSIFY_BYTES[name]), 3)}
+    base = len(PMC_VARIANTS) * seg
+    for k, name in enumerate(PMC_MULTI):
+        f = vals["FETCH_SIZE"][base + k * seg + PMC_WARMUP:base + (k + 1) * seg]
+        w = vals["WRITE_SIZE"][base + k * seg + PMC_WARMUP:base + (k + 1) * seg]
+        if len(f) != PMC_STEPS or len(w) != PMC_STEPS:
+            break  # no multi-batch launches in this run
+        rd, wr = 2.0 * float(np.mean(f)), float(np.mean(w))
+        alg = MULTI_K * BATCH * CLASSIFY_BYTES[name]
+        out[f"{name}_multi{MULTI_K}"] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
+                                         "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3)}
     return out
 
 
@@ -551,6 +562,12 @@ def run_rank(args) -> None:
                                 stream=streams[0].cuda_stream, **variant_kw(v, 0), **outs[0])
             sync_all()
             mgs[0].check()
+        if m_arrs:  # then the multi-batch launches (one classify dispatch per MULTI_K batches)
+            for v in PMC_MULTI:
+                for i in range(PMC_WARMUP + PMC_STEPS):
+                    mcall(i, v, streams[0].cuda_stream)
+                sync_all()
+                mgs[0].check()
         return
 
     # ---- timed region: K steps over all streams, bracketed by barrier + synchronize, max over ranks
