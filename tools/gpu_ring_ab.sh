@@ -1,0 +1,11 @@
+# Ring depth A/B (read-only and records only: in place does not fit three 64-B-row tiles per wave)
+cd "$GRAFT_REPO_ROOT" || exit 9
+R0="$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for pass in 1 2; do
+  for L in tools/ab/lib_*.so; do
+    echo "== $L (pass $pass)"
+    NBG_LIB_OVERRIDE=$PWD/$L timeout -k 10 300 python -u tools/kbench.py --no-multistream --rounds 5 --only "classify noswap nogroup,classify mac_out nogroup,multi4 noswap,multi4 mac_out" > gpurun_out/ab.log 2>&1
+    rc=$?; grep median gpurun_out/ab.log; [ $rc -ne 0 ] && { tail -5 gpurun_out/ab.log; exit $rc; }
+  done
+done
