@@ -683,8 +683,9 @@ def run_rank(args) -> None:
                                           "batch overlaps the classify of the next",
                                 "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts), "
                                         "so the physical traffic is ~1.7x the 78 algorithmic bytes and this variant's "
-                                        "frac is capped near 0.40 by the measured read+rewrite ceiling (DESIGN.md "
-                                        "section 5); variants.read_only is north_star's parse + hash + lookup"}
+                                        "frac is capped near 0.46 by the measured read+rewrite ceiling with nt loads "
+                                        "(DESIGN.md section 5); variants.read_only / read_only_multi4 are north_star's "
+                                        "parse + hash + lookup"}
         if variants:
             line["variants"] = variants
             ro = variants.get(f"read_only_multi{MULTI_K}") or variants.get("read_only")

@@ -23,16 +23,21 @@ __device__ inline void nt_store(uint4* p, uint4 v) {
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
+__device__ inline uint4 nt_load(const uint4* p) {
+  const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(w.x, w.y, w.z, w.w);
+}
+
 constexpr size_t kBytes = 64ull << 20;
 constexpr int kBufs = 8;
 
 // U uint4 per thread, contiguous 1 KiB per wave-instruction; MODE: 0 read, 1 rw full, 2 rw chunk0, 3 copy
-template <int U, int MODE>
+template <int U, int MODE, bool NTL = false>
 __global__ __launch_bounds__(256) void pattern(uint4* __restrict__ buf, uint4* __restrict__ dst, uint32_t* sink) {
   const size_t base = (static_cast<size_t>(blockIdx.x) * 256 * U) + threadIdx.x;
   uint4 v[U];
 #pragma unroll
-  for (int k = 0; k < U; ++k) v[k] = buf[base + k * 256];
+  for (int k = 0; k < U; ++k) v[k] = NTL ? nt_load(&buf[base + k * 256]) : buf[base + k * 256];
   uint32_t acc = 0;
 #pragma unroll
   for (int k = 0; k < U; ++k) {
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(256) void pattern_p(uint4* __restrict__ buf, uint4*
 
 // IMIX descriptor windows: 4 lanes per packet read its 64-B window at off[p] (64-B aligned,
 // scattered over ~375 MB); MODE 0 read, 1 in-place full-window nt rewrite, 2 + dense 12 B/pkt out
-template <int MODE>
+template <int MODE, bool NTL = false>
 __global__ __launch_bounds__(256) void windows(uint8_t* __restrict__ buf, const uint32_t* __restrict__ off,
                                                uint8_t* __restrict__ dst, uint32_t* sink, uint32_t n) {
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, part = lane & 3u, quad = lane >> 2;
@@ -82,7 +87,8 @@ __global__ __launch_bounds__(256) void windows(uint8_t* __restrict__ buf, const 
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t o = static_cast<uint32_t>(__shfl(static_cast<int>(own), k * 16 + quad));
-    v[k] = *reinterpret_cast<const uint4*>(buf + o + part * 16u);
+    v[k] = NTL ? nt_load(reinterpret_cast<const uint4*>(buf + o + part * 16u))
+               : *reinterpret_cast<const uint4*>(buf + o + part * 16u);
   }
   uint32_t acc = 0;
 #pragma unroll
@@ -160,6 +166,19 @@ int main() {
     RUN(4, 4, "read + dense 16B/pkt out U4", B, B / 4);
     RUN(4, 5, "rw full nt-store U4", B, B);
     RUN(4, 6, "rw chunk0 nt-store U4", B, B / 4);
+    {  // the same shapes with non-temporal loads (the product's packet loads since round 2)
+      const int grid = static_cast<int>(n16 / (256 * 4));
+      report("read U4 nt-load", time_it([&](int i) { pattern<4, 0, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, 0);
+      report("rw full nt-load nt-store U4", time_it([&](int i) { pattern<4, 5, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
+      report("read nt-load + dense 16B/pkt out U4", time_it([&](int i) { pattern<4, 4, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 4);
+      // four 64 MiB buffers' worth in one launch (the multi-batch launch's read ceiling)
+      uint4* big;
+      CK(hipMalloc(&big, 4 * kBytes));
+      CK(hipMemset(big, 1, 4 * kBytes));
+      const int g4 = static_cast<int>(4 * n16 / (256 * 4));
+      report("read 256 MiB in one launch U4 nt-load", time_it([&](int) { pattern<4, 0, true><<<g4, 256>>>(big, dst, sink); }, iters), 4 * B, 0);
+      CK(hipFree(big));
+    }
     RUN(4, 3, "copy U4", B, B);
     RUN(8, 3, "copy U8", B, B);
     std::printf("--\n");
@@ -195,6 +214,10 @@ int main() {
     report("imix windows rw nt (in place)", us, W + D, W);
     us = time_it([&](int i) { windows<2><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
     report("imix windows read + 12B/pkt out", us, W + D, 12.0 * n);
+    us = time_it([&](int i) { windows<0, true><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    report("imix windows read nt-load", us, W + D, 0);
+    us = time_it([&](int i) { windows<1, true><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    report("imix windows rw nt-load nt-store", us, W + D, W);
   }
   return 0;
 }
