@@ -774,6 +774,8 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
     if (x.n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify (multi): batch %u: n_pkts must be < 2^30", j);
     if (x.n_pkts && (!x.d_pkts || !x.d_backend))
       return set_error(NBG_EINVAL, "classify (multi): batch %u: null packet or backend buffer", j);
+    if ((x.d_mac_out != nullptr) != (batches[0].d_mac_out != nullptr))
+      return set_error(NBG_EINVAL, "classify (multi): batch %u: every batch or none has d_mac_out", j);
     if (x.n_pkts == 0 || (reinterpret_cast<uintptr_t>(x.d_pkts) & 15u)) lean = false;
     total += x.n_pkts;
     max_n = std::max<uint64_t>(max_n, x.n_pkts);
@@ -829,14 +831,11 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
   a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
   a.part_pkts = part_pkts;
   a.hist16 = group && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
-  const bool records = batches[0].d_mac_out != nullptr;
   StreamBatches sb{};
   GroupMulti gm{};
   uint32_t units = 0;
   for (uint32_t j = 0; j < n_batches; ++j) {
     const nbg_batch& x = batches[j];
-    if ((x.d_mac_out != nullptr) != records)
-      return set_error(NBG_EINVAL, "classify (multi): batch %u: every batch or none has d_mac_out", j);
     sb.pkts[j] = x.d_pkts;
     sb.backend[j] = x.d_backend;
     sb.mac_out[j] = x.d_mac_out;
