@@ -49,8 +49,10 @@ BATCH = 1 << 20
 SLOT = 64
 FRAME = 60
 N_BATCHES = 8
-MULTI_K = 4        # batches per launch of the multi-batch variants
-MULTI_STREAMS = 2  # their streams (distinct batch groups in flight)
+# batches per launch of the multi-batch variants and their streams (distinct batch groups in
+# flight); the environment overrides are for sweeps (tools/gpu_multi_sweep.sh)
+MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
+MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet of the classify kernel per variant:
 #   in place: 64 B packet read + 12 B MAC write + 2 B backend write
