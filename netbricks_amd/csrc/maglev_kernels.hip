@@ -545,6 +545,11 @@ static_assert(kRing >= 2 && kRing <= 3, "classify_stream_kernel tracks the count
 // 48-B rows read faster, whole-line write-back beats 16-B partial-line stores)
 template <int MODE>
 constexpr uint32_t row_of() { return MODE == 1 ? 64u : 48u; }
+#ifndef NBG_RO_ROW64  // measurement build: whole 64-B rows (every DMA lane active) for read-only / records too
+#define NBG_RO_ROW64 0
+#endif
+template <int MODE>
+constexpr uint32_t stream_row_of() { return NBG_RO_ROW64 ? 64u : row_of<MODE>(); }
 constexpr uint32_t kLutLds = 65536;            // LUT bytes staged in LDS
 
 #ifdef NBG_SPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch:
@@ -753,7 +758,7 @@ __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const u
 // supplies pkts, n_pkts, backend, mac_out and part_hist (a view of `a`).
 template <bool F4, bool HIST, int MODE>
 __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a, StreamBatches sb) {
-  constexpr uint32_t kRow = row_of<MODE>(), kTileLds = 64u * kRow;
+  constexpr uint32_t kRow = stream_row_of<MODE>(), kTileLds = 64u * kRow;
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -851,7 +856,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
-    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE, kRow>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
                                                                     p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
@@ -2023,7 +2028,7 @@ size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
 
 size_t stream_lds(uint32_t nb, int mode) {
   const size_t hwords = 2 * (((nb + 1) + 3) & ~3u);
-  const size_t tile = 64u * (mode == 1 ? row_of<1>() : row_of<0>());
+  const size_t tile = 64u * (mode == 1 ? stream_row_of<1>() : stream_row_of<0>());
   return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + hwords * 4u;
 }
 
