@@ -217,7 +217,7 @@ class Maglev:
         (nbg_maglev_classify_device_multi): `batches` is a list of (pkts, n_pkts) with pkts a
         contiguous uint8 tensor on this device.  Every batch gets its own backend / perm / counts
         (and 12-B MAC records with records=True), as group_by would give it alone.  Returns one
-        GroupedBatch per batch."""
+        GroupedBatch per batch, or (GroupedBatch, records tensor) pairs with records=True."""
         import torch
 
         if not 1 <= len(batches) <= NBG_MAX_MULTI:
