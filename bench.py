@@ -2,12 +2,15 @@
 """Benchmark: device-resident Maglev (parse + MAC swap + FNV + LUT + per-backend FIFO grouping).
 
 Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,576 synthetic
-64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM.  One step = one batch
-through `nbg_maglev_classify_device` (classify kernel + grouping kernel), MAC swap in place.
-Steps rotate over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache) and are issued
-round-robin on `--streams` (default 3) HIP streams (independent batches, one handle per stream:
-NetBricks runs one pipeline per RX queue, scheduler/context.rs:241-255), so one batch's
-latency-bound grouping overlaps the next batch's bandwidth-bound classify.
+64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM, MAC swap in place.
+One step = one rotation over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache), i.e. 8
+batches, each through `nbg_maglev_classify_device_ex` with NBG_GROUP_LAG: the call classifies its
+batch and groups the handle's previous batch inside the same streaming launch (the reference's
+producer classifies and enqueues in one loop, operators/group_by.rs:43-55).  Batches are issued
+round-robin on `--streams` (default 3) HIP streams, one handle per stream (NetBricks runs one
+pipeline per RX queue, scheduler/context.rs:241-255); every handle's last pending group is
+launched by nbg_maglev_finish_group inside the timed region, so every batch of the K steps is
+fully classified and grouped between the two synchronisations.
 
 Process model.  `python bench.py --gpus N` is a launcher: it never touches the GPU, spawns N
 rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their environment),
@@ -17,10 +20,12 @@ owns its own batches (weak scaling, no data-path collective in the timed region)
 built on rank 0 and broadcast once over RCCL (setup, untimed).  `--selftest` runs the same
 launcher and rank logic on the CPU with gloo and no HIP call (the CPU test of the launcher).
 
-Roofline: the classify kernel (dominant) is timed with HIP events around each launch in a
-separate single-stream pass (NBG_DEFER_GROUP splits it from the grouping kernel); its HBM
-traffic is measured in the same invocation by two rocprofv3 --pmc passes (FETCH_SIZE,
-WRITE_SIZE) of a short child run, at N = 1.
+Roofline: the dominant kernel (the streaming classify launch, which at steady state also groups
+the previous batch) is timed with HIP events around each launch in a separate single-stream pass;
+its HBM traffic is measured in the same invocation by two rocprofv3 --pmc passes (FETCH_SIZE,
+WRITE_SIZE) of a short child run, at N = 1.  Variants beside the headline: grouping as a separate
+launch (round 2's path), records / read-only, several batches per launch, config C4's per-GPU
+shard (131,072 packets per launch), and configs C3 / C5 (IMIX).
 
 Prints ONE JSON line (rank 0 / the launcher; see DESIGN.md "Measurement").
 """
@@ -48,7 +53,10 @@ TABLE = 65537
 BATCH = 1 << 20
 SLOT = 64
 FRAME = 60
-N_BATCHES = 8
+N_BATCHES = 8           # rotating batches; one step = one rotation (BATCHES_PER_STEP launches)
+BATCHES_PER_STEP = N_BATCHES
+C4_SHARD = BATCH // 8   # config C4: a 1M batch in 8 contiguous shards, one per GPU
+IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the MALL)
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
 # flight); the environment overrides are for sweeps (tools/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
@@ -58,13 +66,18 @@ SEED = 0x4E42474D41474C56
 #   in place: 64 B packet read + 12 B MAC write + 2 B backend write
 #   records:  64 B packet read + 12 B dense MAC record + 2 B backend
 #   read only (north_star's parse + hash + lookup): 64 B read + 2 B backend
-# the whole path adds the grouping kernel's 4 B perm write.
+# the whole path adds the grouping's 4 B perm write; a lagged launch (classify batch i + group
+# batch i-1) moves the whole path's bytes per packet at steady state.
 CLASSIFY_BYTES = {"in_place": 64 + 12 + 2, "records": 64 + 12 + 2, "read_only": 64 + 2}
 PATH_BYTES = {k: v + 4 for k, v in CLASSIFY_BYTES.items()}
+C3_BYTES = {"classify": 64 + 6 + 12 + 2, "path": 64 + 6 + 12 + 2 + 4}      # + u32 off + u16 len
+C5_BYTES = {"classify": 64 + 6 + 2 + 2 + 4, "path": 64 + 6 + 2 + 2 + 4 + 4}  # gate + backend + 2 LPM gathers
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_WARMUP, PMC_STEPS = 10, 40
-PMC_VARIANTS = ("in_place", "records", "read_only")
+# the child's launch sequence, one classify dispatch per call, in this order
+PMC_ORDER = ("in_place", "in_place_separate", "records", "read_only", "c4_shard", "c3", "c5")
 PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
+NBG_SWAP_MACS, NBG_DEFER_GROUP, NBG_GROUP_LAG = 0x1, 0x10, 0x80
 
 
 def log(*a):
@@ -194,6 +207,11 @@ def gather_results(backend, counts, gbuf, gcounts, rank: int, world: int) -> Non
         dist.gather(c, None, dst=0)
 
 
+def aggregate_frac(total_pkts: float, seconds: float, bytes_per_pkt: int, world: int) -> float:
+    """Whole-job HBM fraction: all ranks' algorithmic bytes per second over N x the HBM peak."""
+    return round(total_pkts * bytes_per_pkt / seconds / 1e9 / (world * HBM_PEAK_GBPS), 4)
+
+
 class KernelTimer:
     """HIP events created with hipEventDisableSystemFence (timing only): a default timing event's
     system-scope release writes back and invalidates L2 at every record, which lands inside the
@@ -253,19 +271,38 @@ def _pmc_rows(d, counter):
     for row in csv.DictReader(open(path)):
         name = row.get("Kernel_Name", "")
         if row.get("Counter_Name") == counter and ("classify_stream_kernel" in name or "classify_kernel" in name):
-            rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0))
+            rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0,
+                         name))
     rows.sort()
-    return [v for _, v in rows]
+    return [v for _, v, _ in rows], [n for _, _, n in rows]
 
 
-def pmc_traffic(timeout_s: int = 150):
+def _pmc_algorithmic(name: str) -> int:
+    """Algorithmic bytes of one launch of a PMC_ORDER / multi entry."""
+    if name == "in_place":  # lagged: classify this batch + group the previous one (steady state)
+        return BATCH * PATH_BYTES["in_place"]
+    if name == "in_place_separate":
+        return BATCH * CLASSIFY_BYTES["in_place"]
+    if name in ("records", "read_only"):  # lagged as well
+        return BATCH * PATH_BYTES[name]
+    if name == "c4_shard":
+        return C4_SHARD * CLASSIFY_BYTES["in_place"]
+    if name == "c3":
+        return BATCH * C3_BYTES["classify"]
+    if name == "c5":
+        return BATCH * C5_BYTES["classify"]
+    base = name.split("_multi")[0]
+    return MULTI_K * BATCH * CLASSIFY_BYTES[base]
+
+
+def pmc_traffic(timeout_s: int = 180):
     """HBM bytes per classify launch for each variant, measured now (MI355X_MICROARCH.md HBM
     section: FETCH_SIZE x2 on gfx950 for 16-B-per-lane streaming reads, WRITE_SIZE as read; both in
     KB).  The child (`--pmc-child`) runs PMC_WARMUP + PMC_STEPS launches of each variant in order."""
     if shutil.which("rocprofv3") is None:
         return {"error": "rocprofv3 not found"}
     env = dict(os.environ, TMPDIR="/tmp")
-    vals = {}
+    vals, names = {}, []
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"nbg_pmc_{counter}_", dir="/tmp")
         cmd = ["timeout", "-k", "5", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", counter, "--kernel-trace",
@@ -276,32 +313,27 @@ def pmc_traffic(timeout_s: int = 150):
             shutil.rmtree(d, ignore_errors=True)
             return {"error": f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr[-300:]}"}
         try:
-            vals[counter] = _pmc_rows(d, counter)
+            vals[counter], names = _pmc_rows(d, counter)
         finally:
             shutil.rmtree(d, ignore_errors=True)
     seg = PMC_WARMUP + PMC_STEPS
     out = {"counters": "FETCH_SIZE x2 + WRITE_SIZE (separate rocprofv3 --pmc passes, KB = 1024 B)",
            "launches_per_variant": PMC_STEPS}
-    for k, name in enumerate(PMC_VARIANTS):
+    order = list(PMC_ORDER) + [f"{v}_multi{MULTI_K}" for v in PMC_MULTI]
+    for k, name in enumerate(order):
         f = vals["FETCH_SIZE"][k * seg + PMC_WARMUP:(k + 1) * seg]
         w = vals["WRITE_SIZE"][k * seg + PMC_WARMUP:(k + 1) * seg]
         if len(f) != PMC_STEPS or len(w) != PMC_STEPS:
+            if k >= len(PMC_ORDER):
+                break  # no multi-batch launches in this run
             return {"error": f"unexpected classify dispatch count ({len(vals['FETCH_SIZE'])}, "
-                             f"{len(vals['WRITE_SIZE'])})"}
+                             f"{len(vals['WRITE_SIZE'])}) at {name}"}
         rd, wr = 2.0 * float(np.mean(f)), float(np.mean(w))
+        alg = _pmc_algorithmic(name)
+        kname = names[k * seg + PMC_WARMUP] if len(names) > k * seg + PMC_WARMUP else ""
         out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
-                     "algorithmic_bytes": BATCH * CLASSIFY_BYTES[name],
-                     "ratio": round((rd + wr) / (BATCH * CLASSIFY_BYTES[name]), 3)}
-    base = len(PMC_VARIANTS) * seg
-    for k, name in enumerate(PMC_MULTI):
-        f = vals["FETCH_SIZE"][base + k * seg + PMC_WARMUP:base + (k + 1) * seg]
-        w = vals["WRITE_SIZE"][base + k * seg + PMC_WARMUP:base + (k + 1) * seg]
-        if len(f) != PMC_STEPS or len(w) != PMC_STEPS:
-            break  # no multi-batch launches in this run
-        rd, wr = 2.0 * float(np.mean(f)), float(np.mean(w))
-        alg = MULTI_K * BATCH * CLASSIFY_BYTES[name]
-        out[f"{name}_multi{MULTI_K}"] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
-                                         "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3)}
+                     "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
+                     "kernel": kname.split("(")[0].replace("void nbg::(anonymous namespace)::", "")}
     return out
 
 
@@ -363,6 +395,7 @@ def launch(args, argv) -> int:
             for k, v in line.get("variants", {}).items():
                 if k in pmc and isinstance(v, dict):
                     v["traffic"] = pmc[k]["hbm_bytes"]
+                    v["kernel"] = pmc[k]["kernel"]
     print(json.dumps(line), flush=True)
     return 0
 
@@ -423,32 +456,64 @@ def run_rank(args) -> None:
         dbufs.append(torch.from_numpy(buf).to(dev) if gpu else torch.from_numpy(buf))
     log(f"[rank {rank}] traces ready in {time.time() - t0:.1f}s")
 
+    S = args.streams
     if gpu:
-        mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(args.streams)]
-        streams = [torch.cuda.Stream(dev) for _ in range(args.streams)]
-        outs = [dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
-                     perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
-                     counts=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev))
-                for _ in range(args.streams)]
-        recs = [torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) for _ in range(args.streams)]
+        from netbricks_amd._lib import lib as clib
 
-    def variant_kw(variant, j):
-        if variant == "records":
-            return dict(swap_macs=True, mac_out=recs[j])
-        return dict(swap_macs=variant == "in_place")
+        mgs = [nb.Maglev(lut=lut, n_backends=N_BACKENDS, device=local) for _ in range(S)]
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        # two output sets per stream: with NBG_GROUP_LAG a batch's backend[] is read by the next
+        # call's launch (which groups it) while that launch writes its own batch's backend[]
+        outs = [[dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                      perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                      counts=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(2)]
+                for _ in range(S)]
+        recs = [[torch.empty(BATCH * 12, dtype=torch.uint8, device=dev) for _ in range(2)] for _ in range(S)]
+        classify = clib.nbg_maglev_classify_device_ex
+        finish = clib.nbg_maglev_finish_group
+        hs = [m._h for m in mgs]
+        sts = [s.cuda_stream for s in streams]
+        pk = [d.data_ptr() for d in dbufs]
+        optr = [[(o["backend"].data_ptr(), o["perm"].data_ptr(), o["counts"].data_ptr()) for o in os_] for os_ in outs]
+        rptr = [[r.data_ptr() for r in rs] for rs in recs]
 
-    def step(i, variant="in_place"):
-        if not gpu:
-            return  # selftest: the launcher / process-group / timing logic without HIP
-        j = i % args.streams
-        mgs[j].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME,
-                        stream=streams[j].cuda_stream, **variant_kw(variant, j), **outs[j])
+    def issue(j, k, par, variant, lag, stream=None, n=BATCH, pkts=None, defer=False):
+        """One batch through the C-ABI on handle / stream j, output set par (prebuilt arguments: the
+        timed loop pays one ctypes call per batch)."""
+        flags = ((NBG_SWAP_MACS if variant != "read_only" else 0) | (NBG_GROUP_LAG if lag else 0)
+                 | (NBG_DEFER_GROUP if defer else 0))
+        be, pm, ct = optr[j][par]
+        rc = classify(hs[j], pk[k] if pkts is None else pkts, None, None, SLOT, FRAME, n, flags, be, pm, ct,
+                      rptr[j][par] if variant == "records" else None, sts[j] if stream is None else stream)
+        if rc:
+            raise RuntimeError(f"nbg_maglev_classify_device_ex: {rc}: {nb._lib.last_error()}")
 
-    def timed(variant, steps, warmup, barrier=False):
-        for i in range(warmup):
-            step(i, variant)
-        sync_all()
+    def finish_all(stream=None):
+        for j in range(S):
+            rc = finish(hs[j], sts[j] if stream is None else stream)
+            if rc:
+                raise RuntimeError(f"nbg_maglev_finish_group: {rc}: {nb._lib.last_error()}")
+
+    def rotation(step, variant, lag, n=BATCH, shard=None):
+        """One step: BATCHES_PER_STEP batches round-robin over the streams (global batch index g
+        picks the handle g % S and, per handle, alternating output sets)."""
+        for q in range(BATCHES_PER_STEP):
+            g = step * BATCHES_PER_STEP + q
+            j = g % S
+            if shard is None:
+                issue(j, g % N_BATCHES, (g // S) & 1, variant, lag)
+            else:  # C4 shard: packets of shard (g mod 64) of the 8 batches
+                s = g % (N_BATCHES * 8)
+                issue(j, 0, (g // S) & 1, variant, lag, n=n, pkts=pk[s // 8] + (s % 8) * n * SLOT)
+
+    def timed(variant, steps, warmup, lag, barrier=False, **kw):
+        """Whole-job time of `steps` rotations; every rotating batch is warmed first (at least one
+        rotation, whatever --warmup says), and lagged groups are finished inside the timed region."""
         if gpu:
+            for i in range(max(1, warmup)):
+                rotation(i, variant, lag, **kw)
+            finish_all()
+            sync_all()
             for m in mgs:
                 m.check()
         if barrier and world > 1:
@@ -460,8 +525,10 @@ def run_rank(args) -> None:
             for st in streams:
                 st.wait_event(start_ev)
         t_start = time.perf_counter()
-        for i in range(steps):
-            step(i, variant)
+        if gpu:
+            for i in range(steps):
+                rotation(i, variant, lag, **kw)
+            finish_all()
         sync_all()
         el = time.perf_counter() - t_start
         if barrier and world > 1:
@@ -471,32 +538,43 @@ def run_rank(args) -> None:
                 m.check()
         return el
 
-    def kernel_pass(variant, steps):
-        """Classify kernel alone: single stream, HIP events around each launch on the stream it
-        runs on; the grouping is deferred and launched after the stop event."""
-        st = streams[0]
-        kt, gt = KernelTimer(steps), KernelTimer(steps)
-        for i in range(steps):
-            kt.start(i, st.cuda_stream)
-            mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME, defer_group=True,
-                            stream=st.cuda_stream, **variant_kw(variant, 0), **outs[0])
-            kt.stop(i, st.cuda_stream)
-            gt.start(i, st.cuda_stream)
-            mgs[0].finish_group(st.cuda_stream)
-            gt.stop(i, st.cuda_stream)
+    def kernel_pass(variant, launches, lag, n=BATCH, shard=False):
+        """The classify launch alone: single stream, HIP events around each launch on the stream it
+        runs on.  lag: each launch classifies batch i and groups batch i-1 (the first launch, which
+        has nothing to group, is left out of the average).  Otherwise the grouping is deferred and
+        launched after the stop event."""
+        st = sts[0]
+        kt = KernelTimer(launches + 1)
+        gt = None if lag else KernelTimer(launches + 1)
+        for i in range(launches + 1):
+            pkts = pk[(i // 8) % N_BATCHES] + (i % 8) * n * SLOT if shard else None
+            kt.start(i, st)
+            issue(0, i % N_BATCHES, i & 1, variant, lag, stream=st, n=n, pkts=pkts, defer=not lag)
+            kt.stop(i, st)
+            if not lag:
+                gt.start(i, st)
+                finish(hs[0], st)
+                gt.stop(i, st)
+        finish(hs[0], st)
         sync_all()
-        c_ms, g_ms = kt.ms(), gt.ms()
+        c_ms = kt.ms()[1:]
+        g_ms = gt.ms()[1:] if gt else None
         kt.close()
-        gt.close()
-        ach = BATCH * CLASSIFY_BYTES[variant] / (c_ms.mean() / 1e3) / 1e9
-        return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
-                "frac": round(ach / HBM_PEAK_GBPS, 4), "group_kernel_avg_us": round(g_ms.mean() * 1e3, 2)}
+        if gt:
+            gt.close()
+        bpp = PATH_BYTES[variant] if lag else CLASSIFY_BYTES[variant]
+        ach = n * bpp / (c_ms.mean() / 1e3) / 1e9
+        r = {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
+             "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_pkt": bpp, "pkts_per_launch": n}
+        if g_ms is not None:
+            r["group_kernel_avg_us"] = round(g_ms.mean() * 1e3, 2)
+        return r
 
     # ---- several batches per launch (nbg_maglev_classify_device_multi): MULTI_K batches of 1M in
     #      one streaming-classify launch and one group launch, each batch with its own outputs
     m_arrs = {}
     if gpu and world == 1 and not args.no_variants and not args.no_multi and N_BATCHES % MULTI_K == 0:
-        from netbricks_amd._lib import NbgBatch, lib as clib
+        from netbricks_amd._lib import NbgBatch
         m_outs = [(torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
                    torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(N_BATCHES)]
         for g0 in range(N_BATCHES // MULTI_K):
@@ -508,8 +586,8 @@ def run_rank(args) -> None:
             m_arrs[g0] = arr
 
     def mcall(i, variant, stream, defer=False, j=0):
-        flags = (1 if variant == "in_place" else 0) | (0x10 if defer else 0)  # NBG_SWAP_MACS, NBG_DEFER_GROUP
-        rc = clib.nbg_maglev_classify_device_multi(mgs[j]._h, m_arrs[i % len(m_arrs)], MULTI_K, SLOT, FRAME, flags,
+        flags = (NBG_SWAP_MACS if variant == "in_place" else 0) | (NBG_DEFER_GROUP if defer else 0)
+        rc = clib.nbg_maglev_classify_device_multi(hs[j], m_arrs[i % len(m_arrs)], MULTI_K, SLOT, FRAME, flags,
                                                    stream)
         if rc:
             raise RuntimeError(f"nbg_maglev_classify_device_multi: {rc}")
@@ -517,9 +595,9 @@ def run_rank(args) -> None:
     def multi_pass(variant, calls, warmup):
         """Whole-job rate with MULTI_K batches per call on MULTI_STREAMS streams (distinct batch
         groups in flight), then the multi classify kernel alone (events, grouping deferred)."""
-        ms = min(MULTI_STREAMS, len(m_arrs), args.streams)
-        for i in range(warmup):
-            mcall(i, variant, streams[i % ms].cuda_stream, j=i % ms)
+        ms = min(MULTI_STREAMS, len(m_arrs), S)
+        for i in range(max(warmup, len(m_arrs))):
+            mcall(i, variant, sts[i % ms], j=i % ms)
         sync_all()
         start_ev = torch.cuda.Event()
         start_ev.record(torch.cuda.current_stream(dev))
@@ -527,16 +605,16 @@ def run_rank(args) -> None:
             st.wait_event(start_ev)
         t1 = time.perf_counter()
         for i in range(calls):
-            mcall(i, variant, streams[i % ms].cuda_stream, j=i % ms)
+            mcall(i, variant, sts[i % ms], j=i % ms)
         sync_all()
         el = time.perf_counter() - t1
-        st = streams[0]
+        st = sts[0]
         kt = KernelTimer(calls)
         for i in range(calls):
-            kt.start(i, st.cuda_stream)
-            mcall(i, variant, st.cuda_stream, defer=True)
-            kt.stop(i, st.cuda_stream)
-            mgs[0].finish_group(st.cuda_stream)
+            kt.start(i, st)
+            mcall(i, variant, st, defer=True)
+            kt.stop(i, st)
+            finish(hs[0], st)
         sync_all()
         c_ms = kt.ms()
         kt.close()
@@ -552,94 +630,214 @@ def run_rank(args) -> None:
                         "kernel and one group launch (nbg_maglev_classify_device_multi); every batch keeps its own "
                         "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
 
-    if args.multi_only:  # profiling run: only the multi-batch passes
-        print(json.dumps({f"{v}_multi{MULTI_K}": multi_pass(v, max(args.steps // MULTI_K, 10), 3)
-                          for v in ("read_only", "in_place")}), flush=True)
-        return
+    # ---- configs C3 / C5 (IMIX descriptors): handles, traces and one call per batch
+    imix = {}
 
-    if args.pmc_child:  # under rocprofv3 --pmc: each variant's launches in a fixed order
-        for v in PMC_VARIANTS:
+    def imix_setup():
+        if imix:
+            return imix
+        routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
+        bufs, offs, lens = [], [], []
+        for b in range(IMIX_BATCHES):
+            buf, off, ln = nb.make_trace(BATCH, 1, seed=1000 + b)
+            bufs.append(torch.from_numpy(buf).to(dev))
+            offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
+            lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
+        imix.update(bufs=bufs, offs=offs, lens=lens,
+                    c3=[nb.Maglev([f"be{i}" for i in range(1000)], 655373, device=local) for _ in range(S)],
+                    lpm=nb.Lpm(routes["reference"] + routes["mixed"], device=local),
+                    gates=[torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(S)],
+                    c3out=[dict(backend=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                                perm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                                counts=torch.empty(1001, dtype=torch.uint32, device=dev)) for _ in range(S)])
+        return imix
+
+    def imix_issue(cfg, g, j, stream=None, defer=False):
+        x = imix
+        k = g % IMIX_BATCHES
+        st = sts[j] if stream is None else stream
+        if cfg == "c3":
+            x["c3"][j].group_by(x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k], owned_windows=True,
+                                defer_group=defer, stream=st, **x["c3out"][j])
+        else:
+            nb.chain_lpm_maglev(mgs[j], x["lpm"], x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k],
+                                owned_windows=True, defer_group=defer, gate=x["gates"][j], stream=st,
+                                backend=outs[j][0]["backend"], perm=outs[j][0]["perm"], counts=outs[j][0]["counts"])
+
+    def imix_variant(cfg, steps, warmup):
+        """Config C3 (1000 backends / 655373, IMIX, MAC swap in place) or C5 (lpm -> maglev, IMIX):
+        whole-job rate on S streams (step = BATCHES_PER_STEP batches), then the classify kernel alone."""
+        imix_setup()
+        cm = imix["c3"] if cfg == "c3" else mgs
+        for i in range(max(1, warmup) * BATCHES_PER_STEP):
+            imix_issue(cfg, i, i % S)
+        sync_all()
+        start_ev = torch.cuda.Event()
+        start_ev.record(torch.cuda.current_stream(dev))
+        for st in streams:
+            st.wait_event(start_ev)
+        n_calls = steps * BATCHES_PER_STEP
+        t1 = time.perf_counter()
+        for i in range(n_calls):
+            imix_issue(cfg, i, i % S)
+        sync_all()
+        el = time.perf_counter() - t1
+        kt = KernelTimer(n_calls)
+        st = sts[0]
+        for i in range(n_calls):
+            kt.start(i, st)
+            imix_issue(cfg, i, 0, stream=st, defer=True)
+            kt.stop(i, st)
+            cm[0].finish_group(st)
+        sync_all()
+        for m in cm:
+            m.check()
+        kus = float(kt.ms().mean()) * 1e3
+        kt.close()
+        cb = (C3_BYTES if cfg == "c3" else C5_BYTES)
+        ach = BATCH * cb["classify"] / kus / 1e3
+        r = {"value": round(BATCH * n_calls / el / 1e6, 1), "unit": "Mpps",
+             "ms_per_batch": round(el / n_calls * 1e3, 5), "streams": S, "avg_launch_us": round(kus, 2),
+             "classify_bytes_per_pkt": cb["classify"], "path_bytes_per_pkt": cb["path"], "achieved": round(ach, 1),
+             "frac": round(ach / HBM_PEAK_GBPS, 4)}
+        if cfg == "c3":
+            r["what"] = ("C3: 1000 backends / 655373-slot u16 LUT (L2-gathered), 1M IMIX 7:4:1 frames per batch "
+                         "(u32 off + u16 len descriptors, owned 64-B windows), MAC swap in place + grouping "
+                         "(hist + scan + group kernels)")
+        else:
+            r["what"] = ("C5: test/lpm -> test/maglev fused in one classify kernel (DIR-24-8 of the reference's 105 "
+                         "routes + 902 mixed, tbl24 32 MiB), 65 backends / 65537, 1M IMIX frames per batch; the two MAC "
+                         "swaps cancel (read only); gate + backend + grouping")
+        return r
+
+    if args.pmc_child:  # under rocprofv3 --pmc: each variant's launches in a fixed order, one stream
+        st = sts[0]
+        for v in PMC_ORDER:
             for i in range(PMC_WARMUP + PMC_STEPS):
-                mgs[0].group_by(dbufs[i % N_BATCHES], BATCH, stride=SLOT, frame_len=FRAME,
-                                stream=streams[0].cuda_stream, **variant_kw(v, 0), **outs[0])
+                if v in ("in_place", "records", "read_only"):
+                    issue(0, i % N_BATCHES, i & 1, v, True, stream=st)
+                elif v == "in_place_separate":
+                    issue(0, i % N_BATCHES, i & 1, "in_place", False, stream=st)
+                elif v == "c4_shard":
+                    issue(0, 0, i & 1, "in_place", False, stream=st, n=C4_SHARD,
+                          pkts=pk[(i // 8) % N_BATCHES] + (i % 8) * C4_SHARD * SLOT)
+                else:
+                    if not imix:
+                        sync_all()
+                        imix_setup()
+                    imix_issue(v, i, 0, stream=st)
+            finish(hs[0], st)
             sync_all()
             mgs[0].check()
         if m_arrs:  # then the multi-batch launches (one classify dispatch per MULTI_K batches)
             for v in PMC_MULTI:
                 for i in range(PMC_WARMUP + PMC_STEPS):
-                    mcall(i, v, streams[0].cuda_stream)
+                    mcall(i, v, st)
                 sync_all()
                 mgs[0].check()
         return
 
+    if args.multi_only:  # profiling run: only the multi-batch passes
+        print(json.dumps({f"{v}_multi{MULTI_K}": multi_pass(v, max(args.steps * BATCHES_PER_STEP // MULTI_K, 10), 3)
+                          for v in ("read_only", "in_place")}), flush=True)
+        return
+
     # ---- timed region: K steps over all streams, bracketed by barrier + synchronize, max over ranks
-    elapsed_rank = timed("in_place", args.steps, args.warmup, barrier=True)
+    elapsed_rank = timed("in_place", args.steps, args.warmup, lag=True, barrier=True)
     per_rank_s = gather_floats(elapsed_rank)
     elapsed = max(per_rank_s)
+    # the same measurement at >= 50 steps (400 batches), in the same line: the K-step value is the
+    # steady-state rate when the two agree
+    steady = None
+    if gpu and args.steady_steps > 0:
+        st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=True, barrier=True)))
+        steady = {"steps": args.steady_steps,
+                  "value": round(BATCH * BATCHES_PER_STEP * args.steady_steps * world / st_el / 1e6, 1),
+                  "ms_per_step": round(st_el / args.steady_steps * 1e3, 5)}
 
     # ---- C4 scatter-inclusive pass (N > 1): every step rank 0 scatters world x 1M packets over
-    #      xGMI and each rank classifies its shard; reported beside the device-resident value
+    #      xGMI and each rank classifies its shard; reported beside the device-resident value.  A
+    #      failure here fails the job (exit code != 0), never a silent {"error"}.
     scatter = None
     if gpu and world > 1 and args.scatter_steps > 0:
-        try:
-            recv = torch.empty(BATCH * SLOT, dtype=torch.uint8, device=dev)
-            glob = torch.cat([dbufs[0]] + [torch.empty_like(dbufs[0]) for _ in range(world - 1)]) if rank == 0 else None
-            if rank == 0:
-                for r in range(1, world):  # rank 0 holds every rank's first shard (same seeds as the ranks own)
-                    buf_r, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(r, 0))
-                    glob[r * BATCH * SLOT:(r + 1) * BATCH * SLOT].copy_(torch.from_numpy(buf_r))
-            cur = torch.cuda.current_stream(dev).cuda_stream
-            gb = torch.empty(world * BATCH * 2, dtype=torch.uint8, device=dev) if rank == 0 else None
-            gc = torch.empty(world * (N_BACKENDS + 1), dtype=torch.int32, device=dev) if rank == 0 else None
+        recv = torch.empty(BATCH * SLOT, dtype=torch.uint8, device=dev)
+        glob = torch.cat([dbufs[0]] + [torch.empty_like(dbufs[0]) for _ in range(world - 1)]) if rank == 0 else None
+        if rank == 0:
+            for r in range(1, world):  # rank 0 holds every rank's first shard (same seeds as the ranks own)
+                buf_r, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(r, 0))
+                glob[r * BATCH * SLOT:(r + 1) * BATCH * SLOT].copy_(torch.from_numpy(buf_r))
+        cur = torch.cuda.current_stream(dev).cuda_stream
+        gb = torch.empty(world * BATCH * 2, dtype=torch.uint8, device=dev) if rank == 0 else None
+        gc = torch.empty(world * (N_BACKENDS + 1), dtype=torch.int32, device=dev) if rank == 0 else None
+        o0 = outs[0][0]
 
-            def sstep():
-                scatter_shard(glob, recv, rank, world)
-                mgs[0].group_by(recv, BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True, stream=cur, **outs[0])
-                gather_results(outs[0]["backend"], outs[0]["counts"], gb, gc, rank, world)
+        def sstep():
+            scatter_shard(glob, recv, rank, world)
+            mgs[0].group_by(recv, BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True, stream=cur, **o0)
+            gather_results(o0["backend"], o0["counts"], gb, gc, rank, world)
 
-            for _ in range(3):
-                sstep()
-            sync_all()
-            dist.barrier()
-            sync_all()
-            t1 = time.perf_counter()
-            for _ in range(args.scatter_steps):
-                sstep()
-            sync_all()
-            st_s = max(gather_floats(time.perf_counter() - t1))
-            if rank == 0 and int(gc.sum()) != world * BATCH:
-                raise RuntimeError(f"gathered counts sum {int(gc.sum())} != {world * BATCH}")
-            scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
-                       "ms_per_step": round(st_s / args.scatter_steps * 1e3, 4), "steps": args.scatter_steps,
-                       "root_egress_GBps": round(BATCH * SLOT * (world - 1) * args.scatter_steps / st_s / 1e9, 1),
-                       "what": "rank 0 scatters world x 1M 64-B packets (ncclScatter over xGMI), each rank classifies "
-                               "its shard (MAC swap + grouping), rank 0 gathers every shard's backend[] and counts "
-                               "(ncclGather); single stream per rank"}
-            del recv, glob, gb, gc
-        except Exception as e:  # informational; the device-resident value above stands on its own
-            log(f"[rank {rank}] scatter-inclusive pass failed: {e}")
-            scatter = {"error": str(e)[:200]}
+        for _ in range(3):
+            sstep()
+        sync_all()
+        dist.barrier()
+        sync_all()
+        t1 = time.perf_counter()
+        for _ in range(args.scatter_steps):
+            sstep()
+        sync_all()
+        st_s = max(gather_floats(time.perf_counter() - t1))
+        if rank == 0 and int(gc.sum()) != world * BATCH:
+            raise RuntimeError(f"gathered counts sum {int(gc.sum())} != {world * BATCH}")
+        scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
+                   "ms_per_step": round(st_s / args.scatter_steps * 1e3, 4), "steps": args.scatter_steps,
+                   "root_egress_GBps": round(BATCH * SLOT * (world - 1) * args.scatter_steps / st_s / 1e9, 1),
+                   "what": "rank 0 scatters world x 1M 64-B packets (ncclScatter over xGMI), each rank classifies "
+                           "its shard (MAC swap + grouping), rank 0 gathers every shard's backend[] and counts "
+                           "(ncclGather); single stream per rank"}
+        del recv, glob, gb, gc
 
-    # ---- roofline: the in-place classify kernel timed alone; labelled variants beside (N = 1)
+    # ---- roofline: the headline launch timed alone; labelled variants beside (N = 1)
     roof, variants = None, {}
     if gpu:
-        roof = kernel_pass("in_place", args.steps)
+        launches = args.steps * BATCHES_PER_STEP
+        roof = kernel_pass("in_place", launches, lag=True)
         if world == 1 and not args.no_variants:
+            el = timed("in_place", args.steps, args.warmup, lag=False)
+            variants["in_place_separate"] = {
+                "value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
+                "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
+                **kernel_pass("in_place", launches, lag=False),
+                "what": "round 2's path: classify launch + a separate group launch per batch, same streams"}
             for v in ("records", "read_only"):
-                el = timed(v, args.steps, args.warmup)
-                k = kernel_pass(v, args.steps)
-                variants[v] = {"value": round(BATCH * args.steps / el / 1e6, 1), "unit": "Mpps",
-                               "ms_per_step": round(el / args.steps * 1e3, 5),
+                el = timed(v, args.steps, args.warmup, lag=True)
+                variants[v] = {"value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
+                               "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
                                "classify_bytes_per_pkt": CLASSIFY_BYTES[v], "path_bytes_per_pkt": PATH_BYTES[v],
-                               **k}
-            variants["records"]["what"] = ("MAC swap written as dense 12-B egress records (packet bytes untouched) "
-                                           "+ grouping, same streams")
-            variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + grouping, "
-                                             "same streams")
+                               **kernel_pass(v, launches, lag=True)}
+            variants["records"]["what"] = ("MAC swap written as dense 12-B egress records (packet bytes untouched), "
+                                           "lagged grouping, same streams")
+            variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + lagged "
+                                             "grouping, same streams")
+            # config C4's per-GPU workload: 131,072-packet shards of the 8 batches (64 distinct)
+            el = timed("in_place", args.steps, args.warmup, lag=False, n=C4_SHARD, shard=True)
+            variants["c4_shard"] = {
+                "value": round(C4_SHARD * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
+                "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
+                **kernel_pass("in_place", launches, lag=False, n=C4_SHARD, shard=True),
+                "what": "C4's per-GPU shard: one 1M C2 batch in 8 contiguous 131,072-packet shards, each "
+                        "classified + grouped as one rank would (MAC swap in place), 64 distinct shards rotating "
+                        "on the same streams; below the streaming kernel's 262,144-packet threshold, so the "
+                        "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
             if m_arrs:
-                calls = max(args.steps // MULTI_K, 10)
+                calls = max(args.steps * BATCHES_PER_STEP // MULTI_K, 10)
                 for v in ("read_only", "in_place"):
-                    variants[f"{v}_multi{MULTI_K}"] = multi_pass(v, calls, max(args.warmup // MULTI_K, 3))
+                    variants[f"{v}_multi{MULTI_K}"] = multi_pass(v, calls, max(args.warmup, 3))
+            if not args.no_imix:
+                t0 = time.time()
+                imix_setup()
+                log(f"[rank {rank}] IMIX traces ready in {time.time() - t0:.1f}s")
+                variants["c3"] = imix_variant("c3", args.steps, args.warmup)
+                variants["c5"] = imix_variant("c5", args.steps, args.warmup)
 
     if rank == 0:
         cpu = None
@@ -648,7 +846,7 @@ def run_rank(args) -> None:
                 cpu = cpu_baseline(host_bufs, lut)
             except Exception as e:  # the baseline is informational; never fail the bench on it
                 log(f"cpu baseline failed: {e}")
-        total_pkts = BATCH * args.steps * world
+        total_pkts = BATCH * BATCHES_PER_STEP * args.steps * world
         line = {
             "metric": "Mpps + HBM GB/s device-resident Maglev (64B pkts)",
             "value": round(total_pkts / elapsed / 1e6, 1),
@@ -657,6 +855,7 @@ def run_rank(args) -> None:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "ms_per_batch": round(elapsed / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -665,27 +864,32 @@ def run_rank(args) -> None:
             "config": {"workload": "C2: Maglev 65 backends / 65537-slot LUT, 64B synthetic UDP, "
                                    "1M-packet device-resident batch per GPU",
                        "backends": N_BACKENDS, "table_size": TABLE, "batch_pkts": BATCH, "slot_bytes": SLOT,
-                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "mac_swap": "in place",
-                       "group_by": "perm + counts", "streams": args.streams, "parallelism": f"shard{world}"},
-            "per_gpu_mpps": [round(BATCH * args.steps / s / 1e6, 1) for s in per_rank_s],
+                       "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "batches_per_step": BATCHES_PER_STEP,
+                       "mac_swap": "in place", "group_by": "perm + counts (NBG_GROUP_LAG: batch i grouped inside "
+                                                           "batch i+1's launch; the last by finish_group, timed)",
+                       "streams": S, "parallelism": f"shard{world}"},
+            "per_gpu_mpps": [round(BATCH * BATCHES_PER_STEP * args.steps / s / 1e6, 1) for s in per_rank_s],
             "lut_digest": digest,
             "lut_digest_per_rank": digests,
-            "hbm_gbps_per_gpu": round(BATCH * PATH_BYTES["in_place"] * args.steps / elapsed / 1e9, 1),
+            "hbm_gbps_per_gpu": round(total_pkts / world * PATH_BYTES["in_place"] / elapsed / 1e9, 1),
             "hbm_bytes_per_pkt": PATH_BYTES["in_place"],
+            "aggregate_frac": aggregate_frac(total_pkts, elapsed, PATH_BYTES["in_place"], world),
         }
+        if steady is not None:
+            steady["ratio"] = round(line["value"] / steady["value"], 4)
+            line["steady_state"] = steady
         if roof is not None:
             line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": roof["frac"], "traffic": None,
-                                "kernel": "classify_stream_kernel<F4,HIST,in place> (LDS LUT, LDS-DMA tile ring)",
-                                "bytes_per_pkt": CLASSIFY_BYTES["in_place"], "pkts_per_launch": BATCH,
+                                "kernel": "classify_stream_kernel<F4,HIST,in place,7> (LDS LUT, LDS-DMA tile ring, "
+                                          "lagged grouping of the previous batch)",
+                                "bytes_per_pkt": roof["bytes_per_pkt"], "pkts_per_launch": BATCH,
                                 "avg_launch_us": roof["avg_launch_us"],
-                                "group_kernel_avg_us": roof["group_kernel_avg_us"],
-                                "timing": "single-stream pass, HIP events around each classify launch (grouping "
-                                          "deferred); `value` is the multi-stream rate, where the grouping of one "
-                                          "batch overlaps the classify of the next",
+                                "timing": "single-stream pass, HIP events around each launch (classify batch i + "
+                                          "group batch i-1); `value` is the multi-stream rate",
                                 "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts), "
-                                        "so the physical traffic is ~1.7x the 78 algorithmic bytes and this variant's "
-                                        "frac is capped near 0.46 by the measured read+rewrite ceiling with nt loads "
+                                        "so the physical traffic is ~1.7x the algorithmic bytes and this launch's frac "
+                                        "is capped near 0.48 by the measured read+rewrite ceiling with nt loads "
                                         "(DESIGN.md section 5); variants.read_only / read_only_multi4 are north_star's "
                                         "parse + hash + lookup"}
         if variants:
@@ -706,6 +910,10 @@ def run_rank(args) -> None:
     if gpu:
         for m in mgs:
             m.close()
+        for m in imix.get("c3", []):
+            m.close()
+        if imix:
+            imix["lpm"].close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -713,12 +921,15 @@ def run_rank(args) -> None:
 def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=50, help="timed steps (one step = one rotation over the 8 batches)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--streams", type=int, default=3)
+    ap.add_argument("--steady-steps", type=int, default=50,
+                    help="also time this many steps (same line, `steady_state`); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-variants", action="store_true", help="skip the records / read-only variant passes")
+    ap.add_argument("--no-variants", action="store_true", help="skip the variant passes")
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-batch variants")
+    ap.add_argument("--no-imix", action="store_true", help="skip configs C3 / C5")
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")

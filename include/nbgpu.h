@@ -21,7 +21,12 @@
  *
  * Threading: a handle is used by one thread / one stream at a time (the
  * reference runs one pipeline per pinned scheduler core, scheduler/context.rs:55-69).
- * Use one handle per concurrent stream.
+ * Use one handle per concurrent stream.  A handle remembers the stream of its
+ * last call: a later call on another stream is ordered after the work issued
+ * there (an event recorded on it), and nbg_maglev_check synchronises it.  So
+ * the stream a call names must stay valid until the handle's next call
+ * returns, or until nbg_maglev_destroy (destroy a per-burst stream only after
+ * that).
  */
 #ifndef NBGPU_H
 #define NBGPU_H
@@ -61,6 +66,18 @@ extern "C" {
                                    streaming classify kernel (one block per CU, everything fetched by
                                    LDS-DMA).  Faster on one stream (C5 classify -5 %), slower when
                                    several streams share the GPU (it cannot co-run): DESIGN.md §4 */
+#define NBG_GROUP_LAG 0x80u     /* pipelined grouping for a producer that calls the handle back to back
+                                   (GroupByProducer::execute, operators/group_by.rs:43-55): the call
+                                   classifies its batch (backend[], MAC swap) and leaves the batch's
+                                   grouping pending; the handle's next classify call groups it inside
+                                   its own classify launch (or launches it first, when that call cannot
+                                   carry it), and nbg_maglev_finish_group launches it alone.  So
+                                   d_perm / d_counts of call i are complete once the work of call i+1
+                                   (or of finish_group) is, in stream order; the call's buffers must
+                                   stay untouched until then.  Carried for fixed 64-B-aligned slots,
+                                   >= 262144 packets, <= 255 backends, M <= 65537 and partitions x bins
+                                   within the direct-scan limit; other batches are grouped at once.
+                                   Not with NBG_DEFER_GROUP or in a graph capture. */
 
 typedef struct nbg_maglev nbg_maglev;
 
@@ -98,7 +115,7 @@ int nbg_maglev_reserve(nbg_maglev* h, uint64_t max_pkts);
  *   d_len      nullable u16 frame lengths (mbuf data_len); NULL => every frame is fixed_len
  *   n_pkts     packets in the batch, < 2^30
  *   flags      NBG_SWAP_MACS | NBG_LUT_LDS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP | NBG_LUT_TILED |
- *              NBG_STREAM_DESC
+ *              NBG_STREAM_DESC | NBG_GROUP_LAG
  *   d_backend  out, n_pkts u16: backend index, or NBG_SENTINEL
  *   d_perm     out (nullable), n_pkts u32: packet indices grouped by backend 0..n-1 then the
  *              sentinel group, ascending index inside each group (per-group FIFO order)
@@ -151,8 +168,9 @@ typedef struct nbg_batch {
 int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, uint32_t n_batches, uint32_t stride,
                                      uint16_t fixed_len, uint32_t flags, void* stream);
 
-/* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP on
- * `stream` (which must be ordered after that classify).  No-op when nothing is pending. */
+/* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP (or the pending
+ * group of the last NBG_GROUP_LAG call) on `stream`; a stream other than the handle's last one is
+ * ordered after it.  No-op when nothing is pending. */
 int nbg_maglev_finish_group(nbg_maglev* h, void* stream);
 
 /* Synchronise the handle's last stream and report any HIP error.  Not needed on the hot path. */

@@ -30,6 +30,7 @@ NBG_WB_PARTIAL = 0x8
 NBG_DEFER_GROUP = 0x10
 NBG_LUT_TILED = 0x20
 NBG_STREAM_DESC = 0x40
+NBG_GROUP_LAG = 0x80
 NBG_HOST_SLOTS = 3
 NBG_MAX_MULTI = 8
 NBG_TRACE_UNIQUE = 0x1

@@ -511,6 +511,69 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
   CPROBE(3)
 }
 
+// Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
+// SGPR-base + 32-bit VGPR-offset form (one VGPR per address instead of two).
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
+}
+__device__ __forceinline__ uint32_t ld_u16(const uint16_t* base, uint32_t byte_off) {
+  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
+}
+
+// Inclusive scan over the 64 lanes of a wave with DPP moves (no LDS round trips): shifts by
+// 1, 2, 4, 8 inside each 16-lane row, then row 0's / rows 0-1's totals broadcast into the rows
+// above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).  Lanes a move does not
+// write keep the `old` operand, 0.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false));
+  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false));
+  return x;
+}
+
+// Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
+// exclusive prefix and the total.
+template <uint32_t NT>
+__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t x = wave_incl_scan(v);
+  if (lane == 63u) s_wave[wave] = x;
+  lds_sync();
+  uint32_t wpre = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < NT / 64; ++w) {
+    const uint32_t t = s_wave[w];
+    if (w < wave) wpre += t;
+    tot += t;
+  }
+  lds_sync();
+  total = tot;
+  return wpre + x - v;
+}
+
+// Stable rank of this lane among the lanes of its wave with the same `bin` (valid lanes only), and
+// how many lanes hold that bin: one ballot per bin bit plus one for validity, no loop over lanes.
+template <int BITS>
+__device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32_t lane, uint32_t& rank,
+                                                uint32_t& count) {
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t mv = valid ? ~0u : 0u;
+  const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
+  uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
+#pragma unroll
+  for (int bit = 0; bit < BITS; ++bit) {
+    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
+    const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
+    elo &= ~(static_cast<uint32_t>(bb) ^ m);
+    ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
+  }
+  rank = __popc(elo & static_cast<uint32_t>(lt)) + __popc(ehi & static_cast<uint32_t>(lt >> 32));
+  count = __popc(elo) + __popc(ehi);
+}
+
 // ---- streaming classify (fixed 64-B-aligned slots, u8 LUT <= 65537 entries) -------------------
 //
 // One 512-thread block per CU (persistent).  The block stages the LUT in LDS once with LDS-DMA
@@ -752,13 +815,62 @@ __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const u
   return bin;
 }
 
+// 4 or 2 B per lane from `src` into LDS at m0 + lane * 4.
+__device__ __forceinline__ void glds4(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+__device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_ushort %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_base)
+      : "memory");
+}
+
+
+// Lagged grouping (NBG_GROUP_LAG, GB > 0: the multisplit's bin bits): besides classifying its batch,
+// the launch groups the handle's pending batch `lg` (classified by the previous launch, whose
+// partition rows are complete).  Block c owns partition c: a prologue sums the rows into the
+// partition's per-bin perm bases (group base + prefix over earlier partitions, as group_kernel's),
+// then at every unit step each wave ranks 64 packets of the next 512-packet piece of the partition
+// (ballot multisplit), the unit's existing LDS barrier publishes the per-wave bin counts, and every
+// lane stores perm[base + run + earlier waves' counts + rank] = its packet: the stable per-group FIFO
+// order of group_by.rs:46-51.  Pieces beyond the unit steps run after them.  A piece's backends
+// arrive by LDS-DMA with the tile of its step (counted in `seq`), so grouping never drains the tile
+// ring.  The launch then zeroes the lag histogram buffer the launch after next accumulates into
+// (three buffers rotate: classify into one, group from the previous one, zero the third).
+constexpr uint32_t kLagPiece = 64u * kStreamW;  // packets per piece (one 64-packet rank per wave)
+constexpr uint32_t kLagSlots = 3;                // backend pieces per wave: steps k, k+1, k+2
+
+// LDS words of the lag state past the block histograms (hstride = (nbins + 3) & ~3):
+// base[hs], tot[hs], run[2][hs], cnt[2][kStreamW][hs], then kStreamW * kLagSlots pieces of 64 dwords
+__host__ __device__ constexpr uint32_t lag_lds_words(uint32_t hstride) {
+  return hstride * (4u + 2u * kStreamW) + kStreamW * kLagSlots * 64u;
+}
+
 // MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
 // sb: the batches of this launch (one for nbg_maglev_classify_device; up to kMaxMulti for
 // nbg_maglev_classify_device_multi).  `a` carries what they share; per unit, the unit's batch
-// supplies pkts, n_pkts, backend, mac_out and part_hist (a view of `a`).
-template <bool F4, bool HIST, int MODE>
-__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a, StreamBatches sb) {
+// supplies pkts, n_pkts, backend, mac_out and part_hist (a view of `a`).  GB > 0: one batch, plus
+// the lagged grouping of lg (above).
+template <bool F4, bool HIST, int MODE, int GB = 0>
+__global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyArgs a, StreamBatches sb, LagGroup lg) {
   constexpr uint32_t kRow = stream_row_of<MODE>(), kTileLds = 64u * kRow;
+  static_assert(GB == 0 || HIST, "lagged grouping runs on the per-unit histogram barrier");
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -811,36 +923,177 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   load(nxt, 0);
   uint32_t* hist = hist_base;  // [2][hstride]
 
+  // lagged grouping state (GB > 0): this block's partition [pbeg, pend) of the pending batch, its
+  // 512-packet pieces, and the LDS words past the block histograms
+  uint32_t* g_base = hist_base + 2 * hstride;   // [hstride] perm base of every bin for this partition
+  uint32_t* g_tot = g_base + hstride;           // [hstride] prologue scratch: bin totals
+  uint32_t* g_run = g_tot + hstride;            // [2][hstride] bin counts of earlier pieces
+  uint32_t* g_cnt = g_run + 2 * hstride;        // [2][kStreamW][hstride] per-wave counts of a piece
+  uint32_t* g_bk = g_cnt + 2 * kStreamW * hstride;  // [kStreamW][kLagSlots][64] backends (one dword per lane)
+  const uint32_t bk_lds = GB > 0 ? __builtin_amdgcn_readfirstlane(lds_addr(g_bk + wave * kLagSlots * 64u)) : 0u;
+  const bool g_own = GB > 0 && b < lg.n_parts;  // block-uniform
+  const uint32_t pbeg = g_own ? b * lg.part_pkts : 0u;
+  const uint32_t pend = g_own ? min(pbeg + lg.part_pkts, lg.n_pkts) : 0u;
+  const uint32_t pieces = g_own && lg.perm ? (pend - pbeg + kLagPiece - 1) / kLagPiece : 0u;
+
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
   // waves (the device LUT is padded to whole pieces); the first tiles go out behind them
 #if NBG_SABL == 1  // measurement build: no LUT staging (wrong backends; timing only)
-  const uint32_t pieces = 0;
+  const uint32_t pieces_lut = 0;
 #else
-  const uint32_t pieces = a.lut_lds_bytes >> 10;
+  const uint32_t pieces_lut = a.lut_lds_bytes >> 10;
 #endif
   const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
   // the LUT pieces first, then the first tiles (measured: tiles first, or the LUT through registers
   // off the LDS-DMA path, are both ~0.8 us slower per launch)
-  for (uint32_t q = wave; q < pieces; q += kStreamW)
+  for (uint32_t q = wave; q < pieces_lut; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
   // VM operations this wave issued after the LUT pieces (tile loads, and a lower bound of its
   // stores): waiting for tile k is vmcnt(seq - its count), so the stores issued after a tile do not
   // make the wait for it stricter (vmcnt counts stores too)
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // counts after tiles k, k+1, k+2
+  // lagged grouping: piece q's 64 backends of this wave, one dword per lane (a 2-B LDS-DMA fills a
+  // dword), into slot q % kLagSlots; issued just before the tile of step q, so waiting for that
+  // tile covers it.  One instruction (counted) when the wave has packets in the piece.
+  auto issue_piece = [&](uint32_t q) {
+    if constexpr (GB > 0) {
+      const uint32_t i0 = pbeg + q * kLagPiece + wave * 64u;
+      if (q < pieces && i0 < pend) {
+        const uint32_t i = min(i0 + lane, pend - 1u);
+        glds2(lg.backend + i, bk_lds + (q % kLagSlots) * 256u);
+        ++seq;
+      }
+    }
+  };
   for (uint32_t k = 0; k < first; ++k) {
     const uint32_t u = b + k * G;
     seek(nxt, u);
+    issue_piece(k);
     issue_tile<kRow, MODE != 2>(nxt.v, first_pkt(nxt, u), ring_lds + k * kTileLds, lane);
     seq += 4;
     (k == 0 ? sA : (k == 1 ? sB : sC)) = seq;
   }
   if constexpr (HIST)
     for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
+  if constexpr (GB > 0) {
+    // Prologue: this partition's per-bin perm base (group base + prefix over earlier partitions),
+    // summed straight from the pending batch's L2/MALL-resident partition rows (group_kernel's
+    // direct scan).  Its loads are ordinary ones, so the compiler's wait for them also waits for
+    // the LUT pieces and first tiles issued above (in-order retirement): the unit loop needs both.
+    __shared__ uint32_t s_wave[kStreamW];
+    const bool pro = g_own && (lg.perm || b == 0);  // block-uniform; counts come from block 0
+    if (pro) {
+      for (uint32_t i = tid; i < hstride; i += kStreamNT) {
+        g_base[i] = 0;
+        g_tot[i] = 0;
+        g_run[i] = 0;
+      }
+      lds_sync();
+      const uint32_t c = b;
+      if (lg.hist16) {
+        const uint32_t hw = (nbins + 1) >> 1;
+        const uint32_t L = hw >= kStreamNT ? 1u : kStreamNT / hw;
+        for (uint32_t t = tid; t < hw * L; t += kStreamNT) {
+          const uint32_t w = t % hw, j = t / hw;
+          uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
+          constexpr uint32_t kU = 24;
+          for (uint32_t q0 = j; q0 < lg.n_parts; q0 += kU * L) {
+            uint32_t h[kU];
+#pragma unroll
+            for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(lg.part_hist, (min(q0 + k * L, lg.n_parts - 1u) * hw + w) * 4u);
+#pragma unroll
+            for (uint32_t k = 0; k < kU; ++k) {
+              const uint32_t q = q0 + k * L;
+              const uint32_t lo = q < lg.n_parts ? h[k] & 0xffffu : 0u, hi = q < lg.n_parts ? h[k] >> 16 : 0u;
+              all_lo += lo;
+              all_hi += hi;
+              pre_lo += q < c ? lo : 0u;
+              pre_hi += q < c ? hi : 0u;
+            }
+          }
+          if (pre_lo) atomicAdd(&g_base[2 * w], pre_lo);
+          if (all_lo) atomicAdd(&g_tot[2 * w], all_lo);
+          if (2 * w + 1 < nbins) {
+            if (pre_hi) atomicAdd(&g_base[2 * w + 1], pre_hi);
+            if (all_hi) atomicAdd(&g_tot[2 * w + 1], all_hi);
+          }
+        }
+      } else {
+        const uint32_t L = nbins >= kStreamNT ? 1u : kStreamNT / nbins;
+        for (uint32_t t = tid; t < nbins * L; t += kStreamNT) {
+          const uint32_t bn = t % nbins, j = t / nbins;
+          uint32_t pre = 0, all = 0;
+          constexpr uint32_t kU = 40;
+          for (uint32_t q0 = j; q0 < lg.n_parts; q0 += kU * L) {
+            uint32_t h[kU];
+#pragma unroll
+            for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(lg.part_hist, (min(q0 + k * L, lg.n_parts - 1u) * nbins + bn) * 4u);
+#pragma unroll
+            for (uint32_t k = 0; k < kU; ++k) {
+              pre += q0 + k * L < c ? h[k] : 0u;
+              all += q0 + k * L < lg.n_parts ? h[k] : 0u;
+            }
+          }
+          if (pre) atomicAdd(&g_base[bn], pre);
+          if (all) atomicAdd(&g_tot[bn], all);
+        }
+      }
+      lds_sync();
+      // group bases: exclusive scan of the totals over bins (<= 2^GB bins: <= 512 = one per thread)
+      static_assert((1u << GB) <= kStreamNT, "one bin per thread in the group-base scan");
+      const uint32_t t = tid < nbins ? g_tot[tid] : 0u;
+      uint32_t all;
+      const uint32_t gb = block_excl_scan_n<kStreamNT>(t, s_wave, all);
+      if (tid < nbins) {
+        if (c == 0 && lg.counts) lg.counts[tid] = t;
+        g_base[tid] += gb;
+      }
+    }
+  }
   // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
   // makes every wave's pieces visible to every wave
   wait_tile(first);
   lds_sync();
   SPROBE(1)
+
+  // lagged grouping of piece q, before (A) and after (C, D) the barrier that publishes its counts
+  uint32_t g_bin = 0, g_rank = 0;
+  bool g_valid = false;
+  auto piece_rank = [&](uint32_t q) {  // A: rank this wave's 64 packets, publish the wave's bin counts
+    if constexpr (GB > 0) {
+      const uint32_t i = pbeg + q * kLagPiece + wave * 64u + lane;
+      g_valid = i < pend;
+      const uint32_t raw = g_bk[(wave * kLagSlots + q % kLagSlots) * 64u + lane] & 0xffffu;
+      g_bin = g_valid ? (raw == NBG_SENTINEL ? a.nb : raw) : 0u;
+      uint32_t count;
+      wave_match_rank<GB>(g_bin, g_valid, lane, g_rank, count);
+      uint32_t* row = g_cnt + ((q & 1u) * kStreamW + wave) * hstride;
+      for (uint32_t j = lane; j < hstride; j += 64) row[j] = 0;
+      __builtin_amdgcn_wave_barrier();
+      if (g_valid) row[g_bin] = count;  // every lane of a bin stores the same count
+    }
+  };
+  auto piece_store = [&](uint32_t q) {  // C + D: perm stores; the next piece's running counts
+    if constexpr (GB > 0) {
+      const uint32_t* cq = g_cnt + (q & 1u) * kStreamW * hstride;
+      uint32_t pos = g_base[g_bin] + g_run[(q & 1u) * hstride + g_bin] + g_rank;
+#pragma unroll
+      for (uint32_t w = 0; w < kStreamW; ++w)
+        if (w < wave) pos += cq[w * hstride + g_bin];
+      // pos < n_pkts whenever the rows are consistent; the bound keeps a scratch bug from writing
+      // outside perm (the parity tests would see the wrong entries)
+      if (g_valid && pos < lg.n_pkts) lg.perm[pos] = pbeg + q * kLagPiece + wave * 64u + lane;
+      if (pbeg + q * kLagPiece + wave * 64u < pend) ++seq;  // lane 0 stored
+      if (wave == (q + kStreamW / 2) % kStreamW) {
+        for (uint32_t bn = lane; bn < nbins; bn += 64) {
+          uint32_t s = g_run[(q & 1u) * hstride + bn];
+#pragma unroll
+          for (uint32_t w = 0; w < kStreamW; ++w) s += cq[w * hstride + bn];
+          g_run[((q + 1) & 1u) * hstride + bn] = s;
+        }
+      }
+    }
+  };
 
   for (uint32_t k = 0; k < nt; ++k) {
     const uint32_t u = b + k * G;
@@ -865,6 +1118,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const uint32_t u2 = u + kRing * G;
       seek(nxt, u2);
+      issue_piece(k + kRing);
       issue_tile<kRow, MODE != 2>(nxt.v, first_pkt(nxt, u2), ring_lds + (k % kRing) * kTileLds, lane);
       seq += 4;
       sN = seq;
@@ -874,6 +1128,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
     if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
+    if (k < pieces) piece_rank(k);
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -891,6 +1146,18 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
         stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
+    if (k < pieces) piece_store(k);
+  }
+  if constexpr (GB > 0) {
+    // pieces beyond the unit steps (a pending batch larger than this one)
+    for (uint32_t q = nt; q < pieces; ++q) {
+      issue_piece(q);
+      wait_vm<0>();
+      piece_rank(q);
+      lds_sync();
+      piece_store(q);
+    }
+    for (uint32_t i = b * kStreamNT + tid; i < lg.zero_words; i += G * kStreamNT) lg.zero[i] = 0;
   }
 #ifdef NBG_SPROBE
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores retired
@@ -930,33 +1197,6 @@ template <int MODE>
 __host__ __device__ constexpr uint32_t desc_wave_lds() {
   return desc_ring_tiles<MODE>() * 64u * row_of<MODE>() + kDescRing * kDescLds + 3u * kGatherLds;
 }
-
-// 4 or 2 B per lane from `src` into LDS at m0 + lane * 4.
-__device__ __forceinline__ void glds4(const void* src, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dword %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
-      : "memory");
-}
-__device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_ushort %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
-      : "memory");
-}
-
 
 // A hashed tile waiting for its gather.
 struct DescTile {
@@ -1191,49 +1431,6 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
   }
 }
 
-// Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
-// SGPR-base + 32-bit VGPR-offset form (one VGPR per address instead of two).
-__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t byte_off) {
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
-}
-__device__ __forceinline__ uint32_t ld_u16(const uint16_t* base, uint32_t byte_off) {
-  return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
-}
-
-// Inclusive scan over the 64 lanes of a wave with DPP moves (no LDS round trips): shifts by
-// 1, 2, 4, 8 inside each 16-lane row, then row 0's / rows 0-1's totals broadcast into the rows
-// above (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3).  Lanes a move does not
-// write keep the `old` operand, 0.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false));
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false));
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false));
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false));
-  x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false));
-  return x;
-}
-
-// Block-wide exclusive scan of one value per thread (blocks of NT threads); returns the
-// exclusive prefix and the total.
-template <uint32_t NT>
-__device__ __forceinline__ uint32_t block_excl_scan_n(uint32_t v, uint32_t* s_wave, uint32_t& total) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t x = wave_incl_scan(v);
-  if (lane == 63u) s_wave[wave] = x;
-  lds_sync();
-  uint32_t wpre = 0, tot = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < NT / 64; ++w) {
-    const uint32_t t = s_wave[w];
-    if (w < wave) wpre += t;
-    tot += t;
-  }
-  lds_sync();
-  total = tot;
-  return wpre + x - v;
-}
-
 // Many backends: the partition histograms come from this kernel instead of the classify kernel
 // (whose per-block flush would cost about one global atomic per packet at ~1000 bins).  One
 // 512-thread block per partition counts its packets' backends in LDS and stores the whole row.
@@ -1359,26 +1556,6 @@ __global__ __launch_bounds__(kLookupNT) void tile_lookup_kernel(TileArgs a) {
     const uint64_t e = b[i];
     a.backend[static_cast<uint32_t>(e >> 32)] = tlut[static_cast<uint32_t>(e)];
   }
-}
-
-// Stable rank of this lane among the lanes of its wave with the same `bin` (valid lanes only), and
-// how many lanes hold that bin: one ballot per bin bit plus one for validity, no loop over lanes.
-template <int BITS>
-__device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32_t lane, uint32_t& rank,
-                                                uint32_t& count) {
-  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const uint32_t mv = valid ? ~0u : 0u;
-  const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
-  uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
-#pragma unroll
-  for (int bit = 0; bit < BITS; ++bit) {
-    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
-    const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
-    elo &= ~(static_cast<uint32_t>(bb) ^ m);
-    ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
-  }
-  rank = __popc(elo & static_cast<uint32_t>(lt)) + __popc(ehi & static_cast<uint32_t>(lt >> 32));
-  count = __popc(elo) + __popc(ehi);
 }
 
 // ---- small batches: classify + stable grouping in one launch -------------------------------------
@@ -1961,10 +2138,11 @@ int launch_mode(const ClassifyArgs& a, bool hist, int grid, size_t lds, hipStrea
   return hist ? launch_v<LUTM, false, true>(a, grid, lds, s) : launch_v<LUTM, false, false>(a, grid, lds, s);
 }
 
-template <bool F4, bool HIST>
-int launch_stream_mode(const ClassifyArgs& a, const StreamBatches& sb, int mode, int grid, size_t lds, hipStream_t s) {
-  auto fn = mode == 1 ? classify_stream_kernel<F4, HIST, 1>
-                      : (mode == 2 ? classify_stream_kernel<F4, HIST, 2> : classify_stream_kernel<F4, HIST, 0>);
+template <bool F4, bool HIST, int GB>
+int launch_stream_mode(const ClassifyArgs& a, const StreamBatches& sb, const LagGroup& lg, int mode, int grid,
+                       size_t lds, hipStream_t s) {
+  auto fn = mode == 1 ? classify_stream_kernel<F4, HIST, 1, GB>
+                      : (mode == 2 ? classify_stream_kernel<F4, HIST, 2, GB> : classify_stream_kernel<F4, HIST, 0, GB>);
   static bool attr_set[2][2][3] = {};
   if (!attr_set[F4][HIST][mode]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1972,7 +2150,7 @@ int launch_stream_mode(const ClassifyArgs& a, const StreamBatches& sb, int mode,
       return set_error(NBG_EIO, "streaming classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
     attr_set[F4][HIST][mode] = true;
   }
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a, sb);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), lds, s, a, sb, lg);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "streaming classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -2026,10 +2204,11 @@ size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
 
 }  // namespace
 
-size_t stream_lds(uint32_t nb, int mode) {
-  const size_t hwords = 2 * (((nb + 1) + 3) & ~3u);
+size_t stream_lds(uint32_t nb, int mode, bool lag) {
+  const uint32_t hstride = ((nb + 1) + 3) & ~3u;
   const size_t tile = 64u * (mode == 1 ? stream_row_of<1>() : stream_row_of<0>());
-  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + hwords * 4u;
+  const size_t words = 2 * hstride + (lag ? lag_lds_words(hstride) : 0u);
+  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + words * 4u;
 }
 
 int stream_waves_per_block() { return kStreamW; }
@@ -2051,13 +2230,40 @@ int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, 
 int launch_classify_stream_multi(const ClassifyArgs& a, const StreamBatches& sb, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;
   const int mode = !a.swap ? 0 : (a.mac_out ? 2 : 1);
-  const size_t lds = stream_lds(a.nb, mode);
+  const size_t lds = stream_lds(a.nb, mode, false);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  const LagGroup none{};
   if (a.m == 65537u)
-    return hist ? launch_stream_mode<true, true>(a, sb, mode, grid, lds, s)
-                : launch_stream_mode<true, false>(a, sb, mode, grid, lds, s);
-  return hist ? launch_stream_mode<false, true>(a, sb, mode, grid, lds, s)
-              : launch_stream_mode<false, false>(a, sb, mode, grid, lds, s);
+    return hist ? launch_stream_mode<true, true, 0>(a, sb, none, mode, grid, lds, s)
+                : launch_stream_mode<true, false, 0>(a, sb, none, mode, grid, lds, s);
+  return hist ? launch_stream_mode<false, true, 0>(a, sb, none, mode, grid, lds, s)
+              : launch_stream_mode<false, false, 0>(a, sb, none, mode, grid, lds, s);
+}
+
+int launch_classify_stream_lag(const ClassifyArgs& a, const LagGroup& lg, int grid, void* stream) {
+  const uint32_t nbins = a.nb + 1;
+  if (!a.part_hist || nbins > 512 || lg.n_parts > static_cast<uint32_t>(grid))
+    return set_error(NBG_EINVAL, "streaming classify (lagged group): %u bins, %u partitions on %d blocks", nbins,
+                     lg.n_parts, grid);
+  StreamBatches sb{};
+  sb.pkts[0] = a.pkts;
+  sb.backend[0] = a.backend;
+  sb.mac_out[0] = a.mac_out;
+  sb.part_hist[0] = a.part_hist;
+  sb.n_pkts[0] = a.n_pkts;
+  sb.unit_base[0] = 0;
+  sb.unit_base[1] = (((a.n_pkts + 63u) >> 6) + kStreamW - 1) / kStreamW;
+  sb.n = 1;
+  const int mode = !a.swap ? 0 : (a.mac_out ? 2 : 1);
+  const size_t lds = stream_lds(a.nb, mode, true);
+  if (lds > 160u * 1024u) return set_error(NBG_EINVAL, "streaming classify (lagged group): %zu B of LDS", lds);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const bool b7 = nbins <= 128;
+  if (a.m == 65537u)
+    return b7 ? launch_stream_mode<true, true, 7>(a, sb, lg, mode, grid, lds, s)
+              : launch_stream_mode<true, true, 9>(a, sb, lg, mode, grid, lds, s);
+  return b7 ? launch_stream_mode<false, true, 7>(a, sb, lg, mode, grid, lds, s)
+            : launch_stream_mode<false, true, 9>(a, sb, lg, mode, grid, lds, s);
 }
 
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {

@@ -82,6 +82,13 @@ struct nbg_maglev {
   ScanArgs pending_scan{};
   uint32_t pending_multi = 0;         // > 0: the deferred group is a multi-batch group launch
   GroupMulti pending_gm{};
+  // lagged grouping (NBG_GROUP_LAG): three rotating partition-histogram sets; a lagged classify
+  // accumulates into set lag_idx, groups the pending batch from the previous set and zeroes the third
+  bool pending_lag = false;           // the pending group is a lagged one (pending_args / pending_lg)
+  LagGroup pending_lg{};
+  uint32_t* d_part_lag = nullptr;     // [3][kMaxParts][nb+1] (on first use)
+  uint32_t lag_idx = 0;
+  uint32_t lag_dirty = 0;             // bit k: set k may hold counts (zeroed before it is accumulated into)
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
   bool issued = false;                // a launch has been issued on last_stream
   hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
@@ -224,7 +231,9 @@ void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_bin_base);
   (void)hipFree(h->d_sink);
   (void)hipFree(h->d_part_multi);
+  (void)hipFree(h->d_part_lag);
   (void)hipFree(h->d_counts);
+  h->d_part_lag = nullptr;
   h->d_part_hist = nullptr;
   h->d_part_graph = nullptr;
   h->d_part_prefix = nullptr;
@@ -516,13 +525,81 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
 
 namespace {
 
+// The pending lagged group (NBG_GROUP_LAG) as a group launch of its own on `s` (already ordered
+// after the handle's last launch).  Its rows live in the lag set it was classified into; the
+// standalone group kernel zeroes nothing there (the next lagged classify zeroes the sets).
+int flush_lag(nbg_maglev* h, hipStream_t s) {
+  h->pending = h->pending_lag = false;
+  return launch_group(h->pending_args, kScanDirect, s);
+}
+
+// A lagged classify (NBG_GROUP_LAG): the streaming kernel accumulates this batch's partition rows
+// into lag set k, groups the pending batch (fuse) from set k - 1, and zeroes set k + 1 (mod 3) for
+// the call after next; this batch becomes the pending one.
+int classify_lag(nbg_maglev* h, ClassifyArgs& a, bool fuse, uint32_t n_parts, uint32_t part_pkts, uint32_t* d_perm,
+                 uint32_t* d_counts, hipStream_t s) {
+  const uint32_t nbins = h->nb + 1;
+  const size_t set_words = static_cast<size_t>(kMaxParts) * nbins;
+  if (!h->d_part_lag) {
+    NBG_HIP(hipMalloc(&h->d_part_lag, 3 * set_words * sizeof(uint32_t)));
+    NBG_HIP(hipMemsetAsync(h->d_part_lag, 0, 3 * set_words * sizeof(uint32_t), s));
+    h->lag_dirty = 0;
+    h->lag_idx = 0;
+  }
+  const uint32_t k = h->lag_idx, z = (k + 1) % 3;
+  uint32_t* setk = h->d_part_lag + k * set_words;
+  if (h->lag_dirty & (1u << k)) {  // only after an unusual call sequence: the rotation zeroes ahead
+    NBG_HIP(hipMemsetAsync(setk, 0, set_words * sizeof(uint32_t), s));
+    h->lag_dirty &= ~(1u << k);
+  }
+  a.part_hist = setk;
+  LagGroup lg = fuse ? h->pending_lg : LagGroup{};
+  lg.zero = h->d_part_lag + z * set_words;
+  lg.zero_words = static_cast<uint32_t>(set_words);
+  h->pending = h->pending_lag = false;
+  const int rc = launch_classify_stream_lag(a, lg, h->cus, s);
+  if (rc) return rc;
+  h->lag_dirty = (h->lag_dirty | (1u << k)) & ~(1u << z);
+  h->lag_idx = z;
+  LagGroup& p = h->pending_lg;
+  p = LagGroup{};
+  p.backend = a.backend;
+  p.perm = d_perm;
+  p.counts = d_counts ? d_counts : h->d_counts;
+  p.part_hist = setk;
+  p.n_pkts = a.n_pkts;
+  p.part_pkts = part_pkts;
+  p.n_parts = n_parts;
+  p.hist16 = a.hist16;
+  GroupArgs& ga = h->pending_args;
+  ga = GroupArgs{};
+  ga.backend = a.backend;
+  ga.n_pkts = a.n_pkts;
+  ga.nb = h->nb;
+  uint32_t bits = 0;
+  while ((1u << bits) < nbins) ++bits;
+  ga.bits = bits;
+  ga.n_parts = n_parts;
+  ga.part_pkts = part_pkts;
+  ga.part_hist = setk;
+  ga.hist16 = a.hist16;
+  ga.counts = p.counts;
+  ga.perm = d_perm;
+  ga.bin_base = h->d_bin_base;
+  h->pending = h->pending_lag = true;
+  return NBG_OK;
+}
+
 // One classify (+ grouping) launch; `lpm` non-null runs the chained test/lpm stage first.
 int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len, uint32_t stride,
                     uint16_t fixed_len, uint64_t n_pkts, uint32_t flags, uint16_t* d_backend, uint32_t* d_perm,
                     uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
                     uint16_t* d_gate, void* stream) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
-  if (h->pending) return set_error(NBG_EINVAL, "classify: a deferred group is pending (nbg_maglev_finish_group)");
+  if (h->pending && !h->pending_lag)
+    return set_error(NBG_EINVAL, "classify: a deferred group is pending (nbg_maglev_finish_group)");
+  if ((flags & NBG_GROUP_LAG) && (flags & NBG_DEFER_GROUP))
+    return set_error(NBG_EINVAL, "classify: NBG_GROUP_LAG with NBG_DEFER_GROUP");
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify: n_pkts must be < 2^30");
   if (n_pkts == 0) {
     if (d_counts) NBG_HIP(hipMemsetAsync(d_counts, 0, (h->nb + 1) * sizeof(uint32_t), (hipStream_t)stream));
@@ -548,8 +625,10 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   NBG_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap));
   const bool capturing = cap != hipStreamCaptureStatusNone;
-  if (capturing && (flags & NBG_DEFER_GROUP))
-    return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP cannot be captured in a graph");
+  if (capturing && (flags & (NBG_DEFER_GROUP | NBG_GROUP_LAG)))
+    return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP / NBG_GROUP_LAG cannot be captured in a graph");
+  if (capturing && h->pending)
+    return set_error(NBG_EINVAL, "classify: a lagged group is pending (nbg_maglev_finish_group before capturing)");
   if (capturing && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
     return set_error(NBG_EINVAL, "classify: only single-launch batches (<= 2048 packets, <= %u backends, 16-B aligned) "
                      "can be captured in a graph", kMaxGroupBins - 1);
@@ -574,10 +653,13 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const uint32_t n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
   uint32_t* part_cur = capturing ? h->d_part_graph : h->d_part_hist + static_cast<size_t>(h->parity) * kMaxParts * nbins;
   uint32_t* part_next = capturing ? nullptr : h->d_part_hist + static_cast<size_t>(h->parity ^ 1u) * kMaxParts * nbins;
+  const bool small = !lpm && use_small(n_pkts, nbins, flags, d_pkts);
 
-  if (d_off && !d_len) {
-    if (capturing && h->fixed_len_cap < n_pkts)
-      return set_error(NBG_EINVAL, "classify: make one call of this size before capturing it (no allocation in a graph)");
+  // Descriptor kernels read off[] and len[] both: offsets without lengths get a fixed_len-filled
+  // array.  The small kernel reads fixed_len itself, so a captured call (always the small path)
+  // never records this fill nor depends on the cached value (a captured fill, or a
+  // capture relying on the cache, went stale when an eager call changed fixed_len).
+  if (d_off && !d_len && !small) {
     if (h->fixed_len_cap < n_pkts) {
       (void)hipFree(h->d_fixed_len);
       h->d_fixed_len = nullptr;
@@ -634,7 +716,15 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     h->last_stream = static_cast<hipStream_t>(stream);
     h->issued = true;
   }
-  if (!lpm && use_small(n_pkts, nbins, flags, d_pkts)) {
+  // NBG_GROUP_LAG: this batch's grouping is left pending (carried by the next call's launch) when
+  // it takes the streaming kernel with in-kernel histograms and the direct scan; a pending lagged
+  // group rides on this launch when both fit, else it is launched alone first
+  const bool lag = (flags & NBG_GROUP_LAG) && !capturing && group && !lpm && !wide && !hist_k &&
+                   scan == kScanDirect && a.lean && !lds && !(flags & NBG_LUT_TILED) && !small &&
+                   use_stream(h, n_pkts) && n_parts <= static_cast<uint32_t>(h->cus);
+  const bool fuse = lag && h->pending_lag && h->pending_lg.n_parts <= static_cast<uint32_t>(h->cus);
+  if (h->pending_lag && !fuse && (rc = flush_lag(h, static_cast<hipStream_t>(stream)))) return rc;
+  if (small) {
     GroupArgs g{};
     g.perm = d_perm;
     g.counts = d_counts ? d_counts : (d_perm ? h->d_counts : nullptr);
@@ -677,6 +767,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
     if (capturing && a.part_hist)
       NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
+    if (lag) return classify_lag(h, a, fuse, n_parts, part_pkts, d_perm, d_counts, static_cast<hipStream_t>(stream));
     rc = launch_classify_stream(a, h->cus, stream);
   } else if (d_off && d_len && a.win_owned && !lds && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
              use_stream_desc(h, n_pkts, flags, lpm != nullptr, lpm || !a.swap ? 0 : (a.mac_out ? 2 : 1))) {
@@ -763,6 +854,10 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
     return set_error(NBG_EINVAL, "classify (multi): 1..%u batches", NBG_MAX_MULTI);
   if (flags & ~(NBG_SWAP_MACS | NBG_DEFER_GROUP))
     return set_error(NBG_EINVAL, "classify (multi): flags other than NBG_SWAP_MACS and NBG_DEFER_GROUP");
+  if (h->pending_lag) {  // a pending lagged group is launched alone first
+    const int rc = nbg_maglev_finish_group(h, stream);
+    if (rc) return rc;
+  }
   if (h->pending) return set_error(NBG_EINVAL, "classify (multi): a deferred group is pending (nbg_maglev_finish_group)");
   const bool group = batches[0].d_perm || batches[0].d_counts;
   uint64_t total = 0, max_n = 0;
@@ -947,10 +1042,11 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   if (!h) return set_error(NBG_EINVAL, "finish_group: null handle");
   if (!h->pending) return NBG_OK;
   DeviceGuard g(h->device);
-  h->pending = false;
   int rc = order_after_last(h, static_cast<hipStream_t>(stream));  // after the classify, on any stream
   if (rc) return rc;
   h->last_stream = static_cast<hipStream_t>(stream);
+  if (h->pending_lag) return flush_lag(h, static_cast<hipStream_t>(stream));
+  h->pending = false;
   if (h->pending_multi) {
     const uint32_t n = h->pending_multi;
     h->pending_multi = 0;
@@ -1066,7 +1162,8 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   if (!h || !ticket || (!pkt_ptrs && n) || (!lens && n) || (!backend_out && n))
     return set_error(NBG_EINVAL, "host_submit: null argument");
   if (n >= (1ull << 30)) return set_error(NBG_EINVAL, "host_submit: n must be < 2^30");
-  if (h->pending) return set_error(NBG_EINVAL, "host_submit: a deferred group is pending (nbg_maglev_finish_group)");
+  if (h->pending && !h->pending_lag)
+    return set_error(NBG_EINVAL, "host_submit: a deferred group is pending (nbg_maglev_finish_group)");
   DeviceGuard g(h->device);
   if (!h->host_compute) NBG_HIP(hipStreamCreateWithFlags(&h->host_compute, hipStreamNonBlocking));
   const uint64_t tk = h->next_ticket;
@@ -1113,7 +1210,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
       NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
       const bool group = perm_out || counts_out;
       rc = nbg_maglev_classify_device_ex(h, reg.dev, reinterpret_cast<const uint32_t*>(t.d_win), t.d_len, 0, 0, n,
-                                         (flags & ~NBG_DEFER_GROUP) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL, t.d_backend,
+                                         (flags & ~(NBG_DEFER_GROUP | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL, t.d_backend,
                                          perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr, nullptr, hs);
       if (rc) return rc;
       NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, hs));
@@ -1138,7 +1235,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
   const bool group = perm_out || counts_out;
   rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n,
-                                     (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL)) | NBG_OWNED_WINDOWS, t.d_backend,
+                                     (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS, t.d_backend,
                                      perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr,
                                      swap ? t.d_mac : nullptr, hs);
   if (rc) return rc;

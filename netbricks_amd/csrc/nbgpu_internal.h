@@ -89,6 +89,22 @@ struct StreamBatches {
   uint32_t n;
 };
 
+// NBG_GROUP_LAG: the handle's pending batch (classified by the previous launch) whose grouping rides
+// on this streaming-classify launch.  Block c groups partition c (n_parts <= grid), in 512-packet
+// pieces between its classify units.  n_parts == 0: nothing pending (the launch only zeroes).
+struct LagGroup {
+  const uint16_t* backend;    // the pending batch's backend[]
+  uint32_t* perm;             // nullable: counts only
+  uint32_t* counts;
+  const uint32_t* part_hist;  // its partition rows (written by the previous launch)
+  uint32_t* zero;             // nullable: the lag histogram buffer the launch after next accumulates into
+  uint32_t zero_words;
+  uint32_t n_pkts;
+  uint32_t part_pkts;
+  uint32_t n_parts;
+  uint32_t hist16;            // rows of two 16-bit bins per word
+};
+
 // NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
 struct TileArgs {
   const uint32_t* idx;      // [n_pkts] from the classify kernel (kIdx)
@@ -155,6 +171,10 @@ int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream);
 // The same over several batches (sb.n >= 1; a carries what they share)
 int launch_classify_stream_multi(const ClassifyArgs& a, const StreamBatches& sb, int grid, void* stream);
+// One batch (a.part_hist set) plus the grouping of the pending batch lg (NBG_GROUP_LAG); needs
+// lg.n_parts <= grid and (nb + 1) * lg.n_parts within the direct-scan limit (pick_group_scan)
+int launch_classify_stream_lag(const ClassifyArgs& a, const LagGroup& lg, int grid, void* stream);
+size_t stream_lds(uint32_t nb, int mode, bool lag);
 int stream_waves_per_block();
 // Streaming classify for descriptor layouts with owned windows (u8 LUT in LDS, or the u16 LUT
 // gathered from L2); stream_desc_lds: its dynamic LDS bytes (mode 0 read only, 1 in place, 2 records).

@@ -16,7 +16,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (NBG_DEFER_GROUP, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_MAX_MULTI, NBG_OWNED_WINDOWS,
+from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_MAX_MULTI, NBG_OWNED_WINDOWS,
                    NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
@@ -53,6 +53,13 @@ def _check_dev(name: str, t, dtype, min_size: int, device) -> None:
         raise ValueError(f"{name}: {t.numel()} elements, needs >= {min_size}")
     if t.device != device:
         raise ValueError(f"{name}: on {t.device}, expected {device}")
+
+
+def _slot_tail(stride: int, frame_len: int) -> int:
+    """Bytes the library may touch in the last fixed slot: slots of >= 64 B own their 64-B window
+    (read whole, and rewritten whole by the in-place swap: include/nbgpu.h), narrower slots only
+    their frame."""
+    return max(64, frame_len) if stride >= 64 else frame_len
 
 
 def build_lut(backends: Sequence[str], lut_size: int = 65537) -> np.ndarray:
@@ -148,6 +155,12 @@ class Maglev:
         _check_dev("lens", lens, torch.uint16, n_pkts, dev)
         if offsets is None or lens is None:
             raise ValueError("offsets and lens are required")
+        # the kernel reads (and may rewrite) the 64-B owned window at every offset, over PCIe: an
+        # offset past the registered region would touch host memory outside it (the C host_submit
+        # zero-copy path checks the same bound, nbgpu_api.hip)
+        if n_pkts and int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item()) + 64 \
+                > region.array.nbytes:
+            raise ValueError("offsets: a 64-B window past the end of the registered region")
         if backend is None:
             backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
         if group and perm is None:
@@ -170,12 +183,14 @@ class Maglev:
                  swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_lds: bool = False,
                  owned_windows: bool = False, wb_partial: bool = False,
                  defer_group: bool = False, lut_tiled: bool = False, stream_desc: bool = False,
+                 group_lag: bool = False,
                  backend=None, perm=None, counts=None, mac_out=None, stream=None) -> GroupedBatch:
         """Classify a device-resident batch (torch uint8 tensor on this device).
 
         Packet i starts at pkts[offsets[i]] (u32 tensor) or pkts[i*stride]; its length is
         lens[i] (u16 tensor) or frame_len.  Asynchronous on `stream` (default: torch's
-        current stream)."""
+        current stream).  group_lag=True (NBG_GROUP_LAG): perm / counts of this batch are
+        completed by the handle's next call (inside its classify launch) or by finish_group()."""
         import torch
 
         dev = pkts.device
@@ -183,7 +198,7 @@ class Maglev:
             raise ValueError("pkts: expected a contiguous uint8 tensor")
         if dev.type != "cuda" or dev.index != self.device:
             raise ValueError(f"pkts: on {dev}, expected cuda:{self.device}")
-        if offsets is None and n_pkts and (n_pkts - 1) * stride + min(frame_len, stride) > pkts.numel():
+        if offsets is None and n_pkts and (n_pkts - 1) * stride + _slot_tail(stride, frame_len) > pkts.numel():
             raise ValueError("pkts: smaller than n_pkts fixed slots")
         _check_dev("offsets", offsets, torch.uint32, n_pkts, dev)
         _check_dev("lens", lens, torch.uint16, n_pkts, dev)
@@ -203,7 +218,7 @@ class Maglev:
         flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_LUT_LDS if lut_lds else 0)
                  | (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_WB_PARTIAL if wb_partial else 0)
                  | (NBG_DEFER_GROUP if defer_group else 0) | (NBG_LUT_TILED if lut_tiled else 0)
-                 | (NBG_STREAM_DESC if stream_desc else 0))
+                 | (NBG_STREAM_DESC if stream_desc else 0) | (NBG_GROUP_LAG if group_lag else 0))
         rc = lib.nbg_maglev_classify_device_ex(self._h, _ptr(pkts), _ptr(offsets), _ptr(lens), stride, frame_len,
                                                n_pkts, flags, _ptr(backend), _ptr(perm) if scatter else None,
                                                _ptr(counts) if group else None, _ptr(mac_out), stream)
@@ -230,7 +245,7 @@ class Maglev:
                 raise ValueError(f"batch {j}: expected a contiguous uint8 tensor")
             if dev.type != "cuda" or dev.index != self.device:
                 raise ValueError(f"batch {j}: on {dev}, expected cuda:{self.device}")
-            if n_pkts and (n_pkts - 1) * stride + min(frame_len, stride) > pkts.numel():
+            if n_pkts and (n_pkts - 1) * stride + _slot_tail(stride, frame_len) > pkts.numel():
                 raise ValueError(f"batch {j}: smaller than n_pkts fixed slots")
             backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
             perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev) if group and scatter else None
@@ -247,7 +262,8 @@ class Maglev:
         return [g for g, _ in out] if not records else out
 
     def finish_group(self, stream=None) -> None:
-        """Launch the grouping kernel deferred by group_by(..., defer_group=True)."""
+        """Launch the grouping deferred by group_by(..., defer_group=True) or left pending by
+        group_by(..., group_lag=True)."""
         import torch
 
         if stream is None:

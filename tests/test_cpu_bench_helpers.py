@@ -27,9 +27,27 @@ def test_pmc_rows_filters_and_orders(tmp_path):
         w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
         for r in rows:
             w.writerow(r)
-    got = bench._pmc_rows(str(tmp_path / "pass"), "FETCH_SIZE")
+    got, names = bench._pmc_rows(str(tmp_path / "pass"), "FETCH_SIZE")
     assert got == [1.5 * 1024, 2.0 * 1024, 3.0 * 1024]
-    assert bench._pmc_rows(str(tmp_path / "pass"), "WRITE_SIZE") == [9.0 * 1024]
+    assert "classify_kernel<2" in names[1] and all("classify" in n for n in names)
+    assert bench._pmc_rows(str(tmp_path / "pass"), "WRITE_SIZE")[0] == [9.0 * 1024]
+
+
+def test_pmc_algorithmic_bytes():
+    """Per-launch algorithmic bytes of every PMC entry: lagged launches carry the
+    whole path (82 B: classify + the previous batch's perm), the others their classify bytes."""
+    assert bench._pmc_algorithmic("in_place") == bench.BATCH * 82
+    assert bench._pmc_algorithmic("in_place_separate") == bench.BATCH * 78
+    assert bench._pmc_algorithmic("read_only") == bench.BATCH * 70
+    assert bench._pmc_algorithmic("c4_shard") == 131072 * 78
+    assert bench._pmc_algorithmic("c3") == bench.BATCH * 84
+    assert bench._pmc_algorithmic("c5") == bench.BATCH * 78
+    assert bench._pmc_algorithmic(f"read_only_multi{bench.MULTI_K}") == bench.MULTI_K * bench.BATCH * 66
+
+
+def test_aggregate_frac():
+    # 8 GPUs at 40 Gpps each of 82 B/pkt: 3.28 TB/s per GPU of 8 TB/s
+    assert bench.aggregate_frac(8 * 40e9, 1.0, 82, 8) == round(40e9 * 82 / 1e9 / 8000.0, 4)
 
 
 def test_cpu_inventory_is_sane():
