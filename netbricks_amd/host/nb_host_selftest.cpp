@@ -87,6 +87,76 @@ int main(int argc, char** argv) {
     }
     EXPECT(threw);
   }
+  {
+    // The reference's drop on a full queue: one batch of 1500 packets that all land in group 0 of
+    // 1024-slot queues (mpsc_mbuf_queue.rs:261) keeps 1023 and loses 477 (enqueue_sp refuses,
+    // group_by.rs:50 ignores the refusal).
+    std::vector<nb::MBuf> m(1500);
+    std::vector<nb::MBuf*> batch;
+    std::vector<uint32_t> perm(m.size());
+    for (size_t i = 0; i < m.size(); ++i) {
+      m[i].storage.assign(64, 0);
+      batch.push_back(&m[i]);
+      perm[i] = static_cast<uint32_t>(i);
+    }
+    const uint32_t counts[3] = {1500, 0, 0};
+    std::vector<std::shared_ptr<nb::MpscQueue>> qs = {std::make_shared<nb::MpscQueue>(nb::kQueueSlots),
+                                                      std::make_shared<nb::MpscQueue>(nb::kQueueSlots)};
+    EXPECT(nb::admit_batch(qs, 1500, nb::Admission::kDropOnFull));
+    nb::EnqueueStats st;
+    nb::enqueue_grouped(batch.data(), perm.data(), counts, qs, st);
+    EXPECT(st.dropped == 477 && qs[0]->size() == 1023 && qs[1]->size() == 0);
+    nb::MBuf* out[32];
+    EXPECT(qs[0]->dequeue(out, 32) == 32 && out[0] == &m[0] && out[31] == &m[31]);  // the first 1023 kept, in order
+  }
+  {
+    // Capped batches with backpressure: batches of cap_batch() packets (whole bursts, <= 1023) are
+    // admitted only when every 1024-slot queue can take a whole batch, so even the worst case —
+    // every packet of every batch in one group, a consumer draining one 32-packet burst of one group
+    // per round (merge_batch.rs:44-57) — drops nothing and keeps FIFO order.  The same schedule with
+    // the reference's drop-on-full admission loses packets.
+    EXPECT(nb::cap_batch(4096) == 992 && nb::cap_batch(1023) == 992 && nb::cap_batch(100) == 96 &&
+           nb::cap_batch(10) == 32);
+    for (int mode = 0; mode < 2; ++mode) {
+      const auto adm = mode == 0 ? nb::Admission::kBackpressure : nb::Admission::kDropOnFull;
+      const uint32_t cap = nb::cap_batch(4096), total = 20000, groups = 3;
+      std::vector<nb::MBuf> m(total);
+      std::vector<std::shared_ptr<nb::MpscQueue>> qs;
+      for (uint32_t g = 0; g < groups; ++g) qs.push_back(std::make_shared<nb::MpscQueue>(nb::kQueueSlots));
+      nb::EnqueueStats st;
+      uint32_t next = 0, delivered = 0, which = 0;
+      std::vector<uint32_t> last_seen(groups, 0);
+      bool in_order = true;
+      for (int round = 0; round < 200000 && (next < total || delivered + st.dropped < total); ++round) {
+        if (next < total && nb::admit_batch(qs, cap, adm)) {
+          const uint32_t n = std::min(cap, total - next);
+          const uint32_t g = (next / cap) % 2;  // every packet of a batch in one group (0 or 1)
+          std::vector<nb::MBuf*> batch;
+          std::vector<uint32_t> perm(n);
+          for (uint32_t i = 0; i < n; ++i) {
+            m[next + i].port_seq = next + i + 1;
+            batch.push_back(&m[next + i]);
+            perm[i] = i;
+          }
+          uint32_t counts[4] = {0, 0, 0, 0};
+          counts[g] = n;
+          nb::enqueue_grouped(batch.data(), perm.data(), counts, qs, st);
+          next += n;
+        }
+        nb::MBuf* out[32];
+        const uint32_t got = qs[which]->dequeue(out, 32);
+        for (uint32_t i = 0; i < got; ++i) {
+          in_order &= out[i]->port_seq > last_seen[which];
+          last_seen[which] = static_cast<uint32_t>(out[i]->port_seq);
+        }
+        delivered += got;
+        which = (which + 1) % groups;
+      }
+      EXPECT(in_order);
+      if (mode == 0) EXPECT(st.dropped == 0 && delivered == total);
+      else EXPECT(st.dropped > 0 && delivered + st.dropped == total);
+    }
+  }
   if (argc > 2) {  // pcap round trip: argv[1] in, argv[2] out
     auto recs = nb::read_pcap(argv[1]);
     EXPECT(!recs.empty());

@@ -19,6 +19,7 @@
 // order — exactly what GroupByProducer::execute (group_by.rs:43-55) does packet by packet.
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstring>
@@ -262,24 +263,49 @@ class MaglevGroup {
   std::shared_ptr<nbg_maglev> h_;
 };
 
+// The group queues keep the reference's 1024 slots (new_mpsc_queue_pair, mpsc_mbuf_queue.rs:261-265;
+// 1023 usable), so one GPU batch may hold at most 1023 packets: then even a batch whose packets all
+// land in one group fits an empty queue.
+constexpr uint32_t kQueueSlots = 1024;
+constexpr uint32_t kMaxGpuBatch = kQueueSlots - 1;
+
+// When the producer pulls the next batch from its port.
+//   kBackpressure (default; a deliberate deviation): only when every group queue has room for a
+//     whole batch, so no packet is ever dropped — packets wait in the port (the NIC's RX ring), as
+//     they do in DPDK when a pipeline falls behind.
+//   kDropOnFull (the reference): always; a packet whose queue is full is lost (GroupByProducer
+//     ignores enqueue_one's result, group_by.rs:50; enqueue_sp refuses it, mpsc_mbuf_queue.rs:91-115).
+enum class Admission { kBackpressure, kDropOnFull };
+
+// Packets per GPU batch: at most kMaxGpuBatch, whole 32-packet bursts (receive_batch.rs:26).
+inline uint32_t cap_batch(uint32_t want) { return std::max(kBurst, std::min(want, kMaxGpuBatch) / kBurst * kBurst); }
+
+inline bool admit_batch(const std::vector<std::shared_ptr<MpscQueue>>& queues, uint32_t max_batch, Admission a) {
+  if (a == Admission::kDropOnFull) return true;
+  for (auto& q : queues)
+    if (q->free_slots() < max_batch) return false;
+  return true;
+}
+
 // GroupBy (group_by.rs:15-113) with the GPU producer: ct queues, get_group(i) for i < ct.  Packets
 // the reference would panic on (the would-panic sentinel group) are freed by the producer and
-// counted (would_panic()); everything else keeps the reference semantics.
+// counted (would_panic()); everything else keeps the reference semantics.  max_batch is capped at
+// kMaxGpuBatch (1023; 992 = 31 whole bursts) so that the reference's 1024-slot queues can always
+// take a batch.
 class GroupBy {
  public:
   GroupBy(ParsedMacBatch parent, uint32_t groups, MaglevGroup fn, StandaloneScheduler& sched,
-          uint32_t max_batch = 4096)
+          uint32_t max_batch = kMaxGpuBatch, Admission admission = Admission::kBackpressure)
       : groups_(groups) {
     if (groups != fn.backends()) throw std::invalid_argument("group_by: groups != Maglev backends");
-    // the reference's queues hold 1024 mbufs (mpsc_mbuf_queue.rs:261); a GPU batch of
-    // max_batch packets needs room for a whole batch in one group
-    uint32_t qsize = 1024;
-    while (qsize < 2 * max_batch) qsize <<= 1;
-    for (uint32_t i = 0; i < groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(qsize));
-    producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch);
+    if (max_batch == 0) throw std::invalid_argument("group_by: max_batch must be >= 1");
+    max_batch = cap_batch(max_batch);
+    for (uint32_t i = 0; i < groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(kQueueSlots));
+    producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch, admission);
     task_ = sched.add_task(producer_);
   }
   uint32_t len() const { return groups_; }
+  uint32_t max_batch() const { return producer_->max_batch; }
 
   // get_group(i): RestoreHeader over a ReceiveBatch of the group's MPSC consumer (group_by.rs:102-112).
   std::shared_ptr<RestoreHeader> get_group(uint32_t i) {
@@ -298,23 +324,21 @@ class GroupBy {
 
  private:
   struct Producer : Executable {
-    Producer(ParsedMacBatch p, MaglevGroup f, std::vector<std::shared_ptr<MpscQueue>> q, uint32_t max_batch)
-        : parent(std::move(p)), fn(std::move(f)), queues(std::move(q)), max_batch(max_batch) {}
+    Producer(ParsedMacBatch p, MaglevGroup f, std::vector<std::shared_ptr<MpscQueue>> q, uint32_t max_batch,
+             Admission admission)
+        : parent(std::move(p)), fn(std::move(f)), queues(std::move(q)), max_batch(max_batch), admission(admission) {}
     // GroupByProducer::execute (group_by.rs:43-55) for a whole batch: pull bursts until the
     // batch is full or the port is idle, classify on the GPU, enqueue in per-group FIFO order.
     void execute() override {
-      // backpressure: leave packets in the port (NIC ring) while a group could not absorb a
-      // whole batch, instead of pulling them and dropping on a full queue
-      for (auto& q : queues)
-        if (q->free_slots() < max_batch) return;
+      if (!admit_batch(queues, max_batch, admission)) return;
       std::vector<MBuf*> batch;
-      for (;;) {
+      for (;;) {  // whole bursts only: max_batch is a multiple of kBurst
         parent.parent->act();
         auto& b = parent.parent->pkts;
         batch.insert(batch.end(), b.begin(), b.end());
         const bool idle = b.size() < kBurst;
         parent.parent->done();
-        if (idle || batch.size() >= max_batch) break;
+        if (idle || batch.size() + kBurst > max_batch) break;
       }
       if (batch.empty()) return;
       const size_t n = batch.size();
@@ -337,6 +361,7 @@ class GroupBy {
     MaglevGroup fn;
     std::vector<std::shared_ptr<MpscQueue>> queues;
     uint32_t max_batch;
+    Admission admission;
     std::vector<uint8_t*> ptrs;
     std::vector<uint16_t> lens, backend;
     std::vector<uint32_t> perm, counts;
@@ -380,11 +405,12 @@ struct MaglevPipeline {
 
 inline MaglevPipeline maglev(std::shared_ptr<Batch> parent, StandaloneScheduler& s,
                              const std::vector<std::string>& backends, std::shared_ptr<PacketTx> port,
-                             uint64_t lut_size = 65537, uint32_t max_batch = 4096) {
+                             uint64_t lut_size = 65537, uint32_t max_batch = kMaxGpuBatch,
+                             Admission admission = Admission::kBackpressure) {
   const uint32_t ct = static_cast<uint32_t>(backends.size());
   MaglevGroup lut(backends, lut_size);  // Maglev::new(backends, 65537), nf.rs:90
   auto groups = std::make_shared<GroupBy>(transform(parse_mac(std::move(parent)), MacSwap{}), ct, lut, s,
-                                          max_batch);
+                                          max_batch, admission);
   std::vector<std::shared_ptr<Batch>> outs;
   for (uint32_t i = 0; i < ct; ++i) outs.push_back(groups->get_group(i));  // nf.rs:109
   auto tx = std::make_shared<MergeSend>(outs, std::move(port));

@@ -38,11 +38,11 @@ def read_pcap(path):
     return out
 
 
-def run_pipeline(tmp_path, frames, names, batch=4096, zero_copy=False):
+def run_pipeline(tmp_path, frames, names, batch=992, zero_copy=False, drop_on_full=False):
     rx, tx, order = tmp_path / "in.pcap", tmp_path / "out.pcap", tmp_path / "order.txt"
     write_pcap(rx, frames)
     args = [NB, "--rx", str(rx), "--tx", str(tx), "--order", str(order), "--batch", str(batch)]
-    args += ["--zero-copy", "1" if zero_copy else "0"]
+    args += ["--zero-copy", "1" if zero_copy else "0", "--drop-on-full", "1" if drop_on_full else "0"]
     args += ["--names", ",".join(names)]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
@@ -90,7 +90,9 @@ def test_lemmy_pcap_through_pipeline(torch_cuda, tmp_path, zero_copy):
 
 @pytest.mark.parametrize("batch,zero_copy", [(32, False), (4096, False), (4096, True)])
 def test_c1_10k_udp_pcap_65_backends(torch_cuda, tmp_path, batch, zero_copy):
-    """BASELINE config C1: 65 backends / 65537-slot table, 10k-packet UDP pcap."""
+    """BASELINE config C1: 65 backends / 65537-slot table, 10k-packet UDP pcap.  The group queues
+    keep the reference's 1024 slots; --batch 4096 is capped at 992 packets (whole bursts, <= 1023),
+    and the producer waits while a queue could not take a whole batch: nothing is dropped."""
     from netbricks_amd import make_trace
 
     buf, off, ln = make_trace(10000, 0, seed=2024)
@@ -99,3 +101,29 @@ def test_c1_10k_udp_pcap_65_backends(torch_cuda, tmp_path, batch, zero_copy):
     out, idx, stdout = run_pipeline(tmp_path, frames, names, batch=batch, zero_copy=zero_copy)
     check(frames, names, out, idx)
     assert '"dropped": 0' in stdout
+    assert f'"max_batch": {min(batch, 992)}' in stdout
+
+
+def test_c1_drop_on_full_keeps_reference_semantics(torch_cuda, tmp_path):
+    """--drop-on-full: the producer pulls a batch every round, as the reference's does, and a full
+    1024-slot queue loses the packet (group_by.rs:50, mpsc_mbuf_queue.rs:91-115).  With 3 groups and
+    the consumer draining one 32-packet burst per round, 10k packets overflow: what is sent is a
+    subset, each frame at most once, still in per-group FIFO order, and sent + dropped = received."""
+    import json
+
+    from netbricks_amd import make_trace
+
+    buf, off, ln = make_trace(10000, 0, seed=2025)
+    frames = [buf[o:o + l].tobytes() for o, l in zip(off, ln)]
+    names = ["Larry", "Curly", "Moe"]
+    out, idx, stdout = run_pipeline(tmp_path, frames, names, batch=992, drop_on_full=True)
+    st = json.loads(stdout)
+    assert st["dropped"] > 0 and st["tx"] + st["dropped"] + st["would_panic"] == st["rx"] == 10000
+    assert len(set(idx)) == len(idx) == st["tx"]
+    lut = orc.lut_build(names, 65537)
+    be = orc.classify(buf.copy(), 10000, lut, offs=off.astype(np.uint64), lens=ln)
+    last = {}
+    for i in idx:
+        g = int(be[i])
+        assert last.get(g, -1) < i
+        last[g] = i
