@@ -629,7 +629,13 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP / NBG_GROUP_LAG cannot be captured in a graph");
   if (capturing && h->pending)
     return set_error(NBG_EINVAL, "classify: a lagged group is pending (nbg_maglev_finish_group before capturing)");
-  if (capturing && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
+  // NBG_GRAPH_ANY=1 (diagnostic builds of the capture root-cause experiment, tools/gpu_graph_rootcause.sh):
+  // let multi-launch batches be captured too
+  static const bool graph_any = [] {
+    const char* e = std::getenv("NBG_GRAPH_ANY");
+    return e && std::atoi(e) != 0;
+  }();
+  if (capturing && !graph_any && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
     return set_error(NBG_EINVAL, "classify: only single-launch batches (<= 2048 packets, <= %u backends, 16-B aligned) "
                      "can be captured in a graph", kMaxGroupBins - 1);
   int rc = capturing ? NBG_OK : order_after_last(h, static_cast<hipStream_t>(stream));
