@@ -857,9 +857,10 @@ constexpr uint32_t kLagPiece = 64u * kStreamW;  // packets per piece (one 64-pac
 constexpr uint32_t kLagSlots = 3;                // backend pieces per wave: steps k, k+1, k+2
 
 // LDS words of the lag state past the block histograms (hstride = (nbins + 3) & ~3):
-// base[hs], tot[hs], run[2][hs], cnt[2][kStreamW][hs], then kStreamW * kLagSlots pieces of 64 dwords
+// base[hs], tot[hs], run[2][hs], cnt[2][kStreamW][hs], kStreamW * kLagSlots pieces of 64 dwords, and
+// the block scan's per-wave sums (dynamic LDS only: the kernel may take all 160 KiB)
 __host__ __device__ constexpr uint32_t lag_lds_words(uint32_t hstride) {
-  return hstride * (4u + 2u * kStreamW) + kStreamW * kLagSlots * 64u;
+  return hstride * (4u + 2u * kStreamW) + kStreamW * kLagSlots * 64u + kStreamW;
 }
 
 // MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
@@ -980,7 +981,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     // summed straight from the pending batch's L2/MALL-resident partition rows (group_kernel's
     // direct scan).  Its loads are ordinary ones, so the compiler's wait for them also waits for
     // the LUT pieces and first tiles issued above (in-order retirement): the unit loop needs both.
-    __shared__ uint32_t s_wave[kStreamW];
+    uint32_t* s_wave = g_bk + kStreamW * kLagSlots * 64u;  // [kStreamW]
     const bool pro = g_own && (lg.perm || b == 0);  // block-uniform; counts come from block 0
     if (pro) {
       for (uint32_t i = tid; i < hstride; i += kStreamNT) {
