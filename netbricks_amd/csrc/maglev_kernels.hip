@@ -111,11 +111,34 @@ __device__ __forceinline__ uint32_t lpm_lookup(const uint16_t* tbl24, const uint
   return (t & 0x8000u) ? tbl_long[((t & 0x7fffu) << 8) + (ip & 0xffu)] : t;
 }
 
+// One byte of global memory, loaded and waited for inside one asm statement: the compiler's wait
+// pass never sees it pending (see classify_slow's SYNC).
+__device__ __forceinline__ uint32_t ld_byte_sync(const uint8_t* p) {
+  uint32_t v;
+  asm volatile(
+      "global_load_ubyte %0, %1, off\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=v"(v)
+      : "v"(p)
+      : "memory");
+  return v;
+}
+
 // Byte-wise path: any alignment, any length, any IHL.  Returns the bin (nb = sentinel);
 // CHAIN also sets the lpm gate (sentinel when test/lpm cannot parse the packet).
-template <int LUTM, bool F4, bool CHAIN>
+// SYNC (the streaming kernels): every byte is read by ld_byte_sync.  Compiler-visible loads here
+// would stay pending, as far as the compiler's wait pass knows, across the unit loop's back-edge,
+// and it then puts vmcnt(0) waits on the main path wherever the register allocator reuses their
+// VGPRs, draining the LDS-DMA tile ring every step (measured: 2x per-step time in the lagged-
+// grouping kernel).  A synchronous byte load costs a full memory round trip, but only packets off
+// the fast path (none in the C2/C3/C5 traces) take this path.
+template <int LUTM, bool F4, bool CHAIN, bool SYNC = false>
 __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const uint8_t* lut_lds, uint8_t* p,
                                                   uint32_t len, uint32_t pkt, uint32_t& gate) {
+  auto rd = [](const uint8_t* x) -> uint32_t {
+    if constexpr (SYNC) return ld_byte_sync(x);
+    return *x;
+  };
   gate = kSentinel;
   if (len < kEth) return a.nb;  // Packet::parse_header assert (interface/packet.rs:392-399)
   const uint8_t* q = p + kEth;
@@ -124,27 +147,26 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
     // test/lpm: parse::<IpHeader> asserts payload_size >= 20 (packet.rs:392-399, ip.rs:53-56);
     // the gate is the group index of its group_by(lpm_groups) (test/lpm/src/nf.rs:216-221)
     if (plen < 20) return a.nb;
-    const uint32_t ip = (static_cast<uint32_t>(q[12]) << 24) | (q[13] << 16) | (q[14] << 8) | q[15];
+    const uint32_t ip = (rd(q + 12) << 24) | (rd(q + 13) << 16) | (rd(q + 14) << 8) | rd(q + 15);
     gate = lpm_lookup(a.tbl24, a.tbl_long, ip);
     if (gate >= a.lpm_groups) return a.nb;
   } else if (a.swap) {  // transform runs before group_by over the batch (chain: two swaps cancel)
     uint8_t* o = a.mac_out ? a.mac_out + static_cast<size_t>(pkt) * 12u : p;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const uint8_t d = p[k], s = p[k + 6];
+      const uint8_t d = static_cast<uint8_t>(rd(p + k)), s = static_cast<uint8_t>(rd(p + k + 6));
       o[k] = s;
       o[k + 6] = d;
     }
   }
   if (plen < 20) return a.nb;  // slice OOB in ipv4_extract_flow
-  const uint32_t ps = (q[0] & 0xfu) * 4u;
+  const uint32_t ps = (rd(q) & 0xfu) * 4u;
   if (plen < ps + 4) return a.nb;
-  const uint32_t src = q[12] | (q[13] << 8) | (q[14] << 16) | (static_cast<uint32_t>(q[15]) << 24);
-  const uint32_t dst = q[16] | (q[17] << 8) | (q[18] << 16) | (static_cast<uint32_t>(q[19]) << 24);
-  const uint32_t ports =
-      q[ps] | (q[ps + 1] << 8) | (q[ps + 2] << 16) | (static_cast<uint32_t>(q[ps + 3]) << 24);
+  const uint32_t src = rd(q + 12) | (rd(q + 13) << 8) | (rd(q + 14) << 16) | (rd(q + 15) << 24);
+  const uint32_t dst = rd(q + 16) | (rd(q + 17) << 8) | (rd(q + 18) << 16) | (rd(q + 19) << 24);
+  const uint32_t ports = rd(q + ps) | (rd(q + ps + 1) << 8) | (rd(q + ps + 2) << 16) | (rd(q + ps + 3) << 24);
   uint32_t lo, hi;
-  fnv_flow(lo, hi, src, dst, ports, q[9]);
+  fnv_flow(lo, hi, src, dst, ports, rd(q + 9));
   return lookup<LUTM, F4>(a, lut_lds, lo, hi);
 }
 
@@ -806,10 +828,13 @@ __device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uin
 template <bool F4>
 __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const uint8_t* lut, uint32_t p, uint32_t bin,
                                                   bool slow) {
+#ifdef NBG_EXP_NOSLOW
+  slow = false;
+#endif
   if (slow) {
     uint32_t gate;
-    bin = classify_slow<kLdsU8Tail, F4, false>(a, lut, a.pkts + static_cast<size_t>(p) * a.stride, a.fixed_len, p,
-                                               gate);
+    bin = classify_slow<kLdsU8Tail, F4, false, true>(a, lut, a.pkts + static_cast<size_t>(p) * a.stride, a.fixed_len,
+                                                     p, gate);
   }
   a.backend[p] = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
   return bin;
@@ -853,14 +878,18 @@ __device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
 // arrive by LDS-DMA with the tile of its step (counted in `seq`), so grouping never drains the tile
 // ring.  The launch then zeroes the lag histogram buffer the launch after next accumulates into
 // (three buffers rotate: classify into one, group from the previous one, zero the third).
+#ifndef NBG_LAG_ABL  // diagnostic ablations (wrong results): bit 0 no prologue, bit 1 no pieces in the
+#define NBG_LAG_ABL 0  // unit loop, bit 2 no perm stores
+#endif
 constexpr uint32_t kLagPiece = 64u * kStreamW;  // packets per piece (one 64-packet rank per wave)
 constexpr uint32_t kLagSlots = 3;                // backend pieces per wave: steps k, k+1, k+2
 
 // LDS words of the lag state past the block histograms (hstride = (nbins + 3) & ~3):
-// base[hs], tot[hs], run[2][hs], cnt[2][kStreamW][hs], kStreamW * kLagSlots pieces of 64 dwords, and
-// the block scan's per-wave sums (dynamic LDS only: the kernel may take all 160 KiB)
+// base[hs], tot[hs], run[2][hs], cnt[2][kStreamW][hs], pbs[2][hs] (a piece's bin starts),
+// kStreamW * kLagSlots pieces of 64 dwords, the block scan's per-wave sums, and srt[2][kLagPiece]
+// (pos, packet) pairs of a piece sorted by bin (dynamic LDS only: the kernel may take all 160 KiB)
 __host__ __device__ constexpr uint32_t lag_lds_words(uint32_t hstride) {
-  return hstride * (4u + 2u * kStreamW) + kStreamW * kLagSlots * 64u + kStreamW;
+  return hstride * (6u + 2u * kStreamW) + kStreamW * kLagSlots * 64u + kStreamW + 2u * kLagPiece * 2u;
 }
 
 // MODE: 0 = read only, 1 = MAC swap in place, 2 = swapped MACs as 12-B records (a.mac_out)
@@ -930,12 +959,34 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   uint32_t* g_tot = g_base + hstride;           // [hstride] prologue scratch: bin totals
   uint32_t* g_run = g_tot + hstride;            // [2][hstride] bin counts of earlier pieces
   uint32_t* g_cnt = g_run + 2 * hstride;        // [2][kStreamW][hstride] per-wave counts of a piece
-  uint32_t* g_bk = g_cnt + 2 * kStreamW * hstride;  // [kStreamW][kLagSlots][64] backends (one dword per lane)
+  uint32_t* g_pbs = g_cnt + 2 * kStreamW * hstride;  // [2][hstride] where each bin starts in a sorted piece
+  uint32_t* g_bk = g_pbs + 2 * hstride;         // [kStreamW][kLagSlots][64] backends (one dword per lane)
+  uint32_t* s_wave = g_bk + kStreamW * kLagSlots * 64u;  // [kStreamW] block scan
+  uint2* g_srt = reinterpret_cast<uint2*>(s_wave + kStreamW);  // [2][kLagPiece] (perm position, packet)
   const uint32_t bk_lds = GB > 0 ? __builtin_amdgcn_readfirstlane(lds_addr(g_bk + wave * kLagSlots * 64u)) : 0u;
   const bool g_own = GB > 0 && b < lg.n_parts;  // block-uniform
   const uint32_t pbeg = g_own ? b * lg.part_pkts : 0u;
   const uint32_t pend = g_own ? min(pbeg + lg.part_pkts, lg.n_pkts) : 0u;
   const uint32_t pieces = g_own && lg.perm ? (pend - pbeg + kLagPiece - 1) / kLagPiece : 0u;
+  const bool pro = !(NBG_LAG_ABL & 1) && g_own && (lg.perm || b == 0);  // block-uniform; counts from block 0
+
+  // Prologue loads (GB > 0): this partition's per-bin perm base (group base + prefix over earlier
+  // partitions) is summed straight from the pending batch's partition rows (group_kernel's direct
+  // scan): L threads per row word, each over rows j, j + L, ...  The first kPU rows of every thread
+  // are loaded here, before the LUT pieces and the first tiles, so they retire first: the compiler's
+  // waits for them (it does not see the LDS-DMA loads) never wait for the tile ring.
+  constexpr uint32_t kPU = GB > 0 ? 32u : 1u;
+  const uint32_t rw = lg.hist16 ? (nbins + 1) >> 1 : nbins;  // words per row
+  const uint32_t pL = rw >= kStreamNT ? 1u : kStreamNT / rw;
+  const uint32_t pw = tid % rw, pj = tid / rw;
+  const bool pthr = pro && tid < rw * pL;
+  uint32_t ph[kPU];
+  if constexpr (GB > 0) {
+    if (pthr) {
+#pragma unroll
+      for (uint32_t k = 0; k < kPU; ++k) ph[k] = ld_u32(lg.part_hist, (min(pj + k * pL, lg.n_parts - 1u) * rw + pw) * 4u);
+    }
+  }
 
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
   // waves (the device LUT is padded to whole pieces); the first tiles go out behind them
@@ -977,13 +1028,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   if constexpr (HIST)
     for (uint32_t i = tid; i < 2 * hstride; i += kStreamNT) hist[i] = 0;
   if constexpr (GB > 0) {
-    // Prologue: this partition's per-bin perm base (group base + prefix over earlier partitions),
-    // summed straight from the pending batch's L2/MALL-resident partition rows (group_kernel's
-    // direct scan).  Its loads are ordinary ones, so the compiler's wait for them also waits for
-    // the LUT pieces and first tiles issued above (in-order retirement): the unit loop needs both.
-    uint32_t* s_wave = g_bk + kStreamW * kLagSlots * 64u;  // [kStreamW]
-    const bool pro = g_own && (lg.perm || b == 0);  // block-uniform; counts come from block 0
-    if (pro) {
+    if (pro) {  // the sums, while the LUT pieces and the first tiles are in flight
       for (uint32_t i = tid; i < hstride; i += kStreamNT) {
         g_base[i] = 0;
         g_tot[i] = 0;
@@ -991,52 +1036,26 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       }
       lds_sync();
       const uint32_t c = b;
-      if (lg.hist16) {
-        const uint32_t hw = (nbins + 1) >> 1;
-        const uint32_t L = hw >= kStreamNT ? 1u : kStreamNT / hw;
-        for (uint32_t t = tid; t < hw * L; t += kStreamNT) {
-          const uint32_t w = t % hw, j = t / hw;
-          uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
-          constexpr uint32_t kU = 24;
-          for (uint32_t q0 = j; q0 < lg.n_parts; q0 += kU * L) {
-            uint32_t h[kU];
+      if (pthr) {
+        uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
+        auto add = [&](uint32_t q, uint32_t h) {
+          const uint32_t lo = !lg.hist16 ? h : (h & 0xffffu), hi = lg.hist16 ? h >> 16 : 0u;
+          const bool in = q < lg.n_parts;
+          all_lo += in ? lo : 0u;
+          all_hi += in ? hi : 0u;
+          pre_lo += in && q < c ? lo : 0u;
+          pre_hi += in && q < c ? hi : 0u;
+        };
 #pragma unroll
-            for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(lg.part_hist, (min(q0 + k * L, lg.n_parts - 1u) * hw + w) * 4u);
-#pragma unroll
-            for (uint32_t k = 0; k < kU; ++k) {
-              const uint32_t q = q0 + k * L;
-              const uint32_t lo = q < lg.n_parts ? h[k] & 0xffffu : 0u, hi = q < lg.n_parts ? h[k] >> 16 : 0u;
-              all_lo += lo;
-              all_hi += hi;
-              pre_lo += q < c ? lo : 0u;
-              pre_hi += q < c ? hi : 0u;
-            }
-          }
-          if (pre_lo) atomicAdd(&g_base[2 * w], pre_lo);
-          if (all_lo) atomicAdd(&g_tot[2 * w], all_lo);
-          if (2 * w + 1 < nbins) {
-            if (pre_hi) atomicAdd(&g_base[2 * w + 1], pre_hi);
-            if (all_hi) atomicAdd(&g_tot[2 * w + 1], all_hi);
-          }
-        }
-      } else {
-        const uint32_t L = nbins >= kStreamNT ? 1u : kStreamNT / nbins;
-        for (uint32_t t = tid; t < nbins * L; t += kStreamNT) {
-          const uint32_t bn = t % nbins, j = t / nbins;
-          uint32_t pre = 0, all = 0;
-          constexpr uint32_t kU = 40;
-          for (uint32_t q0 = j; q0 < lg.n_parts; q0 += kU * L) {
-            uint32_t h[kU];
-#pragma unroll
-            for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(lg.part_hist, (min(q0 + k * L, lg.n_parts - 1u) * nbins + bn) * 4u);
-#pragma unroll
-            for (uint32_t k = 0; k < kU; ++k) {
-              pre += q0 + k * L < c ? h[k] : 0u;
-              all += q0 + k * L < lg.n_parts ? h[k] : 0u;
-            }
-          }
-          if (pre) atomicAdd(&g_base[bn], pre);
-          if (all) atomicAdd(&g_tot[bn], all);
+        for (uint32_t k = 0; k < kPU; ++k) add(pj + k * pL, ph[k]);
+        for (uint32_t q = pj + kPU * pL; q < lg.n_parts; q += pL)  // rows past the first kPU (rare)
+          add(q, ld_u32(lg.part_hist, (q * rw + pw) * 4u));
+        const uint32_t b0 = lg.hist16 ? 2 * pw : pw;
+        if (pre_lo) atomicAdd(&g_base[b0], pre_lo);
+        if (all_lo) atomicAdd(&g_tot[b0], all_lo);
+        if (lg.hist16 && b0 + 1 < nbins) {
+          if (pre_hi) atomicAdd(&g_base[b0 + 1], pre_hi);
+          if (all_hi) atomicAdd(&g_tot[b0 + 1], all_hi);
         }
       }
       lds_sync();
@@ -1051,16 +1070,26 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       }
     }
   }
+  SPROBE(10)
   // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
   // makes every wave's pieces visible to every wave
   wait_tile(first);
   lds_sync();
   SPROBE(1)
 
-  // lagged grouping of piece q, before (A) and after (C, D) the barrier that publishes its counts
-  uint32_t g_bin = 0, g_rank = 0;
+  // Lagged grouping of piece q runs across three barriers, so that every barrier the unit loop already
+  // has carries it (sync point s = the loop step, then tail barriers):
+  //   before barrier q:  rank the wave's 64 packets (ballot multisplit), publish the wave's bin counts
+  //   after barrier q:   each packet's perm position (base + earlier pieces + earlier waves + rank);
+  //                      one wave: the next piece's running counts and this piece's bin starts (pbs)
+  //   after barrier q+1: each packet's slot in the piece sorted by bin (pbs + earlier waves + rank)
+  //   after barrier q+2: thread t stores sorted slot t: consecutive threads write consecutive perm
+  //                      entries of one bin (coalesced), where lane-order stores scattered every lane
+  uint32_t g_bin = 0, g_rank = 0;    // piece q (ranked, before barrier q)
   bool g_valid = false;
-  auto piece_rank = [&](uint32_t q) {  // A: rank this wave's 64 packets, publish the wave's bin counts
+  uint32_t p_pos = 0, p_bin = 0, p_pre = 0;  // piece q-1 (positioned, after barrier q-1)
+  bool p_valid = false;
+  auto piece_rank = [&](uint32_t q) {  // before barrier q
     if constexpr (GB > 0) {
       const uint32_t i = pbeg + q * kLagPiece + wave * 64u + lane;
       g_valid = i < pend;
@@ -1074,24 +1103,57 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if (g_valid) row[g_bin] = count;  // every lane of a bin stores the same count
     }
   };
-  auto piece_store = [&](uint32_t q) {  // C + D: perm stores; the next piece's running counts
+  auto piece_sync = [&](uint32_t s) {  // after barrier s
     if constexpr (GB > 0) {
-      const uint32_t* cq = g_cnt + (q & 1u) * kStreamW * hstride;
-      uint32_t pos = g_base[g_bin] + g_run[(q & 1u) * hstride + g_bin] + g_rank;
+      // piece s-2: coalesced stores of its sorted slots
+      if (s >= 2 && s - 2 < pieces) {
+        const uint32_t q = s - 2, n_q = min(pend - (pbeg + q * kLagPiece), kLagPiece);
+        const uint2 e = g_srt[(q & 1u) * kLagPiece + tid];
+        if (!(NBG_LAG_ABL & 4) && tid < n_q && e.x < lg.n_pkts) lg.perm[e.x] = e.y;
+        if (wave * 64u < n_q) ++seq;  // lane 0 stored
+      }
+      // piece s-1: its sorted slot
+      if (s >= 1 && s - 1 < pieces && p_valid) {
+        const uint32_t q = s - 1;
+        const uint32_t slot = g_pbs[(q & 1u) * hstride + p_bin] + p_pre;
+        g_srt[(q & 1u) * kLagPiece + slot] = make_uint2(p_pos, pbeg + q * kLagPiece + wave * 64u + lane);
+      }
+      // piece s: perm positions; one wave: running counts and bin starts
+      if (s < pieces) {
+        const uint32_t* cq = g_cnt + (s & 1u) * kStreamW * hstride;
+        uint32_t pre = g_rank;
 #pragma unroll
-      for (uint32_t w = 0; w < kStreamW; ++w)
-        if (w < wave) pos += cq[w * hstride + g_bin];
-      // pos < n_pkts whenever the rows are consistent; the bound keeps a scratch bug from writing
-      // outside perm (the parity tests would see the wrong entries)
-      if (g_valid && pos < lg.n_pkts) lg.perm[pos] = pbeg + q * kLagPiece + wave * 64u + lane;
-      if (pbeg + q * kLagPiece + wave * 64u < pend) ++seq;  // lane 0 stored
-      if (wave == (q + kStreamW / 2) % kStreamW) {
-        for (uint32_t bn = lane; bn < nbins; bn += 64) {
-          uint32_t s = g_run[(q & 1u) * hstride + bn];
+        for (uint32_t w = 0; w < kStreamW; ++w)
+          if (w < wave) pre += cq[w * hstride + g_bin];
+        p_pos = g_base[g_bin] + g_run[(s & 1u) * hstride + g_bin] + pre;
+        p_bin = g_bin;
+        p_pre = pre;
+        p_valid = g_valid;
+        if (wave == (s + kStreamW / 2) % kStreamW) {
+          constexpr uint32_t kB = (1u << GB) / 64u;  // consecutive bins per lane
+          uint32_t pc[kB], tot = 0;
 #pragma unroll
-          for (uint32_t w = 0; w < kStreamW; ++w) s += cq[w * hstride + bn];
-          g_run[((q + 1) & 1u) * hstride + bn] = s;
+          for (uint32_t i = 0; i < kB; ++i) {
+            const uint32_t bn = lane * kB + i;
+            uint32_t v = 0;
+            if (bn < nbins) {
+#pragma unroll
+              for (uint32_t w = 0; w < kStreamW; ++w) v += cq[w * hstride + bn];
+              g_run[((s + 1) & 1u) * hstride + bn] = g_run[(s & 1u) * hstride + bn] + v;
+            }
+            pc[i] = v;
+            tot += v;
+          }
+          uint32_t st = wave_incl_scan(tot) - tot;
+#pragma unroll
+          for (uint32_t i = 0; i < kB; ++i) {
+            const uint32_t bn = lane * kB + i;
+            if (bn < nbins) g_pbs[(s & 1u) * hstride + bn] = st;
+            st += pc[i];
+          }
         }
+      } else {
+        p_valid = false;
       }
     }
   };
@@ -1129,7 +1191,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
     if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
-    if (k < pieces) piece_rank(k);
+    if (!(NBG_LAG_ABL & 2) && k < pieces) piece_rank(k);
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -1147,16 +1209,21 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
         stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
-    if (k < pieces) piece_store(k);
+    if (!(NBG_LAG_ABL & 2)) piece_sync(k);
   }
   if constexpr (GB > 0) {
-    // pieces beyond the unit steps (a pending batch larger than this one)
-    for (uint32_t q = nt; q < pieces; ++q) {
-      issue_piece(q);
-      wait_vm<0>();
-      piece_rank(q);
-      lds_sync();
-      piece_store(q);
+    // sync points past the unit steps: pieces beyond them (a pending batch larger than this one),
+    // then the last two pieces' sorted slots and stores
+    if (!(NBG_LAG_ABL & 2)) {
+      for (uint32_t s = nt; s < pieces + 2; ++s) {
+        if (s < pieces) {
+          issue_piece(s);
+          wait_vm<0>();
+          piece_rank(s);
+        }
+        lds_sync();
+        piece_sync(s);
+      }
     }
     for (uint32_t i = b * kStreamNT + tid; i < lg.zero_words; i += G * kStreamNT) lg.zero[i] = 0;
   }

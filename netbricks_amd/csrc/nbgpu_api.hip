@@ -727,7 +727,8 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   // group rides on this launch when both fit, else it is launched alone first
   const bool lag = (flags & NBG_GROUP_LAG) && !capturing && group && !lpm && !wide && !hist_k &&
                    scan == kScanDirect && a.lean && !lds && !(flags & NBG_LUT_TILED) && !small &&
-                   use_stream(h, n_pkts) && n_parts <= static_cast<uint32_t>(h->cus);
+                   use_stream(h, n_pkts) && n_parts <= static_cast<uint32_t>(h->cus) &&
+                   stream_lds(h->nb, !a.swap ? 0 : (a.mac_out ? 2 : 1), true) <= 160u * 1024u;
   const bool fuse = lag && h->pending_lag && h->pending_lg.n_parts <= static_cast<uint32_t>(h->cus);
   if (h->pending_lag && !fuse && (rc = flush_lag(h, static_cast<hipStream_t>(stream)))) return rc;
   if (small) {

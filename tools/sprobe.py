@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--group", action="store_true", help="with grouping (the kernel's per-unit histogram barriers)")
+    ap.add_argument("--lag", action="store_true", help="NBG_GROUP_LAG: each launch also groups the previous batch")
     args = ap.parse_args()
     import torch
 
@@ -36,15 +37,21 @@ def main():
     mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
     n = args.n
     bufs = [torch.from_numpy(nb.make_trace(n, 0, seed=b + 5)[0]).to(dev) for b in range(8)]
-    be = torch.empty(n, dtype=torch.uint16, device=dev)
+    be = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(2)]
+    pm = [torch.empty(n, dtype=torch.uint32, device=dev) for _ in range(2)]
     rec = torch.empty(n * 12, dtype=torch.uint8, device=dev)
     for variant in ("read_only", "in_place", "records"):
         kw = dict(swap_macs=variant != "read_only")
         if variant == "records":
             kw["mac_out"] = rec
         for i in range(20):
-            mg.group_by(bufs[i % 8], n, group=args.group, backend=be, **kw)
-        torch.cuda.synchronize()
+            if args.lag:
+                mg.group_by(bufs[i % 8], n, group_lag=True, backend=be[i & 1], perm=pm[i & 1], **kw)
+            else:
+                mg.group_by(bufs[i % 8], n, group=args.group, backend=be[0], **kw)
+        torch.cuda.synchronize()  # the last launch's timeline (the finish_group launch is not probed)
+        if args.lag:
+            mg.finish_group()
         waves = 256 * 8
         raw = np.zeros(4096 * 12, dtype=np.uint64)
         assert fn(raw.ctypes.data, raw.size) == 0
@@ -53,6 +60,8 @@ def main():
         us = (t - t0) / 100.0  # 100 MHz -> us
         print(f"== {variant}: launch span {us[:, 11].max():.2f} us (first entry to last exit)")
         print(f"   entry        {pct(us[:, 0])}")
+        if args.lag:
+            print(f"   prologue done {pct(us[:, 10])}")
         print(f"   LUT visible  {pct(us[:, 1])}")
         for k in range(8):
             print(f"   tile {k} in    {pct(us[:, 2 + k])}")
