@@ -4,13 +4,13 @@
 Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,576 synthetic
 64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM, MAC swap in place.
 One step = one rotation over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache), i.e. 8
-batches, each through `nbg_maglev_classify_device_ex` with NBG_GROUP_LAG: the call classifies its
-batch and groups the handle's previous batch inside the same streaming launch (the reference's
-producer classifies and enqueues in one loop, operators/group_by.rs:43-55).  Batches are issued
-round-robin on `--streams` (default 3) HIP streams, one handle per stream (NetBricks runs one
-pipeline per RX queue, scheduler/context.rs:241-255); every handle's last pending group is
-launched by nbg_maglev_finish_group inside the timed region, so every batch of the K steps is
-fully classified and grouped between the two synchronisations.
+batches, each through one `nbg_maglev_classify_device_ex` call (streaming classify launch + group
+launch) made straight through ctypes with prebuilt arguments.  Batches are issued round-robin on
+`--streams` (default 3) HIP streams, one handle per stream (NetBricks runs one pipeline per RX
+queue, scheduler/context.rs:241-255), so one batch's latency-bound grouping overlaps the next
+batch's bandwidth-bound classify; every batch of the K steps is fully classified and grouped
+between the two synchronisations.  `variants.in_place_lag` is the same with NBG_GROUP_LAG (batch
+i grouped inside batch i+1's classify launch; measured slower).
 
 Process model.  `python bench.py --gpus N` is a launcher: it never touches the GPU, spawns N
 rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their environment),
@@ -20,12 +20,12 @@ owns its own batches (weak scaling, no data-path collective in the timed region)
 built on rank 0 and broadcast once over RCCL (setup, untimed).  `--selftest` runs the same
 launcher and rank logic on the CPU with gloo and no HIP call (the CPU test of the launcher).
 
-Roofline: the dominant kernel (the streaming classify launch, which at steady state also groups
-the previous batch) is timed with HIP events around each launch in a separate single-stream pass;
+Roofline: the dominant kernel (the streaming classify launch) is timed with HIP events around each
+launch in a separate single-stream pass (grouping deferred past the stop event);
 its HBM traffic is measured in the same invocation by two rocprofv3 --pmc passes (FETCH_SIZE,
-WRITE_SIZE) of a short child run, at N = 1.  Variants beside the headline: grouping as a separate
-launch (round 2's path), records / read-only, several batches per launch, config C4's per-GPU
-shard (131,072 packets per launch), and configs C3 / C5 (IMIX).
+WRITE_SIZE) of a short child run, at N = 1.  Variants beside the headline: lagged grouping,
+records / read-only, several batches per launch, config C4's per-GPU shard (131,072 packets per
+launch), and configs C3 / C5 (IMIX).
 
 Prints ONE JSON line (rank 0 / the launcher; see DESIGN.md "Measurement").
 """
@@ -75,7 +75,7 @@ C5_BYTES = {"classify": 64 + 6 + 2 + 2 + 4, "path": 64 + 6 + 2 + 2 + 4 + 4}  # g
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_WARMUP, PMC_STEPS = 10, 40
 # the child's launch sequence, one classify dispatch per call, in this order
-PMC_ORDER = ("in_place", "in_place_separate", "records", "read_only", "c4_shard", "c3", "c5")
+PMC_ORDER = ("in_place", "in_place_lag", "records", "read_only", "c4_shard", "c3", "c5")
 PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
 NBG_SWAP_MACS, NBG_DEFER_GROUP, NBG_GROUP_LAG = 0x1, 0x10, 0x80
 
@@ -279,12 +279,10 @@ def _pmc_rows(d, counter):
 
 def _pmc_algorithmic(name: str) -> int:
     """Algorithmic bytes of one launch of a PMC_ORDER / multi entry."""
-    if name == "in_place":  # lagged: classify this batch + group the previous one (steady state)
+    if name == "in_place_lag":  # lagged: classify this batch + group the previous one (steady state)
         return BATCH * PATH_BYTES["in_place"]
-    if name == "in_place_separate":
-        return BATCH * CLASSIFY_BYTES["in_place"]
-    if name in ("records", "read_only"):  # lagged as well
-        return BATCH * PATH_BYTES[name]
+    if name in ("in_place", "records", "read_only"):
+        return BATCH * CLASSIFY_BYTES[name]
     if name == "c4_shard":
         return C4_SHARD * CLASSIFY_BYTES["in_place"]
     if name == "c3":
@@ -333,7 +331,7 @@ def pmc_traffic(timeout_s: int = 180):
         kname = names[k * seg + PMC_WARMUP] if len(names) > k * seg + PMC_WARMUP else ""
         out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
                      "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
-                     "kernel": kname.split("(")[0].replace("void nbg::(anonymous namespace)::", "")}
+                     "kernel": kname.replace("void nbg::(anonymous namespace)::", "").split("(nbg::")[0]}
     return out
 
 
@@ -715,9 +713,9 @@ def run_rank(args) -> None:
         for v in PMC_ORDER:
             for i in range(PMC_WARMUP + PMC_STEPS):
                 if v in ("in_place", "records", "read_only"):
-                    issue(0, i % N_BATCHES, i & 1, v, True, stream=st)
-                elif v == "in_place_separate":
-                    issue(0, i % N_BATCHES, i & 1, "in_place", False, stream=st)
+                    issue(0, i % N_BATCHES, i & 1, v, False, stream=st)
+                elif v == "in_place_lag":
+                    issue(0, i % N_BATCHES, i & 1, "in_place", True, stream=st)
                 elif v == "c4_shard":
                     issue(0, 0, i & 1, "in_place", False, stream=st, n=C4_SHARD,
                           pkts=pk[(i // 8) % N_BATCHES] + (i % 8) * C4_SHARD * SLOT)
@@ -743,14 +741,14 @@ def run_rank(args) -> None:
         return
 
     # ---- timed region: K steps over all streams, bracketed by barrier + synchronize, max over ranks
-    elapsed_rank = timed("in_place", args.steps, args.warmup, lag=True, barrier=True)
+    elapsed_rank = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
     per_rank_s = gather_floats(elapsed_rank)
     elapsed = max(per_rank_s)
     # the same measurement at >= 50 steps (400 batches), in the same line: the K-step value is the
     # steady-state rate when the two agree
     steady = None
     if gpu and args.steady_steps > 0:
-        st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=True, barrier=True)))
+        st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=False, barrier=True)))
         steady = {"steps": args.steady_steps,
                   "value": round(BATCH * BATCHES_PER_STEP * args.steady_steps * world / st_el / 1e6, 1),
                   "ms_per_step": round(st_el / args.steady_steps * 1e3, 5)}
@@ -800,24 +798,26 @@ def run_rank(args) -> None:
     roof, variants = None, {}
     if gpu:
         launches = args.steps * BATCHES_PER_STEP
-        roof = kernel_pass("in_place", launches, lag=True)
+        roof = kernel_pass("in_place", launches, lag=False)
         if world == 1 and not args.no_variants:
-            el = timed("in_place", args.steps, args.warmup, lag=False)
-            variants["in_place_separate"] = {
+            el = timed("in_place", args.steps, args.warmup, lag=True)
+            variants["in_place_lag"] = {
                 "value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
                 "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
-                **kernel_pass("in_place", launches, lag=False),
-                "what": "round 2's path: classify launch + a separate group launch per batch, same streams"}
+                **kernel_pass("in_place", launches, lag=True),
+                "what": "NBG_GROUP_LAG: batch i grouped inside batch i+1's streaming classify launch (one launch per "
+                        "batch); slower here: the CU is VALU-busy classifying, so the grouping cannot hide under the "
+                        "launch's HBM time (DESIGN.md section 4)"}
             for v in ("records", "read_only"):
-                el = timed(v, args.steps, args.warmup, lag=True)
+                el = timed(v, args.steps, args.warmup, lag=False)
                 variants[v] = {"value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
                                "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
                                "classify_bytes_per_pkt": CLASSIFY_BYTES[v], "path_bytes_per_pkt": PATH_BYTES[v],
-                               **kernel_pass(v, launches, lag=True)}
-            variants["records"]["what"] = ("MAC swap written as dense 12-B egress records (packet bytes untouched), "
-                                           "lagged grouping, same streams")
-            variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + lagged "
-                                             "grouping, same streams")
+                               **kernel_pass(v, launches, lag=False)}
+            variants["records"]["what"] = ("MAC swap written as dense 12-B egress records (packet bytes untouched) "
+                                           "+ grouping, same streams")
+            variants["read_only"]["what"] = ("north_star's parse + hash + lookup: no MAC rewrite, backend[] + grouping, "
+                                             "same streams")
             # config C4's per-GPU workload: 131,072-packet shards of the 8 batches (64 distinct)
             el = timed("in_place", args.steps, args.warmup, lag=False, n=C4_SHARD, shard=True)
             variants["c4_shard"] = {
@@ -865,8 +865,7 @@ def run_rank(args) -> None:
                                    "1M-packet device-resident batch per GPU",
                        "backends": N_BACKENDS, "table_size": TABLE, "batch_pkts": BATCH, "slot_bytes": SLOT,
                        "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "batches_per_step": BATCHES_PER_STEP,
-                       "mac_swap": "in place", "group_by": "perm + counts (NBG_GROUP_LAG: batch i grouped inside "
-                                                           "batch i+1's launch; the last by finish_group, timed)",
+                       "mac_swap": "in place", "group_by": "perm + counts (group launch per batch)",
                        "streams": S, "parallelism": f"shard{world}"},
             "per_gpu_mpps": [round(BATCH * BATCHES_PER_STEP * args.steps / s / 1e6, 1) for s in per_rank_s],
             "lut_digest": digest,
@@ -881,15 +880,16 @@ def run_rank(args) -> None:
         if roof is not None:
             line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": roof["frac"], "traffic": None,
-                                "kernel": "classify_stream_kernel<F4,HIST,in place,7> (LDS LUT, LDS-DMA tile ring, "
-                                          "lagged grouping of the previous batch)",
+                                "kernel": "classify_stream_kernel<F4,HIST,in place> (LDS LUT, LDS-DMA tile ring)",
                                 "bytes_per_pkt": roof["bytes_per_pkt"], "pkts_per_launch": BATCH,
                                 "avg_launch_us": roof["avg_launch_us"],
-                                "timing": "single-stream pass, HIP events around each launch (classify batch i + "
-                                          "group batch i-1); `value` is the multi-stream rate",
+                                "group_kernel_avg_us": roof["group_kernel_avg_us"],
+                                "timing": "single-stream pass, HIP events around each classify launch (grouping "
+                                          "deferred); `value` is the multi-stream rate, where the grouping of one "
+                                          "batch overlaps the classify of the next",
                                 "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts), "
-                                        "so the physical traffic is ~1.7x the algorithmic bytes and this launch's frac "
-                                        "is capped near 0.48 by the measured read+rewrite ceiling with nt loads "
+                                        "so the physical traffic is ~1.7x the 78 algorithmic bytes and this variant's "
+                                        "frac is capped near 0.46 by the measured read+rewrite ceiling with nt loads "
                                         "(DESIGN.md section 5); variants.read_only / read_only_multi4 are north_star's "
                                         "parse + hash + lookup"}
         if variants:

@@ -639,7 +639,7 @@ constexpr uint32_t kLutLds = 65536;            // LUT bytes staged in LDS
 
 #ifdef NBG_SPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch:
                    // [0] entry, [1] LUT visible (after the barrier), [2 + k] tile k landed, [11] exit
-constexpr uint32_t kSProbeWaves = 4096, kSProbeSlots = 12;
+constexpr uint32_t kSProbeWaves = 4096, kSProbeSlots = 20;
 __device__ unsigned long long g_sprobe[kSProbeWaves * kSProbeSlots];
 #define SPROBE(slot)                                                                              \
   if (lane == 0 && blockIdx.x * kStreamW + wave < kSProbeWaves && (slot) < kSProbeSlots)          \
@@ -1191,7 +1191,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
     if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
+    if (k == 4) SPROBE(12)
     if (!(NBG_LAG_ABL & 2) && k < pieces) piece_rank(k);
+    if (k == 4) SPROBE(13)
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -1204,12 +1206,15 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       // partition row and zeroes it.  The next barrier (unit k + 1) orders that before unit k + 2
       // counts into the same buffer.
       lds_sync();
+      if (k == 4) SPROBE(14)
       if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
         stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
+    if (k == 4) SPROBE(15)
     if (!(NBG_LAG_ABL & 2)) piece_sync(k);
+    if (k == 4) SPROBE(16)
   }
   if constexpr (GB > 0) {
     // sync points past the unit steps: pieces beyond them (a pending batch larger than this one),

@@ -34,11 +34,11 @@ def test_pmc_rows_filters_and_orders(tmp_path):
 
 
 def test_pmc_algorithmic_bytes():
-    """Per-launch algorithmic bytes of every PMC entry: lagged launches carry the
+    """Per-launch algorithmic bytes of every PMC entry: a lagged launch carries the
     whole path (82 B: classify + the previous batch's perm), the others their classify bytes."""
-    assert bench._pmc_algorithmic("in_place") == bench.BATCH * 82
-    assert bench._pmc_algorithmic("in_place_separate") == bench.BATCH * 78
-    assert bench._pmc_algorithmic("read_only") == bench.BATCH * 70
+    assert bench._pmc_algorithmic("in_place_lag") == bench.BATCH * 82
+    assert bench._pmc_algorithmic("in_place") == bench.BATCH * 78
+    assert bench._pmc_algorithmic("read_only") == bench.BATCH * 66
     assert bench._pmc_algorithmic("c4_shard") == 131072 * 78
     assert bench._pmc_algorithmic("c3") == bench.BATCH * 84
     assert bench._pmc_algorithmic("c5") == bench.BATCH * 78

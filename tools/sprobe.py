@@ -53,9 +53,9 @@ def main():
         if args.lag:
             mg.finish_group()
         waves = 256 * 8
-        raw = np.zeros(4096 * 12, dtype=np.uint64)
+        raw = np.zeros(4096 * 20, dtype=np.uint64)
         assert fn(raw.ctypes.data, raw.size) == 0
-        t = raw.reshape(4096, 12)[:waves].astype(np.float64)
+        t = raw.reshape(4096, 20)[:waves].astype(np.float64)
         t0 = t[:, 0].min()
         us = (t - t0) / 100.0  # 100 MHz -> us
         print(f"== {variant}: launch span {us[:, 11].max():.2f} us (first entry to last exit)")
@@ -66,6 +66,11 @@ def main():
         for k in range(8):
             print(f"   tile {k} in    {pct(us[:, 2 + k])}")
         print(f"   exit         {pct(us[:, 11])}")
+        # inside step 4 (per wave, relative to its tile-4 arrival): classify + next issue, rank,
+        # barrier, flush, lagged-group sync work
+        d = us[:, 12:17] - us[:, 6:7]
+        for nm, c in zip(("classified", "ranked", "barrier", "flushed", "synced"), range(5)):
+            print(f"   step4 {nm:10s} {pct(d[:, c])}")
         steady = np.diff(us[:, 2:10], axis=1)
         print(f"   tile interval (k -> k+1) median {np.median(steady):.2f} us, p90 {np.percentile(steady, 90):.2f}")
         # where the exit spread comes from: per block (max over its waves), grouped by XCD (blocks
