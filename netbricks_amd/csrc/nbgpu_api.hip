@@ -1055,6 +1055,9 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   if (h->pending_lag) return flush_lag(h, static_cast<hipStream_t>(stream));
   h->pending = false;
   if (h->pending_multi) {
+    // the fused multi path is taken only with the partition rows in the classify kernel and the
+    // direct (or LDS) scan in the group prologue (nbg_maglev_classify_device_multi), so there is no
+    // hist or scan kernel to launch here, unlike the single-batch branch below
     const uint32_t n = h->pending_multi;
     h->pending_multi = 0;
     return launch_group_multi(h->pending_gm, n, h->pending_scan_mode, stream);

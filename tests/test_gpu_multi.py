@@ -112,3 +112,32 @@ def test_multi_rejects_bad_counts(torch_cuda, mg65):
     d = torch_cuda.zeros(64 * 10, dtype=torch_cuda.uint8, device="cuda:0")
     with pytest.raises(ValueError):
         mg65.group_by_multi([(d, 10)] * 9)
+
+
+def test_multi_deferred_group_on_second_stream(torch_cuda, mg65, lut65):
+    """NBG_DEFER_GROUP on the fused multi-batch path: the classify launch on one stream,
+    the one group launch of all batches by finish_group on a second stream (ordered after it by the
+    handle's event), then a single group_by on the first stream: every batch bit-exact."""
+    torch = torch_cuda
+    sizes = [1 << 20, 300_000, 700_001]
+    host, dev = _batches(torch, sizes, seed=400)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    out = mg65.group_by_multi(dev, defer_group=True, stream=s1.cuda_stream)
+    mg65.finish_group(s2.cuda_stream)
+    buf, _, _ = __import__("netbricks_amd").make_trace(400_000, 0, seed=410)
+    d = torch.from_numpy(buf.copy()).to(torch.device("cuda:0"))
+    r = mg65.group_by(d, 400_000, stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    mg65.check()
+    for j, (h, n) in enumerate(zip(host, sizes)):
+        ref = h.copy()
+        be = orc.classify(ref, n, lut65)
+        perm, counts = orc.group(be, 65)
+        np.testing.assert_array_equal(_np(out[j].backend, np.uint16)[:n], be, err_msg=f"batch {j}")
+        np.testing.assert_array_equal(_np(out[j].perm, np.uint32)[:n], perm, err_msg=f"batch {j}")
+        np.testing.assert_array_equal(_np(out[j].counts, np.uint32), counts, err_msg=f"batch {j}")
+    ref = buf.copy()
+    be = orc.classify(ref, 400_000, lut65)
+    perm, counts = orc.group(be, 65)
+    np.testing.assert_array_equal(_np(r.perm, np.uint32)[:400_000], perm)
+    np.testing.assert_array_equal(_np(r.counts, np.uint32), counts)
