@@ -1191,9 +1191,9 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
     if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
-    if (k == 4) SPROBE(12)
+    if (k == 4) { SPROBE(12) }
     if (!(NBG_LAG_ABL & 2) && k < pieces) piece_rank(k);
-    if (k == 4) SPROBE(13)
+    if (k == 4) { SPROBE(13) }
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -1206,15 +1206,15 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       // partition row and zeroes it.  The next barrier (unit k + 1) orders that before unit k + 2
       // counts into the same buffer.
       lds_sync();
-      if (k == 4) SPROBE(14)
+      if (k == 4) { SPROBE(14) }
       if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
         stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
-    if (k == 4) SPROBE(15)
+    if (k == 4) { SPROBE(15) }
     if (!(NBG_LAG_ABL & 2)) piece_sync(k);
-    if (k == 4) SPROBE(16)
+    if (k == 4) { SPROBE(16) }
   }
   if constexpr (GB > 0) {
     // sync points past the unit steps: pieces beyond them (a pending batch larger than this one),
