@@ -20,6 +20,7 @@
 // Integer/byte work only; no MFMA.  HBM-bound.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "nbgpu_internal.h"
@@ -2393,6 +2394,20 @@ int launch_hist(const HistArgs& a, void* stream) {
   hipLaunchKernelGGL(hist_kernel, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "hist launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+__global__ __launch_bounds__(kBlock) void zero_kernel(uint32_t* p, uint32_t words) {
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < words; i += gridDim.x * kBlock) p[i] = 0;
+}
+
+int launch_zero(uint32_t* p, size_t words, void* stream) {
+  if (words == 0) return NBG_OK;
+  const uint32_t grid = static_cast<uint32_t>(std::min<size_t>((words + kBlock - 1) / kBlock, 1024));
+  hipLaunchKernelGGL(zero_kernel, dim3(grid), dim3(kBlock), 0, static_cast<hipStream_t>(stream), p,
+                     static_cast<uint32_t>(words));
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "zero launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 

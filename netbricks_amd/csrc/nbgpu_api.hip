@@ -525,6 +525,17 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
 
 namespace {
 
+// The partition rows of a captured call are zeroed inside the graph.  NBG_CAPTURE_ZERO_KERNEL (A/B
+// builds of the graph-replay root-cause experiment): by a kernel node instead of a memset node.
+int zero_captured(uint32_t* p, size_t words, void* stream) {
+#if NBG_CAPTURE_ZERO_KERNEL
+  return launch_zero(p, words, stream);
+#else
+  NBG_HIP(hipMemsetAsync(p, 0, words * 4, static_cast<hipStream_t>(stream)));
+  return NBG_OK;
+#endif
+}
+
 // The pending lagged group (NBG_GROUP_LAG) as a group launch of its own on `s` (already ordered
 // after the handle's last launch).  Its rows live in the lag set it was classified into; the
 // standalone group kernel zeroes nothing there (the next lagged classify zeroes the sets).
@@ -773,7 +784,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
     a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
     if (capturing && a.part_hist)
-      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
+      if ((rc = zero_captured(a.part_hist, static_cast<size_t>(n_parts) * nbins, stream))) return rc;
     if (lag) return classify_lag(h, a, fuse, n_parts, part_pkts, d_perm, d_counts, static_cast<hipStream_t>(stream));
     rc = launch_classify_stream(a, h->cus, stream);
   } else if (d_off && d_len && a.win_owned && !lds && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
@@ -783,12 +794,12 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
       a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
     }
     if (capturing && a.part_hist)
-      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
+      if ((rc = zero_captured(a.part_hist, static_cast<size_t>(n_parts) * nbins, stream))) return rc;
     a.sink = h->d_sink;
     rc = launch_classify_stream_desc(a, h->wide, h->cus, stream);
   } else {
     if (capturing && a.part_hist)
-      NBG_HIP(hipMemsetAsync(a.part_hist, 0, static_cast<size_t>(n_parts) * nbins * 4, static_cast<hipStream_t>(stream)));
+      if ((rc = zero_captured(a.part_hist, static_cast<size_t>(n_parts) * nbins, stream))) return rc;
     rc = launch_classify(a, h->wide, lds, grid, stream);
   }
   if (rc) return rc;

@@ -7,6 +7,10 @@
 
 #include "../../include/nbgpu.h"
 
+#ifndef NBG_CAPTURE_ZERO_KERNEL
+#define NBG_CAPTURE_ZERO_KERNEL 0
+#endif
+
 namespace nbg {
 
 // Thread-local last-error string (nbg_last_error); returns `code` for chaining.
@@ -181,6 +185,7 @@ int stream_waves_per_block();
 int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, void* stream);
 size_t stream_desc_lds(uint32_t nb, int mode, bool wide_lut);
 int launch_scan(const ScanArgs& a, void* stream);
+int launch_zero(uint32_t* p, size_t words, void* stream);  // p[0, words) = 0 (one kernel)
 int launch_hist(const HistArgs& a, void* stream);
 bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
