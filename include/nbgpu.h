@@ -168,6 +168,37 @@ typedef struct nbg_batch {
 int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, uint32_t n_batches, uint32_t stride,
                                      uint16_t fixed_len, uint32_t flags, void* stream);
 
+/*
+ * Persistent RX ring (the GPUDirect RX model: an RX queue that never stops, ReceiveBatch::execute
+ * polling its port, framework/src/operators/receive_batch.rs:26,52-61).  nbg_ring_start launches ONE
+ * streaming-classify kernel on `stream` (one block per CU) that runs until nbg_ring_stop: it stages
+ * the LUT in LDS once and classifies batches as they are posted, so no launch, LUT staging or
+ * pipeline ramp is paid per batch.  nbg_ring_post hands it one device-resident batch of fixed
+ * slots (the streaming kernel's layout: stride % 16 == 0, 64 <= stride < 2^24, fixed_len >= 48,
+ * d_pkts and d_backend 16-B aligned) through a descriptor ring in pinned host memory, and returns
+ * its ticket (0, 1, 2, ... in post order) without waiting; a post finds a free slot first
+ * (NBG_RING_SLOTS batches may be outstanding).  Batch `ticket` is complete when nbg_ring_poll
+ * reports more than `ticket` completed batches, or nbg_ring_wait(ticket) returns: its backend[] and
+ * (NBG_SWAP_MACS) its in-place MAC swap are then in HBM, written through the L2, for any later
+ * launch or copy.  Per packet the results are those of nbg_maglev_classify_device_ex with the same
+ * arguments and no grouping (perm / counts are not produced on the ring).  Everything a post names
+ * stays untouched by the caller until the batch is complete.
+ * The kernel owns its stream (and the LDS of every CU it occupies) until it ends: after
+ * nbg_ring_stop, or by itself after idle_ms without a post (its exit condition when the producer
+ * goes away; 0 = 2000 ms; the next ring call then returns NBG_ETIMEDOUT).  nbg_ring_stop completes
+ * every posted batch, waits for the kernel to end, and frees the ring.  One ring per handle; one
+ * producer thread per ring.  Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
+ * flags: 0 (read only) or NBG_SWAP_MACS (in place).
+ */
+#define NBG_RING_SLOTS 16u
+typedef struct nbg_ring nbg_ring;
+int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms,
+                   void* stream, nbg_ring** out);
+int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket);
+int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
+int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);
+int nbg_ring_stop(nbg_ring* r);
+
 /* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP (or the pending
  * group of the last NBG_GROUP_LAG call) on `stream`; a stream other than the handle's last one is
  * ordered after it.  No-op when nothing is pending. */

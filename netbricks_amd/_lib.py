@@ -33,6 +33,7 @@ NBG_STREAM_DESC = 0x40
 NBG_GROUP_LAG = 0x80
 NBG_HOST_SLOTS = 3
 NBG_MAX_MULTI = 8
+NBG_RING_SLOTS = 16
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
@@ -62,6 +63,11 @@ SIGNATURES = {
                                                 _P, _P, _P, _P, _P]),
     "nbg_maglev_classify_device_multi": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint32, _P]),
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
+    "nbg_ring_start": (C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint32, C.c_uint32, _P, C.POINTER(_P)]),
+    "nbg_ring_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),
+    "nbg_ring_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "nbg_ring_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
+    "nbg_ring_stop": (C.c_int, [_P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_maglev_host_submit": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, C.POINTER(C.c_uint64)]),

@@ -133,12 +133,18 @@ __device__ __forceinline__ uint32_t ld_byte_sync(const uint8_t* p) {
 // VGPRs, draining the LDS-DMA tile ring every step (measured: 2x per-step time in the lagged-
 // grouping kernel).  A synchronous byte load costs a full memory round trip, but only packets off
 // the fast path (none in the C2/C3/C5 traces) take this path.
-template <int LUTM, bool F4, bool CHAIN, bool SYNC = false>
+// WT (the persistent ring kernel): the MAC bytes are stored write-through (sc1), so that they are in
+// HBM once the store retires (nbg_ring completion, no L2 write-back in a kernel that never ends).
+template <int LUTM, bool F4, bool CHAIN, bool SYNC = false, bool WT = false>
 __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const uint8_t* lut_lds, uint8_t* p,
                                                   uint32_t len, uint32_t pkt, uint32_t& gate) {
   auto rd = [](const uint8_t* x) -> uint32_t {
     if constexpr (SYNC) return ld_byte_sync(x);
     return *x;
+  };
+  auto wr = [](uint8_t* x, uint8_t v) {
+    if constexpr (WT) __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *x = v;
   };
   gate = kSentinel;
   if (len < kEth) return a.nb;  // Packet::parse_header assert (interface/packet.rs:392-399)
@@ -156,8 +162,8 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const uint8_t d = static_cast<uint8_t>(rd(p + k)), s = static_cast<uint8_t>(rd(p + k + 6));
-      o[k] = s;
-      o[k + 6] = d;
+      wr(o + k, s);
+      wr(o + k + 6, d);
     }
   }
   if (plen < 20) return a.nb;  // slice OOB in ipv4_extract_flow
@@ -190,6 +196,20 @@ __device__ __forceinline__ uint4 ldg16(const uint8_t* p) { return *reinterpret_c
 __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
   const u32x4_t w = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+}
+
+// Write-through 16-B store (sc1: the line leaves L2 for HBM; MI355X_MICROARCH.md visibility table):
+// the persistent ring kernel's outputs, visible to any later launch or copy once the store retires.
+// Inline asm (the compiler cannot emit sc1 on a 64-bit-addressed 16-B store); s_nop 1 keeps the
+// compiler's next instruction off the data VGPRs while the store reads them.
+__device__ __forceinline__ void stg16_wt(void* p, uint4 v) {
+  const u32x4_t w = {v.x, v.y, v.z, v.w};
+  asm volatile(
+      "global_store_dwordx4 %0, %1, off sc1\n\t"
+      "s_nop 1"
+      :
+      : "v"(p), "v"(w)
+      : "memory");
 }
 
 // Workgroup barrier for LDS-only hand-offs: wait for this wave's LDS operations, then s_barrier.
@@ -664,7 +684,7 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
       "global_load_lds_dwordx4 %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
       : "memory");
 }
 
@@ -688,7 +708,7 @@ __device__ __forceinline__ void glds16_tile(const void* src, uint32_t lds_base) 
         "global_load_lds_dwordx4 %1, off nt\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(src), "s"(lds_base)
+        : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
         : "memory");
   } else {
     glds16(src, lds_base);
@@ -770,7 +790,7 @@ __device__ __forceinline__ void stream_flush(const ClassifyArgs& a, uint32_t* hi
 
 // Classify one tile from its LDS ring buffer `x` (row of this lane's packet) and write the results.
 // Returns the bin to count (histogram) through `bin`; false when the lane has no packet.
-template <bool F4, int MODE, uint32_t kRow = row_of<MODE>()>
+template <bool F4, int MODE, uint32_t kRow = row_of<MODE>(), bool WT = false>
 __device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uint8_t* lut, const uint8_t* x,
                                                 uint32_t p, uint32_t& bin_out, bool& slow_out) {
   const bool valid = p < a.n_pkts;
@@ -811,7 +831,10 @@ __device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uin
       const bool qfast = q < a.n_pkts && ((w3 >> 16) & 0xfu) == 5u;
       if (part == 0u)
         v = make_uint4((v.y >> 16) | (v.z << 16), (v.z >> 16) | (v.x << 16), (v.x >> 16) | (v.y << 16), v.w);
-      if (qfast) stg16_nt(a.pkts + static_cast<size_t>(q) * a.stride + part * 16u, v);
+      if (qfast) {
+        if constexpr (WT) stg16_wt(a.pkts + static_cast<size_t>(q) * a.stride + part * 16u, v);
+        else stg16_nt(a.pkts + static_cast<size_t>(q) * a.stride + part * 16u, v);
+      }
     }
   } else if constexpr (MODE == 2) {
     if (fast) {
@@ -851,7 +874,7 @@ __device__ __forceinline__ void glds4(const void* src, uint32_t lds_base) {
       "global_load_lds_dword %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
       : "memory");
 }
 __device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
@@ -863,7 +886,7 @@ __device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
       "global_load_lds_ushort %1, off\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(src), "s"(lds_base)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
       : "memory");
 }
 
@@ -1237,6 +1260,283 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores retired
 #endif
   SPROBE(11)
+}
+
+// ---- persistent RX-ring classify (nbg_ring_*) ----------------------------------------------------
+//
+// One launch per ring for the whole run: the RX ring that never stops (ReceiveBatch polling its port,
+// framework/src/operators/receive_batch.rs:26,52-61).  Same blocks, LUT staging, LDS-DMA tile ring
+// and interleaved 512-packet units as classify_stream_kernel, but the unit sequence is open-ended:
+// batch j covers units [ulo_j, uhi_j) of one sequence, block b takes units b, b + G, b + 2G, ... of
+// it, and batches arrive through a descriptor ring in pinned host memory while the kernel runs.  So
+// the LUT is staged once per ring and the tile pipeline runs across batch boundaries without a
+// ramp.
+//
+//   Descriptors.  Wave 0 of every block keeps up to kRingCache batch descriptors in LDS.  It
+//   prefetches the next kRingFetch ring slots by LDS-DMA (system scope: the slots live in host
+//   memory) ahead of its next tile, so the fetch is covered by that tile's counted wait and never
+//   drains the ring; a slot is taken once its seq and check match (a read that overlaps the host
+//   rewriting the slot fails the check and is retried).  The count of known batches is published
+//   through a step-parity LDS word behind the unit barrier, so every wave sees the same count.
+//   When the block has no tile to classify (the next unit is in no known batch) it drains and
+//   wave 0 polls the ring slot (and the stop word) with s_sleep between polls: the idle path.
+//   Exit: stop set and nothing posted, or idle_ticks without a new batch (the exit condition every
+//   wave reaches when the host goes away).
+//
+//   Completion.  Outputs are stored write-through (sc1: backend[] packed 16 B per lane, the in-place
+//   windows 16 B per lane), so a store that retired is in HBM.  In-order vmcnt: once every wave has
+//   waited for tile k (the unit barrier of step k), the stores of steps <= k - 3 retired.  Wave 0
+//   then publishes, per block, the count of batches all of whose units of this block are complete
+//   (one system-scope store to pinned memory when the count changes); the host takes the minimum.
+constexpr uint32_t kRingCache = 4;  // batch descriptors in LDS (from the current unit's batch on)
+constexpr uint32_t kRingFetch = 2;  // ring slots per prefetch (one LDS-DMA dword load, 32 lanes)
+constexpr uint32_t kRingCtlWords = kRingCache * 16u + kRingFetch * 16u + 4u + kStreamW * 32u;
+
+__device__ __forceinline__ void glds4_sys(const void* src, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off sc0 sc1\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_base))
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <bool F4, int MODE>
+__global__ __launch_bounds__(kStreamNT, 1) void classify_ring_kernel(ClassifyArgs a, RingArgs r) {
+  static_assert(MODE == 0 || MODE == 1, "the ring classifies read only or in place");
+  constexpr uint32_t kRow = stream_row_of<MODE>(), kTileLds = 64u * kRow;
+  extern __shared__ __align__(16) uint8_t smem[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = rfl(tid >> 6);
+  uint8_t* lut = smem;
+  uint8_t* ring = smem + kLutLds + wave * (kRing * kTileLds);
+  uint32_t* cache = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);  // [kRingCache][16]
+  uint32_t* stage = cache + kRingCache * 16u;   // [kRingFetch][16] wave 0's prefetch landing area
+  uint32_t* known_l = stage + kRingFetch * 16u;  // [2] known batches, by step parity; [2] exit
+  uint16_t* rep = reinterpret_cast<uint16_t*>(known_l + 4) + wave * 64u;  // this wave's 64 backends
+  const uint32_t ring_lds = rfl(lds_addr(ring)), lut_lds = rfl(lds_addr(lut)), stage_lds = rfl(lds_addr(stage));
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  SPROBE(0)
+  const uint32_t pieces_lut = a.lut_lds_bytes >> 10;
+  for (uint32_t q = wave; q < pieces_lut; q += kStreamW)
+    glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
+  if (tid < 4) known_l[tid] = 0;
+  wait_vm<0>();
+  lds_sync();
+  SPROBE(1)
+
+  // cursors over the known batches: the unit being classified, and the unit whose tile is issued
+  struct Cursor {
+    uint32_t j;  // batch index (0xffffffff: none yet)
+    uint64_t lo, hi;
+    uint8_t* pkts;
+    uint16_t* backend;
+    uint32_t n;
+  };
+  auto load = [&](Cursor& c, uint32_t j) {
+    const uint32_t* e = cache + (j % kRingCache) * 16u;
+    c.j = j;
+    c.pkts = reinterpret_cast<uint8_t*>(static_cast<uintptr_t>(rfl(e[0])) | static_cast<uintptr_t>(rfl(e[1])) << 32);
+    c.backend = reinterpret_cast<uint16_t*>(static_cast<uintptr_t>(rfl(e[2])) | static_cast<uintptr_t>(rfl(e[3])) << 32);
+    c.lo = static_cast<uint64_t>(rfl(e[4])) | static_cast<uint64_t>(rfl(e[5])) << 32;
+    c.hi = static_cast<uint64_t>(rfl(e[6])) | static_cast<uint64_t>(rfl(e[7])) << 32;
+    c.n = rfl(e[8]);
+  };
+  uint32_t known = 0;  // block-uniform: read after a barrier
+  auto seek = [&](Cursor& c, uint64_t u) -> bool {
+    while (u >= c.hi) {
+      const uint32_t nj = c.j + 1u;
+      if (static_cast<int32_t>(nj - known) >= 0) return false;
+      load(c, nj);
+    }
+    return true;
+  };
+  Cursor cur{0xffffffffu, 0, 0, nullptr, nullptr, 0}, nxt = cur;
+  const uint64_t Gu = G;
+  uint32_t k = 0, iss = 0;                   // unit steps of this block classified / issued
+  uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // VM operations issued; counts after tiles k, k+1, k+2
+  auto issue = [&](uint32_t t) -> bool {
+    const uint64_t u = b + static_cast<uint64_t>(t) * Gu;
+    if (!seek(nxt, u)) return false;
+    ClassifyArgs v = a;
+    v.pkts = nxt.pkts;
+    v.n_pkts = nxt.n;
+    issue_tile<kRow, true>(v, static_cast<uint32_t>(((u - nxt.lo) * kStreamW + wave) * 64u),
+                           ring_lds + (rfl(t) % kRing) * kTileLds, lane);
+    seq += 4;
+    const uint32_t d = t - k;
+    if (d == 0) sA = seq;
+    else if (d == 1) sB = seq;
+    else sC = seq;
+    ++iss;
+    return true;
+  };
+
+  // wave 0's descriptor state
+  uint32_t known_w = 0, pf_seq = 0, pf_base = 0, last_pf = 0, pub = 0;
+  bool pf = false;
+  uint32_t hA = 0xffffffffu, hB = 0xffffffffu;  // batch of the unit of steps k - 1, k - 2
+  // take staged descriptor i (every lane reads all 16 words) as batch known_w when it is that batch
+  auto take = [&](const uint32_t* d) -> bool {
+    const uint4 w0 = *reinterpret_cast<const uint4*>(d), w1 = *reinterpret_cast<const uint4*>(d + 4);
+    const uint4 w2 = *reinterpret_cast<const uint4*>(d + 8), w3 = *reinterpret_cast<const uint4*>(d + 12);
+    const uint64_t pk = w0.x | static_cast<uint64_t>(w0.y) << 32, be = w0.z | static_cast<uint64_t>(w0.w) << 32;
+    const uint64_t lo = w1.x | static_cast<uint64_t>(w1.y) << 32, hi = w1.z | static_cast<uint64_t>(w1.w) << 32;
+    const uint64_t ck = w3.z | static_cast<uint64_t>(w3.w) << 32;
+    const uint32_t base = cur.j == 0xffffffffu ? 0u : cur.j;
+    const bool ok = w2.y == known_w + 1u && ck == ring_check(pk, be, lo, hi, w2.x, w2.y) && known_w - base < kRingCache;
+    if (!rfl(ok ? 1u : 0u)) return false;
+    if (lane < 16) cache[(known_w % kRingCache) * 16u + lane] = d[lane];
+    ++known_w;
+    return true;
+  };
+  auto publish = [&](uint32_t v) {  // batches < v complete for this block
+    if (static_cast<int32_t>(v - pub) > 0) {
+      pub = v;
+      if (lane == 0) __hip_atomic_store(r.prog + b, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ++seq;
+    }
+  };
+  // idle: poll the next ring slot (and the stop word); returns true to exit
+  auto poll = [&]() -> bool {
+    const uint64_t t0 = wall_clock64();
+    for (uint32_t nap = 1;; nap = min(2u * nap, 16u)) {
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
+      uint32_t w = 0;
+      if (lane < 16) w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane < 16) stage[lane] = w;
+      __builtin_amdgcn_wave_barrier();
+      while (take(stage)) {
+        if (lane < 16) stage[lane] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u))) + lane,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (known_w != known) return false;
+      if (rfl(__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+        // a batch posted before the stop is in its slot by now: look once more
+        if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_wave_barrier();
+        if (take(stage)) return false;
+        return true;
+      }
+      if (wall_clock64() - t0 > r.idle_ticks) {
+        if (lane == 0) __hip_atomic_store(&r.ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return true;
+      }
+      // back off to 16 x 512 clocks (~3.5 us) between polls: the idle grid reads a few GB/s over PCIe
+      for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);
+    }
+  };
+
+  for (;;) {
+    known = rfl(known_l[k & 1u]);
+    while (iss < k + kRing && issue(iss)) {
+    }
+    if (iss == k) {
+      // nothing to classify: drain, then wave 0 fetches descriptors (polling while none is posted).
+      // No issued unit waits for cur, so it takes nxt's place: the descriptor cache then only keeps
+      // batches past the issue cursor (which has walked every known batch), and a block with no unit
+      // in several small batches still gets room to take the next ones.
+      cur = nxt;
+      wait_vm<0>();
+      lds_sync();
+      if (wave == 0) {
+        if (pf) {  // landed (vmcnt(0) above)
+          for (uint32_t i = 0; i < kRingFetch && pf_base + i == known_w; ++i)
+            if (!take(stage + i * 16u)) break;
+          pf = false;
+        }
+        publish(known);  // every unit of this block in batches < known is complete
+        const bool ex = known_w == known && poll();
+        if (lane == 0) {
+          known_l[k & 1u] = known_w;
+          known_l[2] = ex ? 1u : 0u;
+        }
+      }
+      lds_sync();
+      if (rfl(known_l[2])) break;
+      continue;
+    }
+#if NBG_SEQWAIT
+    wait_vm_n(seq - sA);
+#else
+    wait_vm<0>();
+#endif
+#ifdef NBG_SPROBE
+    if (k - r.probe_step < 16u) { SPROBE(2 + (k - r.probe_step)) }
+#endif
+    const uint64_t u = b + static_cast<uint64_t>(k) * Gu;
+    seek(cur, u);
+    const uint32_t h0 = cur.j;
+    if (wave == 0) {
+      // descriptor prefetch: take a landed one (its LDS-DMA retired: pf_seq <= sA), then issue the
+      // next ahead of this step's tile, so the wait for that tile covers it
+      if (pf && static_cast<int32_t>(sA - pf_seq) >= 0) {
+        for (uint32_t i = 0; i < kRingFetch && pf_base + i == known_w; ++i)
+          if (!take(stage + i * 16u)) break;
+        pf = false;
+      }
+      if (!pf && known_w - cur.j < kRingCache && known_w - nxt.j <= 2u && k - last_pf >= 4u) {
+        pf_base = known_w;
+        if (lane < 16u * kRingFetch)
+          glds4_sys(reinterpret_cast<const uint32_t*>(r.desc + ((known_w + lane / 16u) & (r.slots - 1u))) + (lane & 15u),
+                    stage_lds);
+        ++seq;
+        pf_seq = seq;
+        pf = true;
+        last_pf = k;
+      }
+    }
+    ClassifyArgs v = a;
+    v.pkts = cur.pkts;
+    v.n_pkts = cur.n;
+    v.backend = cur.backend;
+    const uint32_t tb = static_cast<uint32_t>(((u - cur.lo) * kStreamW + wave) * 64u);
+    const uint32_t p = tb + lane;
+    uint32_t bin = 0;
+    bool slow = false;
+    const bool valid = tb < v.n_pkts &&
+                       stream_classify<F4, MODE, kRow, true>(v, lut, ring + (k % kRing) * kTileLds + lane * kRow, p, bin, slow);
+    if (iss == k + kRing) {  // the next tile into the buffer just read
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      issue(iss);
+    }
+    if (valid && slow) {
+      uint32_t gate;
+      bin = classify_slow<kLdsU8Tail, F4, false, true, true>(v, lut, v.pkts + static_cast<size_t>(p) * v.stride,
+                                                             v.fixed_len, p, gate);
+    }
+    if (tb < v.n_pkts) {
+      const uint16_t be = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+      const uint32_t cnt = min(64u, v.n_pkts - tb);
+      if (cnt == 64u) {  // 16 B per lane: lanes 0..7 store the wave's 128 B
+        rep[lane] = be;
+        asm volatile("" ::: "memory");  // the u16 writes before the 16-B reads of the same words
+        __builtin_amdgcn_wave_barrier();
+        const uint4 w = reinterpret_cast<const uint4*>(rep)[lane & 7u];
+        if (lane < 8u) stg16_wt(v.backend + tb + lane * 8u, w);
+      } else if (valid) {
+        __hip_atomic_store(v.backend + p, be, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ++seq;
+    }
+    if (wave == 0 && lane == 0) known_l[(k + 1u) & 1u] = known_w;
+    lds_sync();
+    // every wave has waited for tile k: the stores of steps <= k - 3 retired
+    if (wave == 0 && hB != 0xffffffffu) publish(hB);
+    hB = hA;
+    hA = h0;
+    sA = sB;
+    sB = sC;
+    ++k;
+  }
+  SPROBE(19)
 }
 
 // ---- streaming classify for descriptor layouts (IMIX: u32 offsets + u16 lengths, owned windows) ----
@@ -2338,6 +2638,28 @@ int launch_classify_stream_lag(const ClassifyArgs& a, const LagGroup& lg, int gr
               : launch_stream_mode<true, true, 9>(a, sb, lg, mode, grid, lds, s);
   return b7 ? launch_stream_mode<false, true, 7>(a, sb, lg, mode, grid, lds, s)
             : launch_stream_mode<false, true, 9>(a, sb, lg, mode, grid, lds, s);
+}
+
+size_t ring_lds(int mode) {
+  const size_t tile = 64u * (mode == 1 ? stream_row_of<1>() : stream_row_of<0>());
+  return kLutLds + static_cast<size_t>(kStreamW) * kRing * tile + kRingCtlWords * 4u;
+}
+
+int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int grid, void* stream) {
+  const bool f4 = a.m == 65537u;
+#ifdef NBG_RING_ONE
+  auto fn = classify_ring_kernel<true, 0>;
+#else
+  auto fn = mode == 1 ? (f4 ? classify_ring_kernel<true, 1> : classify_ring_kernel<false, 1>)
+                      : (f4 ? classify_ring_kernel<true, 0> : classify_ring_kernel<false, 0>);
+#endif
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+      hipSuccess)
+    return set_error(NBG_EIO, "ring classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), ring_lds(mode), static_cast<hipStream_t>(stream), a, r);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "ring classify launch: %s", hipGetErrorString(e));
+  return NBG_OK;
 }
 
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -89,6 +90,7 @@ struct nbg_maglev {
   uint32_t* d_part_lag = nullptr;     // [3][kMaxParts][nb+1] (on first use)
   uint32_t lag_idx = 0;
   uint32_t lag_dirty = 0;             // bit k: set k may hold counts (zeroed before it is accumulated into)
+  nbg_ring* ring = nullptr;           // the running persistent ring (nbg_ring_start), if any
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
   bool issued = false;                // a launch has been issued on last_stream
   hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
@@ -487,6 +489,7 @@ int nbg_maglev_create_from_lut(const uint16_t* lut, uint64_t table_size, uint32_
 
 void nbg_maglev_destroy(nbg_maglev* h) {
   if (!h) return;
+  if (h->ring) (void)nbg_ring_stop(h->ring);
   {
     DeviceGuard g(h->device);
     free_scratch(h);
@@ -525,8 +528,11 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
 
 namespace {
 
-// The partition rows of a captured call are zeroed inside the graph.  NBG_CAPTURE_ZERO_KERNEL (A/B
-// builds of the graph-replay root-cause experiment): by a kernel node instead of a memset node.
+// The partition rows of a captured call are zeroed inside the graph, by a kernel node.  A memset node
+// (NBG_CAPTURE_ZERO_KERNEL=0, kept for the record) faults on its second replay when the graph is
+// launched on the legacy null stream under PyTorch's bundled HIP 7.0 runtime, as torch.cuda.graph
+// replays do by default; the image's HIP 7.2 replays it clean, and so does HIP 7.0 on a created
+// stream (DESIGN.md §4 "hipGraph capture", profiles/r03_graph_*.txt).
 int zero_captured(uint32_t* p, size_t words, void* stream) {
 #if NBG_CAPTURE_ZERO_KERNEL
   return launch_zero(p, words, stream);
@@ -613,8 +619,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     return set_error(NBG_EINVAL, "classify: NBG_GROUP_LAG with NBG_DEFER_GROUP");
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "classify: n_pkts must be < 2^30");
   if (n_pkts == 0) {
-    if (d_counts) NBG_HIP(hipMemsetAsync(d_counts, 0, (h->nb + 1) * sizeof(uint32_t), (hipStream_t)stream));
-    return NBG_OK;
+    return d_counts ? zero_captured(d_counts, h->nb + 1, stream) : NBG_OK;  // a kernel: capturable
   }
   if (!d_pkts || !d_backend) return set_error(NBG_EINVAL, "classify: null packet or backend buffer");
   if (lpm && (!d_gate || lpm->device != h->device))
@@ -640,15 +645,15 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     return set_error(NBG_EINVAL, "classify: NBG_DEFER_GROUP / NBG_GROUP_LAG cannot be captured in a graph");
   if (capturing && h->pending)
     return set_error(NBG_EINVAL, "classify: a lagged group is pending (nbg_maglev_finish_group before capturing)");
-  // NBG_GRAPH_ANY=1 (diagnostic builds of the capture root-cause experiment, tools/gpu_graph_rootcause.sh):
-  // let multi-launch batches be captured too
-  static const bool graph_any = [] {
-    const char* e = std::getenv("NBG_GRAPH_ANY");
-    return e && std::atoi(e) != 0;
-  }();
-  if (capturing && !graph_any && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
-    return set_error(NBG_EINVAL, "classify: only single-launch batches (<= 2048 packets, <= %u backends, 16-B aligned) "
-                     "can be captured in a graph", kMaxGroupBins - 1);
+  // A graph keeps the pointers it was captured with, so a captured call must not use scratch that a
+  // later eager call may reallocate: the NBG_LUT_TILED buckets and the fixed_len array that
+  // descriptor batches without lengths get (grown on demand).  Everything else it touches is
+  // allocated with the handle.
+  if (capturing && (flags & NBG_LUT_TILED))
+    return set_error(NBG_EINVAL, "classify: NBG_LUT_TILED cannot be captured in a graph (its scratch grows)");
+  if (capturing && d_off && !d_len && !(!lpm && use_small(n_pkts, nbins, flags, d_pkts)))
+    return set_error(NBG_EINVAL, "classify: pass d_len to capture a descriptor batch of more than %u packets",
+                     small_max());
   int rc = capturing ? NBG_OK : order_after_last(h, static_cast<hipStream_t>(stream));
   if (rc) return rc;
   const bool lds = use_lds_lut(h, flags);
@@ -1088,6 +1093,213 @@ int nbg_maglev_check(nbg_maglev* h) {
   NBG_HIP(hipStreamSynchronize(h->last_stream));
   NBG_HIP(hipGetLastError());
   return NBG_OK;
+}
+
+// ---- persistent RX ring (nbg_ring_*) ---------------------------------------------------------------
+}  // extern "C"
+
+struct nbg_ring {
+  nbg_maglev* h = nullptr;
+  hipStream_t stream = nullptr;
+  uint8_t* host = nullptr;  // pinned, mapped: RingCtl | RingDesc[slots] | prog[grid]
+  volatile RingCtl* ctl = nullptr;
+  RingDesc* desc = nullptr;
+  volatile uint32_t* prog = nullptr;
+  uint32_t slots = NBG_RING_SLOTS;
+  int grid = 0;
+  uint32_t idle_ms = 0;
+  uint64_t posted = 0, units = 0, completed = 0;
+  bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
+};
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+// Completed batches: every block reports how many batches are complete for it; the ring's count is
+// the minimum (as a lag behind `posted`, so that 32-bit counts may wrap).
+void ring_refresh(nbg_ring* r) {
+  const uint32_t p32 = static_cast<uint32_t>(r->posted);
+  uint32_t lag = 0;
+  for (int b = 0; b < r->grid; ++b) lag = std::max(lag, p32 - r->prog[b]);
+  r->completed = r->posted - lag;
+}
+
+// The kernel has ended?  (hipStreamQuery: the ring kernel is the last work on its stream.)
+bool ring_ended(nbg_ring* r) {
+  if (!r->ended && hipStreamQuery(r->stream) != hipErrorNotReady) r->ended = true;
+  return r->ended;
+}
+
+int ring_state_error(nbg_ring* r) {
+  if (r->ctl->error) return set_error(NBG_ETIMEDOUT, "ring: the kernel ended after %u ms without a post", r->idle_ms);
+  return set_error(NBG_EIO, "ring: the kernel has ended (%s)", hipGetErrorString(hipStreamQuery(r->stream)));
+}
+
+void ring_pause(Clock::time_point t0) {
+  if (Clock::now() - t0 > std::chrono::microseconds(200)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms, void* stream,
+                   nbg_ring** out) {
+  if (!h || !out) return set_error(NBG_EINVAL, "ring_start: null argument");
+  *out = nullptr;
+  if (h->ring) return set_error(NBG_EINVAL, "ring_start: the handle already runs a ring");
+  if (h->wide || h->m > 65537) return set_error(NBG_EINVAL, "ring_start: needs <= 255 backends and M <= 65537");
+  if (stride % 16 || stride < 64 || stride >= (1u << 24) || fixed_len < 48)
+    return set_error(NBG_EINVAL, "ring_start: fixed slots with stride %% 16 == 0, 64 <= stride < 2^24, fixed_len >= 48");
+  if (flags & ~NBG_SWAP_MACS) return set_error(NBG_EINVAL, "ring_start: flags other than NBG_SWAP_MACS");
+  if (h->pending) return set_error(NBG_EINVAL, "ring_start: a deferred or lagged group is pending");
+  DeviceGuard g(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = order_after_last(h, s);  // the ring runs after the handle's earlier work
+  if (rc) return rc;
+  auto* r = new (std::nothrow) nbg_ring;
+  if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
+  r->h = h;
+  r->stream = s;
+  r->grid = h->cus;
+  r->idle_ms = idle_ms ? idle_ms : 2000u;
+  const size_t bytes = sizeof(RingCtl) + r->slots * sizeof(RingDesc) + static_cast<size_t>(r->grid) * 4u;
+  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipSuccess) {
+    delete r;
+    return set_error(NBG_ENOMEM, "ring_start: pinned ring of %zu B", bytes);
+  }
+  std::memset(r->host, 0, bytes);
+  r->ctl = reinterpret_cast<RingCtl*>(r->host);
+  r->desc = reinterpret_cast<RingDesc*>(r->host + sizeof(RingCtl));
+  r->prog = reinterpret_cast<uint32_t*>(r->host + sizeof(RingCtl) + r->slots * sizeof(RingDesc));
+  uint8_t* dev = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), r->host, 0) != hipSuccess) {
+    (void)hipHostFree(r->host);
+    delete r;
+    return set_error(NBG_EIO, "ring_start: device address of the pinned ring");
+  }
+  ClassifyArgs a{};
+  a.stride = stride;
+  a.fixed_len = fixed_len;
+  a.lut = h->d_lut;
+  a.m = static_cast<uint32_t>(h->m);
+  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
+  a.nb = h->nb;
+  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  a.win_owned = 1;
+  a.wb_full = 1;
+  a.lean = 1;
+  a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
+  a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+  RingArgs ra{};
+  ra.ctl = reinterpret_cast<RingCtl*>(dev);
+  ra.desc = reinterpret_cast<const RingDesc*>(dev + sizeof(RingCtl));
+  ra.prog = reinterpret_cast<uint32_t*>(dev + sizeof(RingCtl) + r->slots * sizeof(RingDesc));
+  ra.slots = r->slots;
+  ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
+  const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
+  ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
+  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid, s))) {
+    (void)hipHostFree(r->host);
+    delete r;
+    return rc;
+  }
+  h->ring = r;
+  h->last_stream = s;
+  h->issued = true;
+  *out = r;
+  return NBG_OK;
+}
+
+int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
+  if (!r || !ticket) return set_error(NBG_EINVAL, "ring_post: null argument");
+  if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "ring_post: n_pkts must be < 2^30");
+  if (n_pkts && (!d_pkts || !d_backend || (reinterpret_cast<uintptr_t>(d_pkts) & 15u) ||
+                 (reinterpret_cast<uintptr_t>(d_backend) & 15u)))
+    return set_error(NBG_EINVAL, "ring_post: packet and backend buffers must be 16-B aligned");
+  // a free slot: the batch `slots` back is complete
+  const auto t0 = Clock::now();
+  while (r->posted - r->completed >= r->slots) {
+    ring_refresh(r);
+    if (r->posted - r->completed < r->slots) break;
+    if (r->ctl->error || ring_ended(r)) return ring_state_error(r);
+    if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 1000u))
+      return set_error(NBG_ETIMEDOUT, "ring_post: no slot freed in %u ms", r->idle_ms + 1000u);
+    ring_pause(t0);
+  }
+  if (r->ctl->error || ring_ended(r)) return ring_state_error(r);
+  const uint64_t j = r->posted;
+  const uint64_t units = ((n_pkts + 63) / 64 + 7) / 8;  // 512-packet units of 8 waves' tiles
+  RingDesc d{};
+  d.pkts = reinterpret_cast<uintptr_t>(d_pkts);
+  d.backend = reinterpret_cast<uintptr_t>(d_backend);
+  d.ulo = r->units;
+  d.uhi = r->units + units;
+  d.n_pkts = static_cast<uint32_t>(n_pkts);
+  d.seq = static_cast<uint32_t>(j + 1);
+  d.check = ring_check(d.pkts, d.backend, d.ulo, d.uhi, d.n_pkts, d.seq);
+  // one 64-B line: a device read that overlaps this write fails the check and is retried
+  volatile uint64_t* dst = reinterpret_cast<volatile uint64_t*>(r->desc + (j & (r->slots - 1)));
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(&d);
+  for (int i = 0; i < 8; ++i) dst[i] = src[i];
+  std::atomic_thread_fence(std::memory_order_release);
+  r->posted = j + 1;
+  r->units += units;
+  *ticket = j;
+  return NBG_OK;
+}
+
+int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
+  if (!r || !completed) return set_error(NBG_EINVAL, "ring_poll: null argument");
+  ring_refresh(r);
+  *completed = r->completed;
+  if (r->completed < r->posted && (r->ctl->error || ring_ended(r))) return ring_state_error(r);
+  return NBG_OK;
+}
+
+int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms) {
+  if (!r) return set_error(NBG_EINVAL, "ring_wait: null ring");
+  if (ticket >= r->posted) return set_error(NBG_EINVAL, "ring_wait: ticket %llu was not posted", (unsigned long long)ticket);
+  const auto t0 = Clock::now();
+  for (;;) {
+    ring_refresh(r);
+    if (r->completed > ticket) return NBG_OK;
+    if (r->ctl->error || ring_ended(r)) {
+      ring_refresh(r);  // progress stored before the kernel ended
+      if (r->completed > ticket) return NBG_OK;
+      return ring_state_error(r);
+    }
+    if (timeout_ms && Clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+      return set_error(NBG_ETIMEDOUT, "ring_wait: batch %llu not complete after %u ms", (unsigned long long)ticket,
+                       timeout_ms);
+    ring_pause(t0);
+  }
+}
+
+int nbg_ring_stop(nbg_ring* r) {
+  if (!r) return set_error(NBG_EINVAL, "ring_stop: null ring");
+  DeviceGuard g(r->h->device);
+  __atomic_store_n(&const_cast<RingCtl*>(const_cast<volatile RingCtl*>(r->ctl))->stop, 1u, __ATOMIC_RELEASE);
+  const auto t0 = Clock::now();
+  int rc = NBG_OK;
+  while (!ring_ended(r)) {
+    if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 5000u)) {
+      // never free memory a running kernel may still read: leak the ring instead
+      r->h->ring = nullptr;
+      return set_error(NBG_ETIMEDOUT, "ring_stop: the kernel did not end");
+    }
+    ring_pause(t0);
+  }
+  const hipError_t e = hipStreamQuery(r->stream);
+  ring_refresh(r);
+  if (e != hipSuccess) rc = set_error(NBG_EIO, "ring_stop: %s", hipGetErrorString(e));
+  else if (r->completed < r->posted) rc = ring_state_error(r);
+  (void)hipHostFree(r->host);
+  r->h->ring = nullptr;
+  delete r;
+  return rc;
 }
 
 }  // extern "C"

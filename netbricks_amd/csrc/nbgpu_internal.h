@@ -7,8 +7,8 @@
 
 #include "../../include/nbgpu.h"
 
-#ifndef NBG_CAPTURE_ZERO_KERNEL
-#define NBG_CAPTURE_ZERO_KERNEL 0
+#ifndef NBG_CAPTURE_ZERO_KERNEL  // 0: memset nodes in captured calls (the HIP 7.0 null-stream fault)
+#define NBG_CAPTURE_ZERO_KERNEL 1
 #endif
 
 namespace nbg {
@@ -109,6 +109,48 @@ struct LagGroup {
   uint32_t hist16;            // rows of two 16-bit bins per word
 };
 
+// Persistent RX-ring classify (nbg_ring_*).  One batch per ring slot, in pinned host memory: written
+// by nbg_ring_post, read by the kernel over PCIe.  64 B, one line.
+struct RingDesc {
+  uint64_t pkts;
+  uint64_t backend;
+  uint64_t ulo, uhi;  // the batch's units [ulo, uhi) in the ring's unit sequence (512 packets each)
+  uint32_t n_pkts;
+  uint32_t seq;       // batch index + 1 (mod 2^32)
+  uint32_t pad[4];
+  uint64_t check;     // ring_check(): a read that overlaps the host rewriting the slot fails it
+};
+static_assert(sizeof(RingDesc) == 64, "one descriptor per 64-B line");
+struct RingCtl {      // pinned host memory, the first line
+  uint32_t stop;      // host: exit once nothing more is posted
+  uint32_t error;     // device: 1 = idle timeout (the kernel exited by itself)
+  uint32_t pad[14];
+};
+struct RingArgs {
+  RingCtl* ctl;
+  const RingDesc* desc;  // [slots]
+  uint32_t* prog;        // [grid] per block: batches all of whose units of this block are complete
+  uint32_t slots;        // power of two
+  uint32_t probe_step;   // NBG_SPROBE builds: the first of the 16 unit steps recorded
+  uint64_t idle_ticks;   // exit after this long (100 MHz wall clock) without a new batch
+};
+#ifdef __HIPCC__
+#define NBG_HD __host__ __device__
+#else
+#define NBG_HD
+#endif
+NBG_HD inline uint64_t ring_check(uint64_t pkts, uint64_t backend, uint64_t ulo, uint64_t uhi, uint32_t n_pkts,
+                                  uint32_t seq) {
+  uint64_t h = 0x6a09e667f3bcc909ull ^ (static_cast<uint64_t>(seq) << 32 | n_pkts);
+  const uint64_t w[4] = {pkts, backend, ulo, uhi};
+  for (int i = 0; i < 4; ++i) {
+    h ^= w[i] + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+  }
+  return h;
+}
+
 // NBG_LUT_TILED: bucket packets by 64-KiB LUT tile, then look them up per tile in LDS.
 struct TileArgs {
   const uint32_t* idx;      // [n_pkts] from the classify kernel (kIdx)
@@ -179,6 +221,10 @@ int launch_classify_stream_multi(const ClassifyArgs& a, const StreamBatches& sb,
 // lg.n_parts <= grid and (nb + 1) * lg.n_parts within the direct-scan limit (pick_group_scan)
 int launch_classify_stream_lag(const ClassifyArgs& a, const LagGroup& lg, int grid, void* stream);
 size_t stream_lds(uint32_t nb, int mode, bool lag);
+// The persistent ring kernel (nbg_ring_start): a.pkts / n_pkts / backend come from the ring; mode 0
+// read only, 1 MAC swap in place.  Returns after the launch; the kernel runs until stop or idle.
+int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int grid, void* stream);
+size_t ring_lds(int mode);
 int stream_waves_per_block();
 // Streaming classify for descriptor layouts with owned windows (u8 LUT in LDS, or the u16 LUT
 // gathered from L2); stream_desc_lds: its dynamic LDS bytes (mode 0 read only, 1 in place, 2 records).

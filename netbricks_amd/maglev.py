@@ -20,7 +20,7 @@ from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, 
                    NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
-__all__ = ["Maglev", "GroupedBatch", "build_lut", "make_trace", "NBG_SENTINEL"]
+__all__ = ["Maglev", "GroupedBatch", "Ring", "build_lut", "make_trace", "NBG_SENTINEL"]
 
 
 def _ptr(t) -> Optional[int]:
@@ -119,6 +119,9 @@ class Maglev:
         self.lut_size = lib.nbg_maglev_table_size(self._h)
 
     def close(self) -> None:
+        ring = self.__dict__.get("_ring")
+        if ring is not None:
+            ring.stop()
         if self._h:
             lib.nbg_maglev_destroy(self._h)
             self._h = C.c_void_p()
@@ -302,6 +305,12 @@ class Maglev:
         inflight[t] = (ptrs, lens, backend, perm, counts)
         return t
 
+    def ring(self, *, stride: int = 64, frame_len: int = 60, swap_macs: bool = False, idle_ms: int = 2000,
+             stream=None) -> "Ring":
+        """Start this handle's persistent RX ring (nbg_ring_start): one classify kernel on `stream`
+        (default: a new torch stream) that takes batches as they are posted until stop()."""
+        return Ring(self, stride=stride, frame_len=frame_len, swap_macs=swap_macs, idle_ms=idle_ms, stream=stream)
+
     def host_wait(self, ticket: int) -> None:
         check(lib.nbg_maglev_host_wait(self._h, ticket), "nbg_maglev_host_wait")
         self.__dict__.get("_inflight", {}).pop(ticket, None)
@@ -322,6 +331,75 @@ class Maglev:
                                           counts.ctypes.data if group else None)
         check(rc, "nbg_maglev_classify_host")
         return backend[:n], (perm[:n] if group else None), counts
+
+
+class Ring:
+    """A persistent RX ring (include/nbgpu.h, nbg_ring_*): one streaming-classify kernel that stays
+    resident and classifies device-resident fixed-slot batches as they are posted (the RX queue that
+    never stops, framework/src/operators/receive_batch.rs:26,52-61).  post() returns a ticket;
+    wait(ticket) / poll() report completion, after which the batch's backend[] (and in-place swap)
+    are in HBM.  The kernel owns its stream until stop() (or idle_ms without a post)."""
+
+    def __init__(self, mg: "Maglev", *, stride: int, frame_len: int, swap_macs: bool, idle_ms: int, stream=None):
+        import torch
+
+        self._mg = mg
+        self.stride, self.frame_len = stride, frame_len
+        self._stream = stream if stream is not None else torch.cuda.Stream(torch.device("cuda", mg.device))
+        st = self._stream.cuda_stream if hasattr(self._stream, "cuda_stream") else self._stream
+        h = C.c_void_p()
+        check(lib.nbg_ring_start(mg._h, stride, frame_len, NBG_SWAP_MACS if swap_macs else 0, idle_ms, st,
+                                 C.byref(h)), "nbg_ring_start")
+        self._r = h
+        self._held = {}  # ticket -> tensors the kernel reads or writes until the batch is complete
+        mg._ring = self  # Maglev.close() stops the ring first (the handle frees it otherwise)
+
+    def post(self, pkts, n_pkts: int, backend) -> int:
+        import torch
+
+        if self._r is None:
+            raise RuntimeError("ring: stopped")
+        dev = torch.device("cuda", self._mg.device)
+        if pkts.dtype != torch.uint8 or not pkts.is_contiguous() or pkts.device != dev:
+            raise ValueError(f"pkts: expected a contiguous uint8 tensor on {dev}")
+        if n_pkts and pkts.numel() < (n_pkts - 1) * self.stride + _slot_tail(self.stride, self.frame_len):
+            raise ValueError("pkts: too small for n_pkts slots")
+        _check_dev("backend", backend, torch.uint16, n_pkts, dev)
+        t = C.c_uint64()
+        check(lib.nbg_ring_post(self._r, _ptr(pkts), n_pkts, _ptr(backend), C.byref(t)), "nbg_ring_post")
+        self._held[t.value] = (pkts, backend)
+        return t.value
+
+    def poll(self) -> int:
+        c = C.c_uint64()
+        check(lib.nbg_ring_poll(self._r, C.byref(c)), "nbg_ring_poll")
+        for k in [k for k in self._held if k < c.value]:
+            del self._held[k]
+        return c.value
+
+    def wait(self, ticket: int, timeout_ms: int = 10000) -> None:
+        check(lib.nbg_ring_wait(self._r, ticket, timeout_ms), "nbg_ring_wait")
+        for k in [k for k in self._held if k <= ticket]:
+            del self._held[k]
+
+    def stop(self) -> None:
+        if self._r is not None:
+            r, self._r = self._r, None
+            self._held.clear()
+            self._mg.__dict__.pop("_ring", None)
+            check(lib.nbg_ring_stop(r), "nbg_ring_stop")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    def __del__(self):
+        try:
+            self.stop()
+        except Exception:  # noqa: BLE001 (interpreter teardown)
+            pass
 
 
 class HostRegion:
