@@ -190,7 +190,7 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
  * producer thread per ring.  Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
  * flags: 0 (read only) or NBG_SWAP_MACS (in place).
  */
-#define NBG_RING_SLOTS 16u
+#define NBG_RING_SLOTS 64u
 typedef struct nbg_ring nbg_ring;
 int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms,
                    void* stream, nbg_ring** out);

@@ -33,7 +33,7 @@ NBG_STREAM_DESC = 0x40
 NBG_GROUP_LAG = 0x80
 NBG_HOST_SLOTS = 3
 NBG_MAX_MULTI = 8
-NBG_RING_SLOTS = 16
+NBG_RING_SLOTS = 64
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 

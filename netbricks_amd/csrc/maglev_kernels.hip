@@ -143,7 +143,9 @@ __device__ __forceinline__ uint32_t classify_slow(const ClassifyArgs& a, const u
     return *x;
   };
   auto wr = [](uint8_t* x, uint8_t v) {
-    if constexpr (WT) __hip_atomic_store(x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (WT)  // global (not flat): a flat store would also count in lgkmcnt
+      __hip_atomic_store((__attribute__((address_space(1))) uint8_t*)(x), v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     else *x = v;
   };
   gate = kSentinel;
@@ -1288,9 +1290,15 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 //   waited for tile k (the unit barrier of step k), the stores of steps <= k - 3 retired.  Wave 0
 //   then publishes, per block, the count of batches all of whose units of this block are complete
 //   (one system-scope store to pinned memory when the count changes); the host takes the minimum.
+#ifndef NBG_RING_ABL  // measurement builds (tools/build_ab.sh): 1 plain backend stores, 2 none
+#define NBG_RING_ABL 0
+#endif
+#ifndef NBG_RING_WARM  // the control wave's page touches ahead of a batch (0: off, A/B builds)
+#define NBG_RING_WARM 1
+#endif
 constexpr uint32_t kRingCache = 4;  // batch descriptors in LDS (from the current unit's batch on)
 constexpr uint32_t kRingFetch = 2;  // ring slots per prefetch (one LDS-DMA dword load, 32 lanes)
-constexpr uint32_t kRingCtlWords = kRingCache * 16u + kRingFetch * 16u + 4u + kStreamW * 32u;
+constexpr uint32_t kRingCtlWords = kRingCache * 16u + kRingFetch * 16u + 4u + kStreamW * 32u + 16u;
 
 __device__ __forceinline__ void glds4_sys(const void* src, uint32_t lds_base) {
   uint32_t keep;
@@ -1307,153 +1315,206 @@ __device__ __forceinline__ void glds4_sys(const void* src, uint32_t lds_base) {
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
+#ifdef NBG_SPROBE  // diagnostic builds: per block [0] prefetches issued, [1] batches taken from them,
+                   // [2] prefetches that took none, [3] idle entries; [4..19] block 0's last failed stage
+__device__ unsigned int g_ringdbg[1024 * 20];
+#define RINGDBG(i, v) \
+  if (lane == 0) g_ringdbg[blockIdx.x * 20 + (i)] += (v);
+#else
+#define RINGDBG(i, v)
+#endif
+
+// The ring kernel's cursor over the known batches (block-uniform; loaded from the LDS descriptor cache)
+struct RingCursor {
+  uint32_t j;  // batch index (0xffffffff: none yet)
+  uint64_t lo, hi;
+  uint8_t* pkts;
+  uint16_t* backend;
+  uint32_t n;
+};
+
+__device__ __forceinline__ void ring_load(RingCursor& c, const uint32_t* cache, uint32_t j) {
+  const uint32_t* e = cache + (j % kRingCache) * 16u;
+  c.j = j;
+  c.pkts = reinterpret_cast<uint8_t*>(static_cast<uintptr_t>(rfl(e[0])) | static_cast<uintptr_t>(rfl(e[1])) << 32);
+  c.backend = reinterpret_cast<uint16_t*>(static_cast<uintptr_t>(rfl(e[2])) | static_cast<uintptr_t>(rfl(e[3])) << 32);
+  c.lo = static_cast<uint64_t>(rfl(e[4])) | static_cast<uint64_t>(rfl(e[5])) << 32;
+  c.hi = static_cast<uint64_t>(rfl(e[6])) | static_cast<uint64_t>(rfl(e[7])) << 32;
+  c.n = rfl(e[8]);
+}
+
+// Move c forward to the batch holding unit u; false when u lies past the known batches.
+__device__ __forceinline__ bool ring_seek(RingCursor& c, const uint32_t* cache, uint64_t u, uint32_t known) {
+  while (u >= c.hi) {
+    const uint32_t nj = c.j + 1u;
+    if (static_cast<int32_t>(nj - known) >= 0) return false;
+    ring_load(c, cache, nj);
+  }
+  return true;
+}
+
+// Take the staged descriptor d (every lane reads its 16 words) as batch known_w if it is that batch
+// (seq and check match) and the cache has room past `base` (the oldest batch a cursor may still load).
+__device__ __forceinline__ bool ring_take(const uint32_t* d, uint32_t* cache, uint32_t& known_w, uint32_t base,
+                                          uint32_t lane) {
+  const uint4 w0 = *reinterpret_cast<const uint4*>(d), w1 = *reinterpret_cast<const uint4*>(d + 4);
+  const uint4 w2 = *reinterpret_cast<const uint4*>(d + 8), w3 = *reinterpret_cast<const uint4*>(d + 12);
+  const uint64_t pk = w0.x | static_cast<uint64_t>(w0.y) << 32, be = w0.z | static_cast<uint64_t>(w0.w) << 32;
+  const uint64_t lo = w1.x | static_cast<uint64_t>(w1.y) << 32, hi = w1.z | static_cast<uint64_t>(w1.w) << 32;
+  const uint64_t ck = w3.z | static_cast<uint64_t>(w3.w) << 32;
+  const bool ok = w2.y == known_w + 1u && ck == ring_check(pk, be, lo, hi, w2.x, w2.y) && known_w - base < kRingCache;
+  if (!rfl(ok ? 1u : 0u)) return false;
+  // copy the words just checked (d may be rewritten by a landing prefetch meanwhile)
+  const uint4 q = (lane >> 2) == 0 ? w0 : ((lane >> 2) == 1 ? w1 : ((lane >> 2) == 2 ? w2 : w3));
+  const uint32_t x = (lane & 3u) == 0 ? q.x : ((lane & 3u) == 1 ? q.y : ((lane & 3u) == 2 ? q.z : q.w));
+  if (lane < 16) cache[(known_w % kRingCache) * 16u + lane] = x;
+  ++known_w;
+  return true;
+}
+
+// Wave 0, idle: read ring slots (and the stop word) until a new batch is taken; true = exit (stop
+// with nothing posted, or idle_ticks without a batch: then the error word is set).
+__device__ __forceinline__ bool ring_poll(const RingArgs& r, uint32_t* stage, uint32_t* cache, uint32_t& known_w,
+                                          uint32_t base, uint32_t lane) {
+  const uint64_t t0 = wall_clock64();
+  const uint32_t known0 = known_w;
+  for (uint32_t nap = 1;; nap = min(2u * nap, 16u)) {
+    for (;;) {  // every consecutive batch that is posted (and fits)
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
+      if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_wave_barrier();
+      if (!ring_take(stage, cache, known_w, base, lane)) break;
+    }
+    if (known_w != known0) return false;
+    if (rfl(__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+      // a batch posted before the stop is in its slot by now: look once more
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
+      if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_wave_barrier();
+      return !ring_take(stage, cache, known_w, base, lane);
+    }
+    if (static_cast<uint64_t>(wall_clock64()) - t0 > r.idle_ticks) {
+      if (lane == 0) __hip_atomic_store(&r.ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return true;
+    }
+    // back off to 16 x 512 clocks (~3.5 us) between polls: the idle grid reads a few GB/s over PCIe
+    for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+constexpr int kRingNT = kStreamNT + 64;  // the tile waves plus the control wave
+
 template <bool F4, int MODE>
-__global__ __launch_bounds__(kStreamNT, 1) void classify_ring_kernel(ClassifyArgs a, RingArgs r) {
+__global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs a, RingArgs r) {
   static_assert(MODE == 0 || MODE == 1, "the ring classifies read only or in place");
   constexpr uint32_t kRow = stream_row_of<MODE>(), kTileLds = 64u * kRow;
   extern __shared__ __align__(16) uint8_t smem[];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = rfl(tid >> 6);
+  // the control wave (the last) fetches descriptors, publishes completion and polls when idle: its
+  // PCIe reads are in no tile wave's vmcnt, so a slow read never holds a tile wait
+  const bool ctl = wave == static_cast<uint32_t>(kStreamW);
   uint8_t* lut = smem;
-  uint8_t* ring = smem + kLutLds + wave * (kRing * kTileLds);
+  uint8_t* ring = smem + kLutLds + (ctl ? 0u : wave) * (kRing * kTileLds);
   uint32_t* cache = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);  // [kRingCache][16]
-  uint32_t* stage = cache + kRingCache * 16u;   // [kRingFetch][16] wave 0's prefetch landing area
+  uint32_t* stage = cache + kRingCache * 16u;   // [kRingFetch][16] the control wave's prefetch landing area
   uint32_t* known_l = stage + kRingFetch * 16u;  // [2] known batches, by step parity; [2] exit
-  uint16_t* rep = reinterpret_cast<uint16_t*>(known_l + 4) + wave * 64u;  // this wave's 64 backends
+  uint16_t* rep = reinterpret_cast<uint16_t*>(known_l + 4) + (ctl ? 0u : wave) * 64u;  // a tile wave's 64 backends
+  uint32_t* warm_l = known_l + 4 + kStreamW * 32u;  // [16] landing words of the control wave's page touches
   const uint32_t ring_lds = rfl(lds_addr(ring)), lut_lds = rfl(lds_addr(lut)), stage_lds = rfl(lds_addr(stage));
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  SPROBE(0)
-  const uint32_t pieces_lut = a.lut_lds_bytes >> 10;
+  if (!ctl) { SPROBE(0) }
+  const uint32_t pieces_lut = ctl ? 0u : a.lut_lds_bytes >> 10;
   for (uint32_t q = wave; q < pieces_lut; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
   if (tid < 4) known_l[tid] = 0;
   wait_vm<0>();
   lds_sync();
-  SPROBE(1)
+  if (!ctl) { SPROBE(1) }
 
-  // cursors over the known batches: the unit being classified, and the unit whose tile is issued
-  struct Cursor {
-    uint32_t j;  // batch index (0xffffffff: none yet)
-    uint64_t lo, hi;
-    uint8_t* pkts;
-    uint16_t* backend;
-    uint32_t n;
-  };
-  auto load = [&](Cursor& c, uint32_t j) {
-    const uint32_t* e = cache + (j % kRingCache) * 16u;
-    c.j = j;
-    c.pkts = reinterpret_cast<uint8_t*>(static_cast<uintptr_t>(rfl(e[0])) | static_cast<uintptr_t>(rfl(e[1])) << 32);
-    c.backend = reinterpret_cast<uint16_t*>(static_cast<uintptr_t>(rfl(e[2])) | static_cast<uintptr_t>(rfl(e[3])) << 32);
-    c.lo = static_cast<uint64_t>(rfl(e[4])) | static_cast<uint64_t>(rfl(e[5])) << 32;
-    c.hi = static_cast<uint64_t>(rfl(e[6])) | static_cast<uint64_t>(rfl(e[7])) << 32;
-    c.n = rfl(e[8]);
-  };
-  uint32_t known = 0;  // block-uniform: read after a barrier
-  auto seek = [&](Cursor& c, uint64_t u) -> bool {
-    while (u >= c.hi) {
-      const uint32_t nj = c.j + 1u;
-      if (static_cast<int32_t>(nj - known) >= 0) return false;
-      load(c, nj);
-    }
-    return true;
-  };
-  Cursor cur{0xffffffffu, 0, 0, nullptr, nullptr, 0}, nxt = cur;
+  // cursors (every wave keeps them): the unit being classified, and the unit whose tile is issued
+  RingCursor cur{0xffffffffu, 0, 0, nullptr, nullptr, 0}, nxt = cur;
   const uint64_t Gu = G;
   uint32_t k = 0, iss = 0;                   // unit steps of this block classified / issued
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // VM operations issued; counts after tiles k, k+1, k+2
-  auto issue = [&](uint32_t t) -> bool {
-    const uint64_t u = b + static_cast<uint64_t>(t) * Gu;
-    if (!seek(nxt, u)) return false;
-    ClassifyArgs v = a;
-    v.pkts = nxt.pkts;
-    v.n_pkts = nxt.n;
-    issue_tile<kRow, true>(v, static_cast<uint32_t>(((u - nxt.lo) * kStreamW + wave) * 64u),
-                           ring_lds + (rfl(t) % kRing) * kTileLds, lane);
-    seq += 4;
-    const uint32_t d = t - k;
-    if (d == 0) sA = seq;
-    else if (d == 1) sB = seq;
-    else sC = seq;
-    ++iss;
-    return true;
-  };
-
-  // wave 0's descriptor state
-  uint32_t known_w = 0, pf_seq = 0, pf_base = 0, last_pf = 0, pub = 0;
+  // the control wave's descriptor state
+  uint32_t known_w = 0, pf_base = 0, last_pf = 0, pub = 0, warmed = 0xffffffffu;
   bool pf = false;
-  uint32_t hA = 0xffffffffu, hB = 0xffffffffu;  // batch of the unit of steps k - 1, k - 2
-  // take staged descriptor i (every lane reads all 16 words) as batch known_w when it is that batch
-  auto take = [&](const uint32_t* d) -> bool {
-    const uint4 w0 = *reinterpret_cast<const uint4*>(d), w1 = *reinterpret_cast<const uint4*>(d + 4);
-    const uint4 w2 = *reinterpret_cast<const uint4*>(d + 8), w3 = *reinterpret_cast<const uint4*>(d + 12);
-    const uint64_t pk = w0.x | static_cast<uint64_t>(w0.y) << 32, be = w0.z | static_cast<uint64_t>(w0.w) << 32;
-    const uint64_t lo = w1.x | static_cast<uint64_t>(w1.y) << 32, hi = w1.z | static_cast<uint64_t>(w1.w) << 32;
-    const uint64_t ck = w3.z | static_cast<uint64_t>(w3.w) << 32;
-    const uint32_t base = cur.j == 0xffffffffu ? 0u : cur.j;
-    const bool ok = w2.y == known_w + 1u && ck == ring_check(pk, be, lo, hi, w2.x, w2.y) && known_w - base < kRingCache;
-    if (!rfl(ok ? 1u : 0u)) return false;
-    if (lane < 16) cache[(known_w % kRingCache) * 16u + lane] = d[lane];
-    ++known_w;
-    return true;
-  };
-  auto publish = [&](uint32_t v) {  // batches < v complete for this block
-    if (static_cast<int32_t>(v - pub) > 0) {
-      pub = v;
-      if (lane == 0) __hip_atomic_store(r.prog + b, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      ++seq;
-    }
-  };
-  // idle: poll the next ring slot (and the stop word); returns true to exit
-  auto poll = [&]() -> bool {
-    const uint64_t t0 = wall_clock64();
-    for (uint32_t nap = 1;; nap = min(2u * nap, 16u)) {
-      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
-      uint32_t w = 0;
-      if (lane < 16) w = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (lane < 16) stage[lane] = w;
-      __builtin_amdgcn_wave_barrier();
-      while (take(stage)) {
-        if (lane < 16) stage[lane] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u))) + lane,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_wave_barrier();
-      }
-      if (known_w != known) return false;
-      if (rfl(__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
-        // a batch posted before the stop is in its slot by now: look once more
-        if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_wave_barrier();
-        if (take(stage)) return false;
-        return true;
-      }
-      if (wall_clock64() - t0 > r.idle_ticks) {
-        if (lane == 0) __hip_atomic_store(&r.ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return true;
-      }
-      // back off to 16 x 512 clocks (~3.5 us) between polls: the idle grid reads a few GB/s over PCIe
-      for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);
-    }
-  };
+  const uint32_t warm_lds = rfl(lds_addr(warm_l));
+  uint32_t hA = 0xffffffffu, hB = 0xffffffffu, hC = 0xffffffffu;  // batch of the unit of steps k - 1, k - 2, k - 3
+  // a step's backends are stored one step late, behind the next tile issue: the wait for a tile then
+  // covers the write-through stores of four steps back, not three, so their longer acks stay off the
+  // critical path
+  uint4 pw = make_uint4(0, 0, 0, 0);
+  uint16_t* pp = nullptr;
+  bool pend = false;
+
+// the tile of unit step `t` into ring buffer t % kRing (the issue cursor moves to its batch; the
+// control wave only moves its cursor)
+#define RING_ISSUE(t, ok)                                                                                    \
+  {                                                                                                         \
+    const uint64_t u_ = b + static_cast<uint64_t>(t) * Gu;                                                  \
+    ok = ring_seek(nxt, cache, u_, known);                                                                  \
+    if (ok) {                                                                                               \
+      if (!ctl) {                                                                                           \
+        ClassifyArgs v_ = a;                                                                                \
+        v_.pkts = nxt.pkts;                                                                                 \
+        v_.n_pkts = nxt.n;                                                                                  \
+        issue_tile<kRow, true>(v_, static_cast<uint32_t>(((u_ - nxt.lo) * kStreamW + wave) * 64u),         \
+                               ring_lds + (rfl(t) % kRing) * kTileLds, lane);                               \
+        seq += 4;                                                                                           \
+        const uint32_t d_ = (t) - k;                                                                        \
+        if (d_ == 0) sA = seq;                                                                              \
+        else if (d_ == 1) sB = seq;                                                                         \
+        else sC = seq;                                                                                      \
+      }                                                                                                     \
+      ++iss;                                                                                                \
+    }                                                                                                       \
+  }
+// batches < v complete for this block (the control wave; one system-scope store when the count moves)
+#define RING_PUBLISH(v)                                                                                      \
+  {                                                                                                         \
+    const uint32_t v_ = (v);                                                                                \
+    if (static_cast<int32_t>(v_ - pub) > 0) {                                                               \
+      pub = v_;                                                                                             \
+      if (lane == 0) __hip_atomic_store(r.prog + b, v_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);       \
+    }                                                                                                       \
+  }
+// take what has landed of the control wave's prefetch (the LDS-DMA may still be in flight: a slot not
+// yet landed, torn, or not yet posted fails ring_take's seq / check test and is fetched again)
+#define RING_TAKE_STAGED(base)                                                                               \
+  {                                                                                                         \
+    uint32_t i_ = 0;                                                                                        \
+    for (; i_ < kRingFetch && pf_base + i_ == known_w; ++i_)                                                \
+      if (!ring_take(stage + i_ * 16u, cache, known_w, (base), lane)) break;                               \
+    RINGDBG(1, known_w - pf_base)                                                                           \
+    if (i_ == kRingFetch) pf = false;                                                                       \
+  }
 
   for (;;) {
-    known = rfl(known_l[k & 1u]);
-    while (iss < k + kRing && issue(iss)) {
-    }
+    const uint32_t known = rfl(known_l[k & 1u]);  // block-uniform: written before the last barrier
+    for (bool ok = true; ok && iss < k + kRing;) RING_ISSUE(iss, ok)
     if (iss == k) {
-      // nothing to classify: drain, then wave 0 fetches descriptors (polling while none is posted).
-      // No issued unit waits for cur, so it takes nxt's place: the descriptor cache then only keeps
-      // batches past the issue cursor (which has walked every known batch), and a block with no unit
-      // in several small batches still gets room to take the next ones.
+      // nothing to classify: drain, then the control wave fetches descriptors (polling while none is
+      // posted).  No issued unit waits for cur, so it takes nxt's place: the descriptor cache then
+      // only keeps batches past the issue cursor (which has walked every known batch), and a block
+      // with no unit in several small batches still gets room to take the next ones.
       cur = nxt;
+      if (pend) {
+        if (lane < 8u) stg16_wt(pp, pw);
+        pend = false;
+      }
       wait_vm<0>();
       lds_sync();
-      if (wave == 0) {
+      if (ctl) {
+        RINGDBG(3, 1)
+        const uint32_t base = cur.j == 0xffffffffu ? 0u : cur.j;
         if (pf) {  // landed (vmcnt(0) above)
-          for (uint32_t i = 0; i < kRingFetch && pf_base + i == known_w; ++i)
-            if (!take(stage + i * 16u)) break;
+          RING_TAKE_STAGED(base)
           pf = false;
         }
-        publish(known);  // every unit of this block in batches < known is complete
-        const bool ex = known_w == known && poll();
+        RING_PUBLISH(known)  // every unit of this block in batches < known is complete
+        const bool ex = known_w == known && ring_poll(r, stage, cache, known_w, base, lane);
         if (lane == 0) {
           known_l[k & 1u] = known_w;
           known_l[2] = ex ? 1u : 0u;
@@ -1463,80 +1524,123 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_ring_kernel(ClassifyArg
       if (rfl(known_l[2])) break;
       continue;
     }
-#if NBG_SEQWAIT
-    wait_vm_n(seq - sA);
-#else
-    wait_vm<0>();
-#endif
-#ifdef NBG_SPROBE
-    if (k - r.probe_step < 16u) { SPROBE(2 + (k - r.probe_step)) }
-#endif
     const uint64_t u = b + static_cast<uint64_t>(k) * Gu;
-    seek(cur, u);
+    ring_seek(cur, cache, u, known);
     const uint32_t h0 = cur.j;
-    if (wave == 0) {
-      // descriptor prefetch: take a landed one (its LDS-DMA retired: pf_seq <= sA), then issue the
-      // next ahead of this step's tile, so the wait for that tile covers it
-      if (pf && static_cast<int32_t>(sA - pf_seq) >= 0) {
-        for (uint32_t i = 0; i < kRingFetch && pf_base + i == known_w; ++i)
-          if (!take(stage + i * 16u)) break;
-        pf = false;
+    if (ctl) {
+      // descriptor prefetch: take what has landed, then fetch the next slots when the issue cursor
+      // is within two batches of the known ones (again after 6 steps when they were not posted yet)
+      if (pf) {
+        const uint32_t kw0 = known_w;
+        RING_TAKE_STAGED(cur.j)
+        if (known_w == kw0 && k - last_pf >= 6u) {
+          pf = false;
+          RINGDBG(2, 1)
+        }
       }
-      if (!pf && known_w - cur.j < kRingCache && known_w - nxt.j <= 2u && k - last_pf >= 4u) {
+      if (!pf && known_w - cur.j < kRingCache && known_w - nxt.j <= 2u) {
+        if (lane < 16u * kRingFetch) stage[lane] = 0u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pf_base = known_w;
         if (lane < 16u * kRingFetch)
           glds4_sys(reinterpret_cast<const uint32_t*>(r.desc + ((known_w + lane / 16u) & (r.slots - 1u))) + (lane & 15u),
                     stage_lds);
-        ++seq;
-        pf_seq = seq;
         pf = true;
         last_pf = k;
+        RINGDBG(0, 1)
+      }
+#if NBG_RING_WARM
+      // address translation ahead of a batch: once the next batch is known, touch the first line of
+      // each of this block's units in it (packets and backend[]), one LDS-DMA dword per lane that no
+      // wave ever waits for, so the page walks happen steps before its tiles are issued (measured:
+      // a batch boundary cost ~2.5 us more than a step without)
+      if (static_cast<int32_t>(nxt.j + 1u - known_w) < 0 && warmed != nxt.j + 1u) {
+        warmed = nxt.j + 1u;
+        RingCursor w;
+        ring_load(w, cache, warmed);
+        const uint64_t first = w.lo + ((b + Gu - w.lo % Gu) % Gu);  // this block's first unit of the batch
+        const uint64_t unit = first + static_cast<uint64_t>(lane & 7u) * Gu;
+        if (lane < 16u && unit < w.hi) {
+          const uint64_t pkt = (unit - w.lo) * kStreamW * 64u;
+          const void* src = lane < 8u ? static_cast<const void*>(w.pkts + pkt * a.stride)
+                                      : static_cast<const void*>(w.backend + pkt);
+          glds4(src, warm_lds);
+        }
+      }
+#endif
+      if (lane == 0) known_l[(k + 1u) & 1u] = known_w;
+    } else {
+#if NBG_SEQWAIT
+      wait_vm_n(seq - sA);
+#else
+      wait_vm<0>();
+#endif
+#ifdef NBG_SPROBE
+      if (k - r.probe_step < 16u) { SPROBE(2 + (k - r.probe_step)) }
+#endif
+      ClassifyArgs v = a;
+      v.pkts = cur.pkts;
+      v.n_pkts = cur.n;
+      v.backend = cur.backend;
+      const uint32_t tb = static_cast<uint32_t>(((u - cur.lo) * kStreamW + wave) * 64u);
+      const uint32_t p = tb + lane;
+      uint32_t bin = 0;
+      bool slow = false;
+      const bool valid = tb < v.n_pkts && stream_classify<F4, MODE, kRow, true>(
+                                              v, lut, ring + (k % kRing) * kTileLds + lane * kRow, p, bin, slow);
+      if (iss == k + kRing) {  // the next tile into the buffer just read
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bool ok;
+        RING_ISSUE(iss, ok)
+      }
+      if (pend) {  // the previous step's backends
+#if NBG_RING_ABL == 1  // measurement build: plain stores (results not visible at completion)
+        if (lane < 8u) *reinterpret_cast<uint4*>(pp) = pw;
+#elif NBG_RING_ABL == 2  // measurement build: no backend stores
+#else
+        if (lane < 8u) stg16_wt(pp, pw);
+#endif
+        ++seq;
+        pend = false;
+      }
+      if (valid && slow) {
+        uint32_t gate;
+        bin = classify_slow<kLdsU8Tail, F4, false, true, true>(v, lut, v.pkts + static_cast<size_t>(p) * v.stride,
+                                                               v.fixed_len, p, gate);
+      }
+      if (tb < v.n_pkts) {
+        const uint16_t be = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
+        const uint32_t cnt = min(64u, v.n_pkts - tb);
+        if (cnt == 64u) {  // 16 B per lane: lanes 0..7 store the wave's 128 B (next step)
+          rep[lane] = be;
+          asm volatile("" ::: "memory");  // the u16 writes before the 16-B reads of the same words
+          __builtin_amdgcn_wave_barrier();
+          pw = reinterpret_cast<const uint4*>(rep)[lane & 7u];
+          pp = v.backend + tb + (lane & 7u) * 8u;
+          pend = true;
+        } else {
+          if (valid)
+            __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(v.backend + p), be, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          ++seq;
+        }
       }
     }
-    ClassifyArgs v = a;
-    v.pkts = cur.pkts;
-    v.n_pkts = cur.n;
-    v.backend = cur.backend;
-    const uint32_t tb = static_cast<uint32_t>(((u - cur.lo) * kStreamW + wave) * 64u);
-    const uint32_t p = tb + lane;
-    uint32_t bin = 0;
-    bool slow = false;
-    const bool valid = tb < v.n_pkts &&
-                       stream_classify<F4, MODE, kRow, true>(v, lut, ring + (k % kRing) * kTileLds + lane * kRow, p, bin, slow);
-    if (iss == k + kRing) {  // the next tile into the buffer just read
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      issue(iss);
-    }
-    if (valid && slow) {
-      uint32_t gate;
-      bin = classify_slow<kLdsU8Tail, F4, false, true, true>(v, lut, v.pkts + static_cast<size_t>(p) * v.stride,
-                                                             v.fixed_len, p, gate);
-    }
-    if (tb < v.n_pkts) {
-      const uint16_t be = static_cast<uint16_t>(bin == a.nb ? kSentinel : bin);
-      const uint32_t cnt = min(64u, v.n_pkts - tb);
-      if (cnt == 64u) {  // 16 B per lane: lanes 0..7 store the wave's 128 B
-        rep[lane] = be;
-        asm volatile("" ::: "memory");  // the u16 writes before the 16-B reads of the same words
-        __builtin_amdgcn_wave_barrier();
-        const uint4 w = reinterpret_cast<const uint4*>(rep)[lane & 7u];
-        if (lane < 8u) stg16_wt(v.backend + tb + lane * 8u, w);
-      } else if (valid) {
-        __hip_atomic_store(v.backend + p, be, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      ++seq;
-    }
-    if (wave == 0 && lane == 0) known_l[(k + 1u) & 1u] = known_w;
     lds_sync();
-    // every wave has waited for tile k: the stores of steps <= k - 3 retired
-    if (wave == 0 && hB != 0xffffffffu) publish(hB);
+    // every tile wave has waited for tile k: the stores of steps <= k - 4 retired (the backends of
+    // step k - 3 went out behind tile k's issue)
+    if (ctl && hC != 0xffffffffu) RING_PUBLISH(hC)
+    hC = hB;
     hB = hA;
     hA = h0;
     sA = sB;
     sB = sC;
     ++k;
   }
-  SPROBE(19)
+#undef RING_ISSUE
+#undef RING_PUBLISH
+#undef RING_TAKE_STAGED
+  if (!ctl) { SPROBE(19) }
 }
 
 // ---- streaming classify for descriptor layouts (IMIX: u32 offsets + u16 lengths, owned windows) ----
@@ -2656,7 +2760,7 @@ int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
       hipSuccess)
     return set_error(NBG_EIO, "ring classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(kStreamNT), ring_lds(mode), static_cast<hipStream_t>(stream), a, r);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(kRingNT), ring_lds(mode), static_cast<hipStream_t>(stream), a, r);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "ring classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -2909,6 +3013,12 @@ int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int
 extern "C" int nbg_debug_sprobe(unsigned long long* out, uint64_t n) {
   if (n > nbg::kSProbeWaves * nbg::kSProbeSlots) n = nbg::kSProbeWaves * nbg::kSProbeSlots;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_sprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
+}
+#endif
+#ifdef NBG_SPROBE
+extern "C" int nbg_debug_ringdbg(unsigned int* out, uint64_t n) {
+  if (n > 1024 * 20) n = 1024 * 20;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_ringdbg), n * 4) == hipSuccess ? 0 : NBG_EIO;
 }
 #endif
 #ifdef NBG_CPROBE

@@ -1,0 +1,132 @@
+// The persistent RX ring (nbg_ring_*) against one launch per batch, fed from C++ (no Python in the
+// producer loop, so the producer stays ahead of the kernel): C2 batches of 1M 64-B slots, 8 rotating
+// inputs and outputs, 65 backends / 65537 slots, read only ("ro") or in place ("ip").
+//   launch: K x nbg_maglev_classify_device_ex (no grouping) on one stream, HIP events around all K
+//   ring:   the producer posts whenever a slot is free and stamps every change of the completed
+//           count; the steady-state time per batch is the slope of completions over the middle
+//           three quarters of the run (the ramp and the drain excluded), the wall figure includes both
+// Prints one JSON line.
+// Build: hipcc -O2 -std=c++17 -o tools/ring_bench tools/ring_bench.cpp -Lnetbricks_amd -lnbgpu \
+//          -Wl,-rpath,'$ORIGIN/../netbricks_amd'
+// Usage: ring_bench [ro|ip] [batches] [packets]
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../include/nbgpu.h"
+
+#define CK(x)                                                                            \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) {                                                              \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));     \
+      std::exit(1);                                                                      \
+    }                                                                                    \
+  } while (0)
+#define NB(x)                                                                            \
+  do {                                                                                   \
+    int r_ = (x);                                                                        \
+    if (r_ != 0) {                                                                       \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, nbg_last_error());  \
+      std::exit(1);                                                                      \
+    }                                                                                    \
+  } while (0)
+
+using Clock = std::chrono::steady_clock;
+
+int main(int argc, char** argv) {
+  const bool inplace = argc > 1 && std::strcmp(argv[1], "ip") == 0;
+  const int K = argc > 2 ? std::atoi(argv[2]) : 512;
+  const uint64_t n = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : (1u << 20);
+  std::vector<std::string> names;
+  for (int i = 0; i < 65; ++i) names.push_back("backend-" + std::to_string(i));
+  std::vector<const char*> np;
+  std::vector<uint32_t> nl;
+  for (auto& s : names) {
+    np.push_back(s.data());
+    nl.push_back(static_cast<uint32_t>(s.size()));
+  }
+  nbg_maglev* h = nullptr;
+  NB(nbg_maglev_create(np.data(), nl.data(), 65, 65537, 0, &h));
+  constexpr int B = 8;
+  std::vector<uint8_t*> pk(B);
+  std::vector<uint16_t*> be(B);
+  {
+    std::vector<uint32_t> off(n);
+    std::vector<uint16_t> len(n);
+    const uint64_t bytes = nbg_trace_layout(n, 0, 900, off.data(), len.data());
+    std::vector<uint8_t> buf(bytes);
+    for (int i = 0; i < B; ++i) {
+      NB(nbg_trace_fill(buf.data(), off.data(), len.data(), n, 900 + i, 65536, 0));
+      CK(hipMalloc(&pk[i], bytes));
+      CK(hipMalloc(&be[i], n * 2));
+      CK(hipMemcpy(pk[i], buf.data(), bytes, hipMemcpyHostToDevice));
+    }
+  }
+  hipStream_t s;
+  CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const uint32_t flags = inplace ? NBG_SWAP_MACS : 0u;
+  // one launch per batch
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 16; ++i)
+    NB(nbg_maglev_classify_device_ex(h, pk[i % B], nullptr, nullptr, 64, 60, n, flags, be[i % B], nullptr, nullptr,
+                                     nullptr, s));
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < K; ++i)
+    NB(nbg_maglev_classify_device_ex(h, pk[i % B], nullptr, nullptr, 64, 60, n, flags, be[i % B], nullptr, nullptr,
+                                     nullptr, s));
+  CK(hipEventRecord(e1, s));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double launch_us = ms * 1e3 / K;
+  // the ring
+  nbg_ring* r = nullptr;
+  NB(nbg_ring_start(h, 64, 60, flags, 2000, s, &r));
+  uint64_t t = 0;
+  for (int i = 0; i < 16; ++i) NB(nbg_ring_post(r, pk[i % B], n, be[i % B], &t));
+  NB(nbg_ring_wait(r, t, 10000));
+  const uint64_t base = t + 1;
+  std::vector<std::pair<double, uint64_t>> stamps;
+  stamps.reserve(K + 1);
+  uint64_t posted = 0, done = 0;
+  const auto t0 = Clock::now();
+  while (done < static_cast<uint64_t>(K)) {
+    while (posted < static_cast<uint64_t>(K) && posted - done < NBG_RING_SLOTS) {
+      NB(nbg_ring_post(r, pk[posted % B], n, be[posted % B], &t));
+      ++posted;
+    }
+    uint64_t c = 0;
+    NB(nbg_ring_poll(r, &c));
+    c -= base;
+    if (c != done) {
+      stamps.emplace_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count(), c);
+      done = c;
+    }
+  }
+  const double wall = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+  NB(nbg_ring_stop(r));
+  const uint64_t lo = K / 8, hi = K - K / 8;
+  size_t i0 = 0, i1 = 0;
+  while (i0 < stamps.size() && stamps[i0].second < lo) ++i0;
+  while (i1 < stamps.size() && stamps[i1].second < hi) ++i1;
+  const double slope = (stamps[i1].first - stamps[i0].first) / static_cast<double>(stamps[i1].second - stamps[i0].second);
+  std::printf("{\"variant\": \"%s\", \"n_pkts\": %llu, \"batches\": %d, \"launch_us\": %.2f, \"ring_us_per_batch\": %.2f, "
+              "\"ring_wall_us_per_batch\": %.2f, \"ring_gpps\": %.1f, \"launch_gpps\": %.1f}\n",
+              inplace ? "in_place" : "read_only", static_cast<unsigned long long>(n), K, launch_us, slope, wall / K,
+              n / slope / 1e3, n / launch_us / 1e3);
+  nbg_maglev_destroy(h);
+  for (int i = 0; i < B; ++i) {
+    CK(hipFree(pk[i]));
+    CK(hipFree(be[i]));
+  }
+  return 0;
+}

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=256)
     ap.add_argument("--timeline", action="store_true")
+    ap.add_argument("--variants", default="read_only,in_place")
     args = ap.parse_args()
     import torch
 
@@ -40,6 +41,8 @@ def main():
     st = torch.cuda.Stream(dev)
     res = {"n_pkts": n, "batches": K}
     for variant, swap in (("read_only", False), ("in_place", True)):
+        if variant not in args.variants.split(","):
+            continue
         # one launch per batch (the same kernel family), events per launch
         flags = 0x1 if swap else 0
         kt = KernelTimer(K)
@@ -60,15 +63,23 @@ def main():
         for i in range(16):  # warm: the kernel is resident and polling
             ring.post(bufs[i % 8], n, outs[i % 8])
         ring.wait(15)
+        # the feed loop on bare ctypes with prebuilt arguments (Ring.post's checks cost ~5 us a call,
+        # about half a batch): the producer must stay ahead of the kernel
+        post, poll, rr = lib.nbg_ring_post, lib.nbg_ring_poll, ring._r
+        pk = [C.c_void_p(bufs[i].data_ptr()) for i in range(8)]
+        ob = [C.c_void_p(outs[i].data_ptr()) for i in range(8)]
+        tk, cc = C.c_uint64(), C.c_uint64()
         base = 16
         stamps = []
         posted, done = 0, 0
+        slots = nb._lib.NBG_RING_SLOTS
         t0 = time.perf_counter()
         while done < K:
-            while posted < K and posted - done < nb._lib.NBG_RING_SLOTS:
-                ring.post(bufs[posted % 8], n, outs[posted % 8])
+            while posted < K and posted - done < slots:
+                assert post(rr, pk[posted % 8], n, ob[posted % 8], C.byref(tk)) == 0
                 posted += 1
-            c = ring.poll() - base
+            assert poll(rr, C.byref(cc)) == 0
+            c = cc.value - base
             if c != done:
                 stamps.append((time.perf_counter(), c))
                 done = c
@@ -89,8 +100,9 @@ def main():
         fn.argtypes = [C.c_void_p, C.c_uint64]
         probe = int(os.environ.get("NBG_RING_PROBE_STEP", "24"))
         ring = mg.ring(stream=st)
-        for i in range(probe // 8 + 8):  # enough 1M batches to cover the probed steps
-            ring.post(bufs[i % 8], n, outs[i % 8])
+        tk = C.c_uint64()
+        for i in range(probe // 8 + 8):  # enough 1M batches to cover the probed steps, posted ahead
+            assert lib.nbg_ring_post(ring._r, bufs[i % 8].data_ptr(), n, outs[i % 8].data_ptr(), C.byref(tk)) == 0
         ring.wait(probe // 8 + 7)
         ring.stop()
         raw = np.zeros(4096 * 20, dtype=np.uint64)
@@ -98,6 +110,16 @@ def main():
         t = raw.reshape(4096, 20)[:256 * 8].astype(np.float64)
         us = (t[:, 2:18] - t[:, 2:18].min()) / 100.0
         iv = np.diff(us, axis=1)  # per wave: step k -> k+1
+        dbg = np.zeros(1024 * 20, dtype=np.uint32)
+        fd = lib.nbg_debug_ringdbg
+        fd.restype = C.c_int
+        fd.argtypes = [C.c_void_p, C.c_uint64]
+        assert fd(dbg.ctypes.data, dbg.size) == 0
+        d = dbg.reshape(1024, 20)[:256]
+        res["ring_debug"] = {"prefetches": int(d[:, 0].sum()), "taken": int(d[:, 1].sum()),
+                             "empty_prefetches": int(d[:, 2].sum()), "idle_entries": int(d[:, 3].sum()),
+                             "block0_failed_stage": [hex(int(x)) for x in dbg[4:20]]}
+        print(json.dumps({"ring_debug": res["ring_debug"]}), flush=True)
         res["timeline"] = {"probe_step": probe,
                            "median_step_interval_us": [round(float(x), 3) for x in np.median(iv, axis=0)],
                            "p90_step_interval_us": [round(float(x), 3) for x in np.percentile(iv, 90, axis=0)]}
