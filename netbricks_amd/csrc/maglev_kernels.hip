@@ -1274,22 +1274,22 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 // the LUT is staged once per ring and the tile pipeline runs across batch boundaries without a
 // ramp.
 //
-//   Descriptors.  Wave 0 of every block keeps up to kRingCache batch descriptors in LDS.  It
-//   prefetches the next kRingFetch ring slots by LDS-DMA (system scope: the slots live in host
-//   memory) ahead of its next tile, so the fetch is covered by that tile's counted wait and never
-//   drains the ring; a slot is taken once its seq and check match (a read that overlaps the host
-//   rewriting the slot fails the check and is retried).  The count of known batches is published
-//   through a step-parity LDS word behind the unit barrier, so every wave sees the same count.
-//   When the block has no tile to classify (the next unit is in no known batch) it drains and
-//   wave 0 polls the ring slot (and the stop word) with s_sleep between polls: the idle path.
+//   Descriptors.  The control wave (the ninth) of every block keeps up to kRingCache batch
+//   descriptors in LDS.  It prefetches the next kRingFetch slots of its replica of the device ring
+//   (uncached HBM, filled from the host's ring by the relay block, ring_relay) by LDS-DMA; a slot is taken
+//   once its seq and check match (a read that overlaps the relay rewriting the slot fails the check
+//   and is retried).  The count of known batches is published through a step-parity LDS word behind
+//   the unit barrier, so every wave sees the same count.  When the block has no tile to classify
+//   (the next unit is in no known batch) it drains and the control wave polls the slot (and the
+//   device stop word) with s_sleep between polls: the idle path.  No classify CU reads host memory.
 //   Exit: stop set and nothing posted, or idle_ticks without a new batch (the exit condition every
 //   wave reaches when the host goes away).
 //
 //   Completion.  Outputs are stored write-through (sc1: backend[] packed 16 B per lane, the in-place
 //   windows 16 B per lane), so a store that retired is in HBM.  In-order vmcnt: once every wave has
-//   waited for tile k (the unit barrier of step k), the stores of steps <= k - 3 retired.  Wave 0
-//   then publishes, per block, the count of batches all of whose units of this block are complete
-//   (one system-scope store to pinned memory when the count changes); the host takes the minimum.
+//   waited for tile k (the unit barrier of step k), the stores of steps <= k - 3 retired.  The
+//   control wave then publishes, per block, the count of batches all of whose units of this block
+//   are complete (to uncached HBM, when the count changes); the relay reports the minimum to the host.
 #ifndef NBG_RING_ABL  // measurement builds (tools/build_ab.sh): 1 plain backend stores, 2 none
 #define NBG_RING_ABL 0
 #endif
@@ -1372,6 +1372,11 @@ __device__ __forceinline__ bool ring_take(const uint32_t* d, uint32_t* cache, ui
   return true;
 }
 
+// Batch j's descriptor in this block's replica of the ring.
+__device__ __forceinline__ const RingDesc* ring_slot(const RingArgs& r, uint32_t j) {
+  return r.desc + (blockIdx.x & (r.reps - 1u)) * r.slots + (j & (r.slots - 1u));
+}
+
 // Wave 0, idle: read ring slots (and the stop word) until a new batch is taken; true = exit (stop
 // with nothing posted, or idle_ticks without a batch: then the error word is set).
 __device__ __forceinline__ bool ring_poll(const RingArgs& r, uint32_t* stage, uint32_t* cache, uint32_t& known_w,
@@ -1380,15 +1385,15 @@ __device__ __forceinline__ bool ring_poll(const RingArgs& r, uint32_t* stage, ui
   const uint32_t known0 = known_w;
   for (uint32_t nap = 1;; nap = min(2u * nap, 16u)) {
     for (;;) {  // every consecutive batch that is posted (and fits)
-      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(ring_slot(r, known_w));
       if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_wave_barrier();
       if (!ring_take(stage, cache, known_w, base, lane)) break;
     }
     if (known_w != known0) return false;
-    if (rfl(__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+    if (rfl(__hip_atomic_load(r.dstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
       // a batch posted before the stop is in its slot by now: look once more
-      const uint32_t* slot = reinterpret_cast<const uint32_t*>(r.desc + (known_w & (r.slots - 1u)));
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(ring_slot(r, known_w));
       if (lane < 16) stage[lane] = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_wave_barrier();
       return !ring_take(stage, cache, known_w, base, lane);
@@ -1397,8 +1402,112 @@ __device__ __forceinline__ bool ring_poll(const RingArgs& r, uint32_t* stage, ui
       if (lane == 0) __hip_atomic_store(&r.ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return true;
     }
-    // back off to 16 x 512 clocks (~3.5 us) between polls: the idle grid reads a few GB/s over PCIe
+    // back off to 16 x 512 clocks (~3.5 us) between polls of the (uncached) device ring
     for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// The ring's relay: wave 0 of the classify kernel's last block (the other waves of that block exit),
+// so its PCIe reads of the host ring hold no classify CU.  (A separate one-wave kernel measured no
+// good: blocks go to XCDs round-robin and never move, so the XCD that hosted it had one classify
+// block too many for its CUs, and that block never became resident.)
+// Loop: copy every newly posted host slot (seq and check match) into each replica of the uncached
+// device ring; report the minimum of the blocks' completion counts to the host when it moves; on
+// the host's stop, relay what was posted before it, then raise the device stop word and exit once
+// every relayed batch is complete; on idle_ticks without a post or a completion, raise the device
+// stop word and the host error word and exit (the exit every path reaches when the host goes away).
+__device__ __noinline__ void ring_relay(const RingArgs& r, uint32_t lane) {
+  uint32_t known = 0, done = 0, nap = 1;
+  bool stopping = false, stopped = false;
+  uint64_t t_act = wall_clock64();
+  for (;;) {
+    bool moved = false;
+    for (;;) {  // every consecutive posted slot
+      const uint32_t* hs = reinterpret_cast<const uint32_t*>(r.hdesc + (known & (r.slots - 1u)));
+      const uint32_t x = lane < 16u ? __hip_atomic_load(hs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+      uint32_t w[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w[i] = __shfl(x, i);
+      const uint64_t pk = w[0] | static_cast<uint64_t>(w[1]) << 32, be = w[2] | static_cast<uint64_t>(w[3]) << 32;
+      const uint64_t lo = w[4] | static_cast<uint64_t>(w[5]) << 32, hi = w[6] | static_cast<uint64_t>(w[7]) << 32;
+      const uint64_t ck = w[14] | static_cast<uint64_t>(w[15]) << 32;
+      if (!(w[9] == known + 1u && ck == ring_check(pk, be, lo, hi, w[8], w[9]))) break;
+      for (uint32_t q = lane >> 4; q < r.reps; q += 4u) {
+        uint32_t* d = reinterpret_cast<uint32_t*>(r.desc + q * r.slots + (known & (r.slots - 1u)));
+        __hip_atomic_store(d + (lane & 15u), __shfl(x, static_cast<int>(lane & 15u)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      ++known;
+      moved = true;
+    }
+    // completion: the slowest block
+    uint32_t lag = 0;
+    for (uint32_t b = lane; b < r.grid; b += 64u)
+      lag = max(lag, known - __hip_atomic_load(r.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lag = max(lag, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lag), o)));
+    const uint32_t c = known - rfl(lag);
+#ifdef NBG_RING_DEBUG  // diagnostic builds: the relay's state in the host ctl line's pad words
+    if (lane == 0) {
+      volatile uint32_t* dbg = r.ctl->pad;
+      dbg[0] = known;
+      dbg[1] = dbg[1] + 1u;
+      dbg[2] = rfl(lag);
+      dbg[3] = __hip_atomic_load(r.prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      dbg[4] = __hip_atomic_load(r.dstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    {  // blocks behind, the first of them
+      uint32_t behind = 0, first = 0xffffffffu;
+      for (uint32_t b = lane; b < r.grid; b += 64u) {
+        const bool lt = __hip_atomic_load(r.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != known;
+        behind += lt ? 1u : 0u;
+        first = lt ? min(first, b) : first;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        behind += static_cast<uint32_t>(__shfl_xor(static_cast<int>(behind), o));
+        first = min(first, static_cast<uint32_t>(__shfl_xor(static_cast<int>(first), o)));
+      }
+      if (lane == 0) {
+        r.ctl->pad[5] = behind;
+        r.ctl->pad[6] = first;
+        r.ctl->pad[7] = r.grid;
+      }
+    }
+#endif
+    if (c != done) {
+      done = c;
+      if (lane == 0) __hip_atomic_store(&r.ctl->completed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      moved = true;
+    }
+    if (moved) {
+      t_act = wall_clock64();
+      nap = 1;
+      continue;
+    }
+    if (stopped) {
+      if (done == known) break;  // every relayed batch is complete; the blocks exit on the stop word
+    } else if (rfl(__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))) {
+      if (stopping) {
+        // the slots were read once more after the stop was seen: everything posted before it is
+        // relayed; the descriptors are in memory before the stop word
+        wait_vm<0>();
+        if (lane == 0) __hip_atomic_store(r.dstop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        stopped = true;
+        continue;
+      }
+      stopping = true;
+      continue;
+    }
+    if (static_cast<uint64_t>(wall_clock64()) - t_act > r.idle_ticks) {
+      if (lane == 0) {
+        __hip_atomic_store(r.dstop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (done != known || !stopped) __hip_atomic_store(&r.ctl->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      break;
+    }
+    for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(4);
+    nap = min(2u * nap, 8u);
   }
 }
 
@@ -1422,7 +1531,11 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
   uint16_t* rep = reinterpret_cast<uint16_t*>(known_l + 4) + (ctl ? 0u : wave) * 64u;  // a tile wave's 64 backends
   uint32_t* warm_l = known_l + 4 + kStreamW * 32u;  // [16] landing words of the control wave's page touches
   const uint32_t ring_lds = rfl(lds_addr(ring)), lut_lds = rfl(lds_addr(lut)), stage_lds = rfl(lds_addr(stage));
-  const uint32_t G = gridDim.x, b = blockIdx.x;
+  if (blockIdx.x == r.grid) {  // the relay block
+    if (wave == 0) ring_relay(r, lane);
+    return;
+  }
+  const uint32_t G = r.grid, b = blockIdx.x;
   if (!ctl) { SPROBE(0) }
   const uint32_t pieces_lut = ctl ? 0u : a.lut_lds_bytes >> 10;
   for (uint32_t q = wave; q < pieces_lut; q += kStreamW)
@@ -1543,8 +1656,7 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pf_base = known_w;
         if (lane < 16u * kRingFetch)
-          glds4_sys(reinterpret_cast<const uint32_t*>(r.desc + ((known_w + lane / 16u) & (r.slots - 1u))) + (lane & 15u),
-                    stage_lds);
+          glds4_sys(reinterpret_cast<const uint32_t*>(ring_slot(r, known_w + lane / 16u)) + (lane & 15u), stage_lds);
         pf = true;
         last_pf = k;
         RINGDBG(0, 1)

@@ -1100,35 +1100,50 @@ int nbg_maglev_check(nbg_maglev* h) {
 
 struct nbg_ring {
   nbg_maglev* h = nullptr;
-  hipStream_t stream = nullptr;
-  uint8_t* host = nullptr;  // pinned, mapped: RingCtl | RingDesc[slots] | prog[grid]
+  hipStream_t stream = nullptr;        // the ring kernel's (the caller's)
+  uint8_t* host = nullptr;             // pinned, mapped: RingCtl | RingDesc[slots]
+  uint8_t* dev = nullptr;              // uncached HBM: stop word (own line) | prog[grid] | RingDesc[reps][slots]
   volatile RingCtl* ctl = nullptr;
   RingDesc* desc = nullptr;
-  volatile uint32_t* prog = nullptr;
   uint32_t slots = NBG_RING_SLOTS;
+  uint32_t reps = kRingReps;
   int grid = 0;
   uint32_t idle_ms = 0;
   uint64_t posted = 0, units = 0, completed = 0;
   bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
+  // hipStreamQuery is not cheap on a stream with a resident kernel, so the kernel's end is only
+  // checked after the completed count has not moved for kStallCheck
+  std::chrono::steady_clock::time_point moved{};
 };
 
 namespace {
 
 using Clock = std::chrono::steady_clock;
 
-// Completed batches: every block reports how many batches are complete for it; the ring's count is
-// the minimum (as a lag behind `posted`, so that 32-bit counts may wrap).
+// Completed batches: the relay reports the minimum over the blocks' counts (mod 2^32, so taken as
+// a lag behind `posted`).
 void ring_refresh(nbg_ring* r) {
-  const uint32_t p32 = static_cast<uint32_t>(r->posted);
-  uint32_t lag = 0;
-  for (int b = 0; b < r->grid; ++b) lag = std::max(lag, p32 - r->prog[b]);
-  r->completed = r->posted - lag;
+  const uint32_t lag = static_cast<uint32_t>(r->posted) - r->ctl->completed;
+  const uint64_t c = lag <= r->posted - r->completed ? r->posted - lag : r->completed;
+  if (c != r->completed) r->moved = Clock::now();
+  r->completed = c;
 }
+
+constexpr auto kStallCheck = std::chrono::milliseconds(2);
 
 // The kernel has ended?  (hipStreamQuery: the ring kernel is the last work on its stream.)
 bool ring_ended(nbg_ring* r) {
   if (!r->ended && hipStreamQuery(r->stream) != hipErrorNotReady) r->ended = true;
   return r->ended;
+}
+
+// The same, but the stream is only queried once the completed count has stalled for kStallCheck
+// with batches outstanding (the idle kernel's own exit, stop, or a fault); the error word is free.
+bool ring_gone(nbg_ring* r) {
+  if (r->ended || r->ctl->error) return true;
+  if (r->completed >= r->posted) return false;
+  if (Clock::now() - r->moved < kStallCheck) return false;
+  return ring_ended(r);
 }
 
 int ring_state_error(nbg_ring* r) {
@@ -1138,6 +1153,12 @@ int ring_state_error(nbg_ring* r) {
 
 void ring_pause(Clock::time_point t0) {
   if (Clock::now() - t0 > std::chrono::microseconds(200)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
+void ring_free(nbg_ring* r) {
+  if (r->host) (void)hipHostFree(r->host);
+  if (r->dev) (void)hipFree(r->dev);
+  delete r;
 }
 
 }  // namespace
@@ -1154,6 +1175,7 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
     return set_error(NBG_EINVAL, "ring_start: fixed slots with stride %% 16 == 0, 64 <= stride < 2^24, fixed_len >= 48");
   if (flags & ~NBG_SWAP_MACS) return set_error(NBG_EINVAL, "ring_start: flags other than NBG_SWAP_MACS");
   if (h->pending) return set_error(NBG_EINVAL, "ring_start: a deferred or lagged group is pending");
+  if (h->cus < 2) return set_error(NBG_EINVAL, "ring_start: needs a CU for the relay beside the classify blocks");
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = order_after_last(h, s);  // the ring runs after the handle's earlier work
@@ -1162,23 +1184,37 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
   r->h = h;
   r->stream = s;
-  r->grid = h->cus;
+  r->grid = h->cus - 1;  // classify blocks; one more block, on a CU of its own, is the relay
   r->idle_ms = idle_ms ? idle_ms : 2000u;
-  const size_t bytes = sizeof(RingCtl) + r->slots * sizeof(RingDesc) + static_cast<size_t>(r->grid) * 4u;
-  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), bytes, hipHostMallocMapped | hipHostMallocCoherent) !=
-      hipSuccess) {
-    delete r;
-    return set_error(NBG_ENOMEM, "ring_start: pinned ring of %zu B", bytes);
+  r->moved = Clock::now();
+  if (const char* e = std::getenv("NBG_RING_REPS")) {  // measurement: replicas, a power of two <= 256
+    const uint32_t v = static_cast<uint32_t>(std::atoi(e));
+    if (v && v <= 256 && (v & (v - 1)) == 0) r->reps = v;
   }
-  std::memset(r->host, 0, bytes);
+  const size_t hbytes = sizeof(RingCtl) + static_cast<size_t>(r->slots) * sizeof(RingDesc);
+  const size_t prog_off = 64, desc_off = prog_off + ((static_cast<size_t>(r->grid) * 4u + 63u) & ~size_t{63});
+  const size_t dbytes = desc_off + static_cast<size_t>(r->reps) * r->slots * sizeof(RingDesc);
+  uint8_t* hdev = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), hbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess) {
+    ring_free(r);
+    return set_error(NBG_ENOMEM, "ring_start: pinned ring of %zu B", hbytes);
+  }
+  std::memset(r->host, 0, hbytes);
   r->ctl = reinterpret_cast<RingCtl*>(r->host);
   r->desc = reinterpret_cast<RingDesc*>(r->host + sizeof(RingCtl));
-  r->prog = reinterpret_cast<uint32_t*>(r->host + sizeof(RingCtl) + r->slots * sizeof(RingDesc));
-  uint8_t* dev = nullptr;
-  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&dev), r->host, 0) != hipSuccess) {
-    (void)hipHostFree(r->host);
-    delete r;
-    return set_error(NBG_EIO, "ring_start: device address of the pinned ring");
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&r->dev), dbytes, hipDeviceMallocUncached) != hipSuccess) {
+    ring_free(r);
+    return set_error(NBG_ENOMEM, "ring_start: uncached device ring of %zu B", dbytes);
+  }
+  {
+    SetupStream st;
+    (void)st.zero(r->dev, dbytes);
+    if (st.finish() != hipSuccess) {
+      ring_free(r);
+      return set_error(NBG_EIO, "ring_start: zeroing the device ring");
+    }
   }
   ClassifyArgs a{};
   a.stride = stride;
@@ -1194,16 +1230,19 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
   a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
   RingArgs ra{};
-  ra.ctl = reinterpret_cast<RingCtl*>(dev);
-  ra.desc = reinterpret_cast<const RingDesc*>(dev + sizeof(RingCtl));
-  ra.prog = reinterpret_cast<uint32_t*>(dev + sizeof(RingCtl) + r->slots * sizeof(RingDesc));
+  ra.ctl = reinterpret_cast<RingCtl*>(hdev);
+  ra.hdesc = reinterpret_cast<const RingDesc*>(hdev + sizeof(RingCtl));
+  ra.dstop = reinterpret_cast<uint32_t*>(r->dev);
+  ra.prog = reinterpret_cast<uint32_t*>(r->dev + prog_off);
+  ra.desc = reinterpret_cast<RingDesc*>(r->dev + desc_off);
   ra.slots = r->slots;
+  ra.reps = r->reps;
+  ra.grid = static_cast<uint32_t>(r->grid);
   ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
   const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
   ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
-  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid, s))) {
-    (void)hipHostFree(r->host);
-    delete r;
+  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, s))) {
+    ring_free(r);
     return rc;
   }
   h->ring = r;
@@ -1224,13 +1263,14 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
   while (r->posted - r->completed >= r->slots) {
     ring_refresh(r);
     if (r->posted - r->completed < r->slots) break;
-    if (r->ctl->error || ring_ended(r)) return ring_state_error(r);
+    if (ring_gone(r)) return ring_state_error(r);
     if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 1000u))
       return set_error(NBG_ETIMEDOUT, "ring_post: no slot freed in %u ms", r->idle_ms + 1000u);
     ring_pause(t0);
   }
-  if (r->ctl->error || ring_ended(r)) return ring_state_error(r);
+  if (ring_gone(r)) return ring_state_error(r);
   const uint64_t j = r->posted;
+  if (r->completed == j) r->moved = Clock::now();  // the stall clock starts with the first outstanding batch
   const uint64_t units = ((n_pkts + 63) / 64 + 7) / 8;  // 512-packet units of 8 waves' tiles
   RingDesc d{};
   d.pkts = reinterpret_cast<uintptr_t>(d_pkts);
@@ -1240,7 +1280,7 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
   d.n_pkts = static_cast<uint32_t>(n_pkts);
   d.seq = static_cast<uint32_t>(j + 1);
   d.check = ring_check(d.pkts, d.backend, d.ulo, d.uhi, d.n_pkts, d.seq);
-  // one 64-B line: a device read that overlaps this write fails the check and is retried
+  // one 64-B line: a relay read that overlaps this write fails the check and is retried
   volatile uint64_t* dst = reinterpret_cast<volatile uint64_t*>(r->desc + (j & (r->slots - 1)));
   const uint64_t* src = reinterpret_cast<const uint64_t*>(&d);
   for (int i = 0; i < 8; ++i) dst[i] = src[i];
@@ -1251,11 +1291,19 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
   return NBG_OK;
 }
 
+// Diagnostics (not in include/nbgpu.h): the host control line's 16 words.
+int nbg_debug_ring_ctl(nbg_ring* r, uint32_t* out) {
+  if (!r || !out) return NBG_EINVAL;
+  const volatile uint32_t* w = reinterpret_cast<const volatile uint32_t*>(r->ctl);
+  for (int i = 0; i < 16; ++i) out[i] = w[i];
+  return NBG_OK;
+}
+
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
   if (!r || !completed) return set_error(NBG_EINVAL, "ring_poll: null argument");
   ring_refresh(r);
   *completed = r->completed;
-  if (r->completed < r->posted && (r->ctl->error || ring_ended(r))) return ring_state_error(r);
+  if (r->completed < r->posted && ring_gone(r)) return ring_state_error(r);
   return NBG_OK;
 }
 
@@ -1266,7 +1314,7 @@ int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms) {
   for (;;) {
     ring_refresh(r);
     if (r->completed > ticket) return NBG_OK;
-    if (r->ctl->error || ring_ended(r)) {
+    if (ring_gone(r)) {
       ring_refresh(r);  // progress stored before the kernel ended
       if (r->completed > ticket) return NBG_OK;
       return ring_state_error(r);
@@ -1296,9 +1344,8 @@ int nbg_ring_stop(nbg_ring* r) {
   ring_refresh(r);
   if (e != hipSuccess) rc = set_error(NBG_EIO, "ring_stop: %s", hipGetErrorString(e));
   else if (r->completed < r->posted) rc = ring_state_error(r);
-  (void)hipHostFree(r->host);
   r->h->ring = nullptr;
-  delete r;
+  ring_free(r);
   return rc;
 }
 

@@ -109,8 +109,14 @@ struct LagGroup {
   uint32_t hist16;            // rows of two 16-bit bins per word
 };
 
-// Persistent RX-ring classify (nbg_ring_*).  One batch per ring slot, in pinned host memory: written
-// by nbg_ring_post, read by the kernel over PCIe.  64 B, one line.
+// Persistent RX-ring classify (nbg_ring_*).  One batch per ring slot (64 B, one line), written by
+// nbg_ring_post into pinned host memory.  No classify CU ever touches host memory: a one-wave relay
+// kernel on a CU of its own (ring_relay_kernel) copies each posted descriptor into a device ring in
+// uncached HBM (`reps` replicas, block b reads replica b % reps), forwards the host's stop, and
+// reports the minimum of the blocks' per-block completion counts (also uncached HBM) to the host.
+// Measured before the relay: with every classify block reading host memory, the per-batch time
+// varied from 12 to 190 us from run to run and box to box (a PCIe read in a CU's vector memory path
+// holds that CU's tile loads behind it).
 struct RingDesc {
   uint64_t pkts;
   uint64_t backend;
@@ -118,27 +124,33 @@ struct RingDesc {
   uint32_t n_pkts;
   uint32_t seq;       // batch index + 1 (mod 2^32)
   uint32_t pad[4];
-  uint64_t check;     // ring_check(): a read that overlaps the host rewriting the slot fails it
+  uint64_t check;     // ring_check(): a read that overlaps a rewrite of the slot fails it
 };
 static_assert(sizeof(RingDesc) == 64, "one descriptor per 64-B line");
 struct RingCtl {      // pinned host memory, the first line
-  uint32_t stop;      // host: exit once nothing more is posted
-  uint32_t error;     // device: 1 = idle timeout (the kernel exited by itself)
-  uint32_t pad[14];
+  uint32_t stop;      // host: exit once everything posted is classified
+  uint32_t error;     // device: 1 = idle timeout (the kernels exited by themselves)
+  uint32_t completed; // relay: batches complete on every block (mod 2^32)
+  uint32_t pad[13];
 };
 struct RingArgs {
-  RingCtl* ctl;
-  const RingDesc* desc;  // [slots]
-  uint32_t* prog;        // [grid] per block: batches all of whose units of this block are complete
-  uint32_t slots;        // power of two
-  uint32_t probe_step;   // NBG_SPROBE builds: the first of the 16 unit steps recorded
-  uint64_t idle_ticks;   // exit after this long (100 MHz wall clock) without a new batch
+  RingCtl* ctl;           // host
+  const RingDesc* hdesc;  // host [slots]: read by the relay only
+  RingDesc* desc;         // device, uncached [reps][slots]: the classify blocks' descriptors
+  uint32_t* dstop;        // device, uncached: relay -> blocks, every posted batch is relayed and stop was asked
+  uint32_t* prog;         // device, uncached [grid]: per block, batches all of whose units of it are complete
+  uint32_t slots;         // power of two
+  uint32_t reps;          // power of two: replicas of the device ring
+  uint32_t grid;          // classify blocks (block `grid` is the relay)
+  uint32_t probe_step;    // NBG_SPROBE builds: the first of the 16 unit steps recorded
+  uint64_t idle_ticks;    // exit after this long (100 MHz wall clock) without a new batch
 };
 #ifdef __HIPCC__
 #define NBG_HD __host__ __device__
 #else
 #define NBG_HD
 #endif
+constexpr uint32_t kRingReps = 8;  // device-ring replicas, one per XCD (NBG_RING_REPS overrides: measurement)
 NBG_HD inline uint64_t ring_check(uint64_t pkts, uint64_t backend, uint64_t ulo, uint64_t uhi, uint32_t n_pkts,
                                   uint32_t seq) {
   uint64_t h = 0x6a09e667f3bcc909ull ^ (static_cast<uint64_t>(seq) << 32 | n_pkts);
