@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import csv
+import ctypes as C
 import hashlib
 import json
 import os
@@ -628,6 +629,56 @@ def run_rank(args) -> None:
                         "kernel and one group launch (nbg_maglev_classify_device_multi); every batch keeps its own "
                         "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
 
+    # ---- the persistent RX ring (nbg_ring_*): one resident classify kernel fed batch descriptors
+    def ring_pass(variant, batches):
+        """Per-batch time of the ring in steady state: the producer posts the rotating batches whenever
+        a slot is free (bare ctypes, prebuilt arguments) and stamps every change of the completed
+        count; the time per batch is the slope of completions over the middle three quarters of the
+        run (no launch, LUT staging or ramp per batch; HIP events cannot bracket a batch inside one
+        resident kernel).  No grouping on the ring: backend[] (and the in-place swap) only."""
+        swap = variant == "in_place"
+        ring = mgs[0].ring(swap_macs=swap, stream=streams[0])
+        post, poll, rr = clib.nbg_ring_post, clib.nbg_ring_poll, ring._r
+        bes = [C.c_void_p(o[par]["backend"].data_ptr()) for o in outs for par in (0, 1)]
+        pks = [C.c_void_p(p) for p in pk]
+        tk, cc = C.c_uint64(), C.c_uint64()
+        slots = nb._lib.NBG_RING_SLOTS
+        try:
+            for i in range(16):  # warm: the kernel is resident and every rotating batch touched
+                if post(rr, pks[i % N_BATCHES], BATCH, bes[i % len(bes)], C.byref(tk)):
+                    raise RuntimeError(f"nbg_ring_post: {nb._lib.last_error()}")
+            ring.wait(15)
+            base, stamps, posted, done = 16, [], 0, 0
+            t0 = time.perf_counter()
+            while done < batches:
+                while posted < batches and posted - done < slots:
+                    if post(rr, pks[posted % N_BATCHES], BATCH, bes[posted % len(bes)], C.byref(tk)):
+                        raise RuntimeError(f"nbg_ring_post: {nb._lib.last_error()}")
+                    posted += 1
+                if poll(rr, C.byref(cc)):
+                    raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
+                c = cc.value - base
+                if c != done:
+                    stamps.append((time.perf_counter(), c))
+                    done = c
+            wall = time.perf_counter() - t0
+        finally:
+            ring.stop()
+        ts = np.array([x[0] for x in stamps])
+        cs = np.array([x[1] for x in stamps])
+        i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
+        us = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]) * 1e6)
+        bpp = CLASSIFY_BYTES[variant]
+        ach = BATCH * bpp / us / 1e3
+        return {"value": round(BATCH / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
+                "wall_us_per_batch": round(wall / batches * 1e6, 2), "batches": batches, "bytes_per_pkt": bpp,
+                "pkts_per_batch": BATCH, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "kernel": f"classify_ring_kernel<true, {1 if swap else 0}>",
+                "what": "persistent RX ring (nbg_ring_*): one resident classify kernel (LUT staged once) takes "
+                        "1M-packet batches as the producer posts them through a pinned descriptor ring, relayed "
+                        "into HBM by the kernel's last block; per-batch time from the completion slope; "
+                        "backend[] (+ in-place MAC swap) only, no grouping"}
+
     # ---- configs C3 / C5 (IMIX descriptors): handles, traces and one call per batch
     imix = {}
 
@@ -828,6 +879,9 @@ def run_rank(args) -> None:
                         "classified + grouped as one rank would (MAC swap in place), 64 distinct shards rotating "
                         "on the same streams; below the streaming kernel's 262,144-packet threshold, so the "
                         "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
+            if not args.no_ring:
+                for v in ("read_only", "in_place"):
+                    variants[f"ring_{v}"] = ring_pass(v, max(args.steps * BATCHES_PER_STEP, 256))
             if m_arrs:
                 calls = max(args.steps * BATCHES_PER_STEP // MULTI_K, 10)
                 for v in ("read_only", "in_place"):
@@ -899,7 +953,8 @@ def run_rank(args) -> None:
                 line["north_star"] = {"target_frac": 0.70, "frac": float(ro["frac"]), "met": bool(ro["frac"] >= 0.70),
                                       "variant": f"read_only_multi{MULTI_K}" if f"read_only_multi{MULTI_K}" in variants
                                       else "read_only",
-                                      "single_batch_frac": variants.get("read_only", {}).get("frac")}
+                                      "single_batch_frac": variants.get("read_only", {}).get("frac"),
+                                      "ring_single_batch_frac": variants.get("ring_read_only", {}).get("frac")}
         line["cpu_baseline"] = cpu
         if scatter is not None:
             line["scatter_inclusive"] = scatter
@@ -930,6 +985,7 @@ def parse_args(argv):
     ap.add_argument("--no-variants", action="store_true", help="skip the variant passes")
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-batch variants")
     ap.add_argument("--no-imix", action="store_true", help="skip configs C3 / C5")
+    ap.add_argument("--no-ring", action="store_true", help="skip the persistent-ring variants")
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")

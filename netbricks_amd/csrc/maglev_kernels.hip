@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 #define NBG_RING_ABL 0
 #endif
 #ifndef NBG_RING_WARM  // the control wave's page touches ahead of a batch (0: off, A/B builds)
-#define NBG_RING_WARM 1
+#define NBG_RING_WARM 0
 #endif
 constexpr uint32_t kRingCache = 4;  // batch descriptors in LDS (from the current unit's batch on)
 constexpr uint32_t kRingFetch = 2;  // ring slots per prefetch (one LDS-DMA dword load, 32 lanes)
@@ -1416,7 +1416,7 @@ __device__ __forceinline__ bool ring_poll(const RingArgs& r, uint32_t* stage, ui
 // the host's stop, relay what was posted before it, then raise the device stop word and exit once
 // every relayed batch is complete; on idle_ticks without a post or a completion, raise the device
 // stop word and the host error word and exit (the exit every path reaches when the host goes away).
-__device__ __noinline__ void ring_relay(const RingArgs& r, uint32_t lane) {
+__device__ __forceinline__ void ring_relay(const RingArgs& r, uint32_t lane) {
   uint32_t known = 0, done = 0, nap = 1;
   bool stopping = false, stopped = false;
   uint64_t t_act = wall_clock64();
@@ -1551,9 +1551,14 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
   uint32_t k = 0, iss = 0;                   // unit steps of this block classified / issued
   uint32_t seq = 0, sA = 0, sB = 0, sC = 0;  // VM operations issued; counts after tiles k, k+1, k+2
   // the control wave's descriptor state
-  uint32_t known_w = 0, pf_base = 0, last_pf = 0, pub = 0, warmed = 0xffffffffu;
+  uint32_t known_w = 0, pf_base = 0, last_pf = 0, pub = 0;
   bool pf = false;
+#if NBG_RING_WARM
+  uint32_t warmed = 0xffffffffu;
   const uint32_t warm_lds = rfl(lds_addr(warm_l));
+#else
+  (void)warm_l;
+#endif
   uint32_t hA = 0xffffffffu, hB = 0xffffffffu, hC = 0xffffffffu;  // batch of the unit of steps k - 1, k - 2, k - 3
   // a step's backends are stored one step late, behind the next tile issue: the wait for a tile then
   // covers the write-through stores of four steps back, not three, so their longer acks stay off the

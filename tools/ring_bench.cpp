@@ -8,7 +8,8 @@
 // Prints one JSON line.
 // Build: hipcc -O2 -std=c++17 -o tools/ring_bench tools/ring_bench.cpp -Lnetbricks_amd -lnbgpu \
 //          -Wl,-rpath,'$ORIGIN/../netbricks_amd'
-// Usage: ring_bench [ro|ip] [batches] [packets] [ahead]
+// Usage: ring_bench [ro|ip] [batches] [packets] [ahead|chunk]
+//   chunk: the producer refills 32 slots at a time (whenever 32 are free) instead of one per completion
 //   ahead: every batch is posted before the first completion is awaited (batches <= NBG_RING_SLOTS;
 //          the producer out of the loop), the time per batch from the completions as above
 // With an NBG_SPROBE build of libnbgpu.so the ring kernel's counters are printed too.
@@ -50,6 +51,7 @@ int main(int argc, char** argv) {
   const int K = argc > 2 ? std::atoi(argv[2]) : 512;
   const uint64_t n = argc > 3 ? std::strtoull(argv[3], nullptr, 10) : (1u << 20);
   const bool ahead = argc > 4 && std::strcmp(argv[4], "ahead") == 0;
+  const bool chunk = argc > 4 && std::strcmp(argv[4], "chunk") == 0;
   if (ahead && K > static_cast<int>(NBG_RING_SLOTS)) {
     std::fprintf(stderr, "ahead: at most %u batches\n", NBG_RING_SLOTS);
     return 2;
@@ -110,7 +112,8 @@ int main(int argc, char** argv) {
   uint64_t posted = 0, done = 0;
   const auto t0 = Clock::now();
   while (done < static_cast<uint64_t>(K)) {
-    while (posted < static_cast<uint64_t>(K) && (ahead || posted - done < NBG_RING_SLOTS)) {
+    const bool refill = !chunk || posted - done <= NBG_RING_SLOTS - 32;
+    while (refill && posted < static_cast<uint64_t>(K) && (ahead || posted - done < NBG_RING_SLOTS)) {
       NB(nbg_ring_post(r, pk[posted % B], n, be[posted % B], &t));
       ++posted;
     }
@@ -179,6 +182,23 @@ int main(int argc, char** argv) {
   while (i0 < stamps.size() && stamps[i0].second < lo) ++i0;
   while (i1 < stamps.size() && stamps[i1].second < hi) ++i1;
   const double slope = (stamps[i1].first - stamps[i0].first) / static_cast<double>(stamps[i1].second - stamps[i0].second);
+  // the slope over each eighth of the run (a drift over time shows here)
+  {
+    char tmp[64];
+    dbg += ", \"slope_by_eighth\": [";
+    for (int e = 0; e < 8; ++e) {
+      const uint64_t a = K * e / 8, z = K * (e + 1) / 8 - 1;
+      size_t j0 = 0, j1 = 0;
+      while (j0 < stamps.size() && stamps[j0].second < a + 1) ++j0;
+      while (j1 < stamps.size() && stamps[j1].second < z) ++j1;
+      const double sl = j1 < stamps.size() && j0 < j1
+                            ? (stamps[j1].first - stamps[j0].first) / static_cast<double>(stamps[j1].second - stamps[j0].second)
+                            : 0.0;
+      std::snprintf(tmp, sizeof tmp, "%s%.2f", e ? ", " : "", sl);
+      dbg += tmp;
+    }
+    dbg += "]";
+  }
   std::printf("{\"variant\": \"%s\", \"n_pkts\": %llu, \"batches\": %d, \"launch_us\": %.2f, \"ring_us_per_batch\": %.2f, "
               "\"ring_wall_us_per_batch\": %.2f, \"ring_gpps\": %.1f, \"launch_gpps\": %.1f, \"ahead\": %s%s}\n",
               inplace ? "in_place" : "read_only", static_cast<unsigned long long>(n), K, launch_us, slope, wall / K,
