@@ -630,7 +630,7 @@ def run_rank(args) -> None:
                         "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
 
     # ---- the persistent RX ring (nbg_ring_*): one resident classify kernel fed batch descriptors
-    def ring_pass(variant, batches):
+    def ring_pass(variant, batches, n=BATCH):
         """Per-batch time of the ring in steady state: the producer posts the rotating batches whenever
         a slot is free (bare ctypes, prebuilt arguments) and stamps every change of the completed
         count; the time per batch is the slope of completions over the middle three quarters of the
@@ -638,23 +638,38 @@ def run_rank(args) -> None:
         resident kernel).  No grouping on the ring: backend[] (and the in-place swap) only."""
         swap = variant == "in_place"
         ring = mgs[0].ring(swap_macs=swap, stream=streams[0])
-        post, poll, rr = clib.nbg_ring_post, clib.nbg_ring_poll, ring._r
-        bes = [C.c_void_p(o[par]["backend"].data_ptr()) for o in outs for par in (0, 1)]
-        pks = [C.c_void_p(p) for p in pk]
-        tk, cc = C.c_uint64(), C.c_uint64()
+        from netbricks_amd._lib import NbgRingBatch
+
+        burst, poll, rr = clib.nbg_ring_post_burst, clib.nbg_ring_poll, ring._r
+        bes = [o[par]["backend"].data_ptr() for o in outs for par in (0, 1)]
+        # whole batches, or (C4) the 8 contiguous shards of each batch: 64 distinct inputs
+        pks = list(pk) if n == BATCH else [p + s * n * SLOT for p in pk for s in range(8)]
         slots = nb._lib.NBG_RING_SLOTS
+        # the producer's descriptors, prebuilt: batch i of the run is entry i % len(arr); an RX burst
+        # is a window of it (nbg_ring_post_burst posts as many as there are free slots)
+        per = len(pks) * len(bes) // np.gcd(len(pks), len(bes))
+        arr = (NbgRingBatch * (per + slots))()
+        for i in range(per + slots):
+            arr[i] = NbgRingBatch(pks[i % len(pks)], n, bes[i % len(bes)])
+        esz = C.sizeof(NbgRingBatch)
+        base_addr = C.addressof(arr)
+        k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
+
+        def post_upto(first, count):
+            if burst(rr, C.c_void_p(base_addr + (first % per) * esz), count, C.byref(k), C.byref(tk)):
+                raise RuntimeError(f"nbg_ring_post_burst: {nb._lib.last_error()}")
+            return k.value
+
         try:
-            for i in range(16):  # warm: the kernel is resident and every rotating batch touched
-                if post(rr, pks[i % N_BATCHES], BATCH, bes[i % len(bes)], C.byref(tk)):
-                    raise RuntimeError(f"nbg_ring_post: {nb._lib.last_error()}")
+            warm = 0
+            while warm < 16:  # warm: the kernel is resident and the first inputs touched
+                warm += post_upto(warm, 16 - warm)
             ring.wait(15)
             base, stamps, posted, done = 16, [], 0, 0
             t0 = time.perf_counter()
             while done < batches:
-                while posted < batches and posted - done < slots:
-                    if post(rr, pks[posted % N_BATCHES], BATCH, bes[posted % len(bes)], C.byref(tk)):
-                        raise RuntimeError(f"nbg_ring_post: {nb._lib.last_error()}")
-                    posted += 1
+                if posted < batches:
+                    posted += post_upto(16 + posted, min(slots, batches - posted))
                 if poll(rr, C.byref(cc)):
                     raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
                 c = cc.value - base
@@ -669,10 +684,10 @@ def run_rank(args) -> None:
         i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
         us = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]) * 1e6)
         bpp = CLASSIFY_BYTES[variant]
-        ach = BATCH * bpp / us / 1e3
-        return {"value": round(BATCH / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
+        ach = n * bpp / us / 1e3
+        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
                 "wall_us_per_batch": round(wall / batches * 1e6, 2), "batches": batches, "bytes_per_pkt": bpp,
-                "pkts_per_batch": BATCH, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "pkts_per_batch": n, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
                 "kernel": f"classify_ring_kernel<true, {1 if swap else 0}>",
                 "what": "persistent RX ring (nbg_ring_*): one resident classify kernel (LUT staged once) takes "
                         "1M-packet batches as the producer posts them through a pinned descriptor ring, relayed "
@@ -881,7 +896,13 @@ def run_rank(args) -> None:
                         "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
             if not args.no_ring:
                 for v in ("read_only", "in_place"):
-                    variants[f"ring_{v}"] = ring_pass(v, max(args.steps * BATCHES_PER_STEP, 256))
+                    variants[f"ring_{v}"] = ring_pass(v, max(args.steps * BATCHES_PER_STEP, 1024))
+                # C4's per-GPU shard on the ring: 131,072-packet batches without a launch per shard
+                variants["c4_shard_ring"] = ring_pass("in_place", 4096, n=C4_SHARD)
+                variants["c4_shard_ring"]["what"] = (
+                    "C4's per-GPU shard (131,072 packets: one 1M C2 batch in 8 contiguous shards, 64 distinct "
+                    "shards rotating) through the persistent ring, MAC swap in place: no launch, LUT staging "
+                    "or ramp per shard; backend[] + swap only (the grouping of variants.c4_shard is not on the ring)")
             if m_arrs:
                 calls = max(args.steps * BATCHES_PER_STEP // MULTI_K, 10)
                 for v in ("read_only", "in_place"):

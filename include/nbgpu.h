@@ -171,13 +171,16 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
 /*
  * Persistent RX ring (the GPUDirect RX model: an RX queue that never stops, ReceiveBatch::execute
  * polling its port, framework/src/operators/receive_batch.rs:26,52-61).  nbg_ring_start launches ONE
- * streaming-classify kernel on `stream` (one block per CU) that runs until nbg_ring_stop: it stages
- * the LUT in LDS once and classifies batches as they are posted, so no launch, LUT staging or
- * pipeline ramp is paid per batch.  nbg_ring_post hands it one device-resident batch of fixed
- * slots (the streaming kernel's layout: stride % 16 == 0, 64 <= stride < 2^24, fixed_len >= 48,
- * d_pkts and d_backend 16-B aligned) through a descriptor ring in pinned host memory, and returns
- * its ticket (0, 1, 2, ... in post order) without waiting; a post finds a free slot first
- * (NBG_RING_SLOTS batches may be outstanding).  Batch `ticket` is complete when nbg_ring_poll
+ * streaming-classify kernel on `stream` (one block per CU: CUs - 1 classify blocks and a relay
+ * block) that runs until nbg_ring_stop: it stages the LUT in LDS once and classifies batches as
+ * they are posted, so no launch, LUT staging or pipeline ramp is paid per batch.  nbg_ring_post
+ * hands it one device-resident batch of fixed slots (the streaming kernel's layout: stride % 16 ==
+ * 0, 64 <= stride < 2^24, fixed_len >= 48, d_pkts and d_backend 16-B aligned) through a descriptor
+ * ring in pinned host memory (the relay block copies it into HBM; no classify CU reads host
+ * memory), and returns its ticket (0, 1, 2, ... in post order) without waiting; a post finds a free
+ * slot first (NBG_RING_SLOTS batches may be outstanding).  nbg_ring_post_burst posts the first
+ * batches of an array (an RX burst) without waiting: as many as there are free slots, reported in
+ * *n_posted, the first one's ticket in *first_ticket.  Batch `ticket` is complete when nbg_ring_poll
  * reports more than `ticket` completed batches, or nbg_ring_wait(ticket) returns: its backend[] and
  * (NBG_SWAP_MACS) its in-place MAC swap are then in HBM, written through the L2, for any later
  * launch or copy.  Per packet the results are those of nbg_maglev_classify_device_ex with the same
@@ -195,6 +198,13 @@ typedef struct nbg_ring nbg_ring;
 int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms,
                    void* stream, nbg_ring** out);
 int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket);
+typedef struct nbg_ring_batch {
+  uint8_t* d_pkts;
+  uint64_t n_pkts;
+  uint16_t* d_backend;
+} nbg_ring_batch;
+int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
+                        uint64_t* first_ticket);
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);
 int nbg_ring_stop(nbg_ring* r);

@@ -47,6 +47,10 @@ class NbgBatch(C.Structure):
                 ("d_perm", C.c_void_p), ("d_counts", C.c_void_p), ("d_mac_out", C.c_void_p)]
 
 
+class NbgRingBatch(C.Structure):
+    """struct nbg_ring_batch (include/nbgpu.h): one batch of nbg_ring_post_burst."""
+    _fields_ = [("d_pkts", C.c_void_p), ("n_pkts", C.c_uint64), ("d_backend", C.c_void_p)]
+
 
 SIGNATURES = {
     "nbg_maglev_create": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_uint32), C.c_uint32, C.c_uint64,
@@ -65,6 +69,7 @@ SIGNATURES = {
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_ring_start": (C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint32, C.c_uint32, _P, C.POINTER(_P)]),
     "nbg_ring_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),
+    "nbg_ring_post_burst": (C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "nbg_ring_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "nbg_ring_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
     "nbg_ring_stop": (C.c_int, [_P]),

@@ -1252,23 +1252,20 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   return NBG_OK;
 }
 
-int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
-  if (!r || !ticket) return set_error(NBG_EINVAL, "ring_post: null argument");
+}  // extern "C"
+
+namespace {
+
+int ring_check_batch(uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "ring_post: n_pkts must be < 2^30");
   if (n_pkts && (!d_pkts || !d_backend || (reinterpret_cast<uintptr_t>(d_pkts) & 15u) ||
                  (reinterpret_cast<uintptr_t>(d_backend) & 15u)))
     return set_error(NBG_EINVAL, "ring_post: packet and backend buffers must be 16-B aligned");
-  // a free slot: the batch `slots` back is complete
-  const auto t0 = Clock::now();
-  while (r->posted - r->completed >= r->slots) {
-    ring_refresh(r);
-    if (r->posted - r->completed < r->slots) break;
-    if (ring_gone(r)) return ring_state_error(r);
-    if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 1000u))
-      return set_error(NBG_ETIMEDOUT, "ring_post: no slot freed in %u ms", r->idle_ms + 1000u);
-    ring_pause(t0);
-  }
-  if (ring_gone(r)) return ring_state_error(r);
+  return NBG_OK;
+}
+
+// Write batch `posted` into its host slot (the caller found the slot free).
+void ring_put(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
   const uint64_t j = r->posted;
   if (r->completed == j) r->moved = Clock::now();  // the stall clock starts with the first outstanding batch
   const uint64_t units = ((n_pkts + 63) / 64 + 7) / 8;  // 512-packet units of 8 waves' tiles
@@ -1287,7 +1284,48 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
   std::atomic_thread_fence(std::memory_order_release);
   r->posted = j + 1;
   r->units += units;
-  *ticket = j;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
+                        uint64_t* first_ticket) {
+  if (!r || !n_posted || !first_ticket || (n_batches && !batches))
+    return set_error(NBG_EINVAL, "ring_post_burst: null argument");
+  *n_posted = 0;
+  *first_ticket = r->posted;
+  for (uint32_t i = 0; i < n_batches; ++i) {
+    const int rc = ring_check_batch(batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
+    if (rc) return rc;
+  }
+  ring_refresh(r);
+  if (ring_gone(r)) return ring_state_error(r);
+  const uint64_t room = r->slots - (r->posted - r->completed);
+  const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(room, n_batches));
+  for (uint32_t i = 0; i < k; ++i) ring_put(r, batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
+  *n_posted = k;
+  return NBG_OK;
+}
+
+int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
+  if (!r || !ticket) return set_error(NBG_EINVAL, "ring_post: null argument");
+  int rc = ring_check_batch(d_pkts, n_pkts, d_backend);
+  if (rc) return rc;
+  // a free slot: the batch `slots` back is complete
+  const auto t0 = Clock::now();
+  while (r->posted - r->completed >= r->slots) {
+    ring_refresh(r);
+    if (r->posted - r->completed < r->slots) break;
+    if (ring_gone(r)) return ring_state_error(r);
+    if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 1000u))
+      return set_error(NBG_ETIMEDOUT, "ring_post: no slot freed in %u ms", r->idle_ms + 1000u);
+    ring_pause(t0);
+  }
+  if (ring_gone(r)) return ring_state_error(r);
+  *ticket = r->posted;
+  ring_put(r, d_pkts, n_pkts, d_backend);
   return NBG_OK;
 }
 

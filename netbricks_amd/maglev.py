@@ -17,7 +17,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_MAX_MULTI, NBG_OWNED_WINDOWS,
-                   NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch,
+                   NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch, NbgRingBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "Ring", "build_lut", "make_trace", "NBG_SENTINEL"]
@@ -369,6 +369,29 @@ class Ring:
         check(lib.nbg_ring_post(self._r, _ptr(pkts), n_pkts, _ptr(backend), C.byref(t)), "nbg_ring_post")
         self._held[t.value] = (pkts, backend)
         return t.value
+
+    def post_burst(self, batches) -> tuple:
+        """Post the first batches of `batches` ((pkts, n_pkts, backend) triples, an RX burst) without
+        waiting for slots (nbg_ring_post_burst): returns (number posted, first ticket); the rest is
+        for a later call."""
+        import torch
+
+        if self._r is None:
+            raise RuntimeError("ring: stopped")
+        dev = torch.device("cuda", self._mg.device)
+        arr = (NbgRingBatch * max(len(batches), 1))()
+        for i, (pkts, n_pkts, backend) in enumerate(batches):
+            if pkts.dtype != torch.uint8 or not pkts.is_contiguous() or pkts.device != dev:
+                raise ValueError(f"pkts: expected a contiguous uint8 tensor on {dev}")
+            if n_pkts and pkts.numel() < (n_pkts - 1) * self.stride + _slot_tail(self.stride, self.frame_len):
+                raise ValueError("pkts: too small for n_pkts slots")
+            _check_dev("backend", backend, torch.uint16, n_pkts, dev)
+            arr[i] = NbgRingBatch(_ptr(pkts), n_pkts, _ptr(backend))
+        k, t = C.c_uint32(), C.c_uint64()
+        check(lib.nbg_ring_post_burst(self._r, arr, len(batches), C.byref(k), C.byref(t)), "nbg_ring_post_burst")
+        for i in range(k.value):
+            self._held[t.value + i] = (batches[i][0], batches[i][2])
+        return k.value, t.value
 
     def poll(self) -> int:
         c = C.c_uint64()
