@@ -647,7 +647,7 @@ def run_rank(args) -> None:
         slots = nb._lib.NBG_RING_SLOTS
         # the producer's descriptors, prebuilt: batch i of the run is entry i % len(arr); an RX burst
         # is a window of it (nbg_ring_post_burst posts as many as there are free slots)
-        per = len(pks) * len(bes) // np.gcd(len(pks), len(bes))
+        per = len(pks) * len(bes) // int(np.gcd(len(pks), len(bes)))
         arr = (NbgRingBatch * (per + slots))()
         for i in range(per + slots):
             arr[i] = NbgRingBatch(pks[i % len(pks)], n, bes[i % len(bes)])
