@@ -205,6 +205,13 @@ typedef struct nbg_ring_batch {
 } nbg_ring_batch;
 int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
                         uint64_t* first_ticket);
+/* Group a completed ring batch: perm (u32[n], packet indices grouped by backend, arrival order inside
+ * a group) and counts (u32[nb+1]) from its backend[], as nbg_maglev_classify_device_ex would give them
+ * (group_by.rs:46-51).  Two launches on `stream`, which must not be the ring's own (its kernel holds
+ * it); they co-run with the resident ring kernel.  `ticket` must be complete and among the last
+ * NBG_RING_SLOTS posted.  Calls share the ring's grouping scratch: a call on another stream than the
+ * previous one waits for the previous one's work first. */
+int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream);
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);
 int nbg_ring_stop(nbg_ring* r);

@@ -70,6 +70,7 @@ SIGNATURES = {
     "nbg_ring_start": (C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint32, C.c_uint32, _P, C.POINTER(_P)]),
     "nbg_ring_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),
     "nbg_ring_post_burst": (C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    "nbg_ring_group": (C.c_int, [_P, C.c_uint64, _P, _P, _P]),
     "nbg_ring_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "nbg_ring_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
     "nbg_ring_stop": (C.c_int, [_P]),

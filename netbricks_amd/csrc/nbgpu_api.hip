@@ -1110,6 +1110,12 @@ struct nbg_ring {
   int grid = 0;
   uint32_t idle_ms = 0;
   uint64_t posted = 0, units = 0, completed = 0;
+  // per slot, the batch posted there last (nbg_ring_group groups it from its backend[])
+  std::vector<std::pair<uint16_t*, uint64_t>> rec;
+  uint32_t* d_rows = nullptr;    // nbg_ring_group: partition histograms [kMaxParts][nb+1]
+  uint32_t* d_prefix = nullptr;  // and, for the scan-kernel path, per-partition prefixes
+  uint32_t* d_totals = nullptr;  // and totals [nb+1]
+  hipStream_t group_stream = nullptr;  // the stream of the last nbg_ring_group (its scratch's user)
   bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
   // hipStreamQuery is not cheap on a stream with a resident kernel, so the kernel's end is only
   // checked after the completed count has not moved for kStallCheck
@@ -1156,8 +1162,12 @@ void ring_pause(Clock::time_point t0) {
 }
 
 void ring_free(nbg_ring* r) {
+  if (r->group_stream) (void)hipStreamSynchronize(r->group_stream);  // its kernels use the scratch below
   if (r->host) (void)hipHostFree(r->host);
   if (r->dev) (void)hipFree(r->dev);
+  (void)hipFree(r->d_rows);
+  (void)hipFree(r->d_prefix);
+  (void)hipFree(r->d_totals);
   delete r;
 }
 
@@ -1207,6 +1217,13 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&r->dev), dbytes, hipDeviceMallocUncached) != hipSuccess) {
     ring_free(r);
     return set_error(NBG_ENOMEM, "ring_start: uncached device ring of %zu B", dbytes);
+  }
+  const size_t nbins = static_cast<size_t>(h->nb) + 1;
+  r->rec.assign(r->slots, {nullptr, 0});
+  if (hipMalloc(&r->d_rows, kMaxParts * nbins * 4) != hipSuccess ||
+      hipMalloc(&r->d_prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&r->d_totals, nbins * 4) != hipSuccess) {
+    ring_free(r);
+    return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
   }
   {
     SetupStream st;
@@ -1282,6 +1299,7 @@ void ring_put(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend
   const uint64_t* src = reinterpret_cast<const uint64_t*>(&d);
   for (int i = 0; i < 8; ++i) dst[i] = src[i];
   std::atomic_thread_fence(std::memory_order_release);
+  r->rec[j & (r->slots - 1)] = {d_backend, n_pkts};
   r->posted = j + 1;
   r->units += units;
 }
@@ -1327,6 +1345,73 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
   *ticket = r->posted;
   ring_put(r, d_pkts, n_pkts, d_backend);
   return NBG_OK;
+}
+
+int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
+  if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group: null argument");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (s == r->stream) return set_error(NBG_EINVAL, "ring_group: the ring's own stream is held by its kernel");
+  if (ticket >= r->posted) return set_error(NBG_EINVAL, "ring_group: ticket %llu was not posted", (unsigned long long)ticket);
+  if (r->posted - ticket > r->slots)
+    return set_error(NBG_EINVAL, "ring_group: ticket %llu is older than the ring's %u slots", (unsigned long long)ticket,
+                     r->slots);
+  ring_refresh(r);
+  if (ticket >= r->completed)
+    return set_error(NBG_EINVAL, "ring_group: batch %llu is not complete", (unsigned long long)ticket);
+  DeviceGuard g(r->h->device);
+  const auto [backend, n_pkts] = r->rec[ticket & (r->slots - 1)];
+  const uint32_t nbins = r->h->nb + 1;
+  // one stream uses the scratch at a time: a new stream first waits for the previous one's work
+  if (r->group_stream && r->group_stream != s) {
+    hipEvent_t ev = nullptr;
+    NBG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    const hipError_t e1 = hipEventRecord(ev, r->group_stream), e2 = hipStreamWaitEvent(s, ev, 0);
+    (void)hipEventDestroy(ev);
+    if (e1 != hipSuccess || e2 != hipSuccess) return set_error(NBG_EIO, "ring_group: stream order");
+  }
+  r->group_stream = s;
+  if (n_pkts == 0) {
+    NBG_HIP(hipMemsetAsync(d_counts, 0, nbins * 4, s));
+    return NBG_OK;
+  }
+  const uint64_t per = (n_pkts + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
+  const uint32_t part_pkts = static_cast<uint32_t>(per * kChunk);
+  const uint32_t n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
+  HistArgs ha{};
+  ha.backend = backend;
+  ha.n_pkts = static_cast<uint32_t>(n_pkts);
+  ha.nb = r->h->nb;
+  ha.part_pkts = part_pkts;
+  ha.n_parts = n_parts;
+  ha.part_hist = r->d_rows;
+  int rc = launch_hist(ha, s);
+  if (rc) return rc;
+  const int scan = pick_group_scan(nbins, n_parts);
+  if (scan == kScanKernel) {
+    ScanArgs sa{};
+    sa.part_hist = r->d_rows;
+    sa.part_prefix = r->d_prefix;
+    sa.totals = r->d_totals;
+    sa.n_parts = n_parts;
+    sa.nbins = nbins;
+    if ((rc = launch_scan(sa, s))) return rc;
+  }
+  GroupArgs ga{};
+  ga.backend = backend;
+  ga.n_pkts = static_cast<uint32_t>(n_pkts);
+  ga.nb = r->h->nb;
+  uint32_t bits = 0;
+  while ((1u << bits) < nbins) ++bits;
+  ga.bits = bits;
+  ga.n_parts = n_parts;
+  ga.part_pkts = part_pkts;
+  ga.part_hist = r->d_rows;
+  ga.part_prefix = r->d_prefix;
+  ga.totals = r->d_totals;
+  ga.hist16 = 0;
+  ga.counts = d_counts;
+  ga.perm = d_perm;
+  return launch_group(ga, scan, s);
 }
 
 // Diagnostics (not in include/nbgpu.h): the host control line's 16 words.

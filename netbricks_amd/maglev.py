@@ -393,6 +393,20 @@ class Ring:
             self._held[t.value + i] = (batches[i][0], batches[i][2])
         return k.value, t.value
 
+    def group(self, ticket: int, perm, counts, stream=None) -> None:
+        """perm / counts of a completed batch (nbg_ring_group) on `stream` (default: torch's current
+        stream; never the ring's own)."""
+        import torch
+
+        if self._r is None:
+            raise RuntimeError("ring: stopped")
+        dev = torch.device("cuda", self._mg.device)
+        _check_dev("perm", perm, torch.uint32, 0, dev)
+        _check_dev("counts", counts, torch.uint32, self._mg.n_backends + 1, dev)
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        st = st.cuda_stream if hasattr(st, "cuda_stream") else st
+        check(lib.nbg_ring_group(self._r, ticket, _ptr(perm), _ptr(counts), st), "nbg_ring_group")
+
     def poll(self) -> int:
         c = C.c_uint64()
         check(lib.nbg_ring_poll(self._r, C.byref(c)), "nbg_ring_poll")
