@@ -61,6 +61,7 @@ IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the 
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
 # flight); the environment overrides are for sweeps (tools/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
+RING_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_RING_GROUP_STREAMS", "2"))  # side streams grouping ring batches
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet of the classify kernel per variant:
@@ -694,6 +695,64 @@ def run_rank(args) -> None:
                         "into HBM by the kernel's last block; per-batch time from the completion slope; "
                         "backend[] (+ in-place MAC swap) only, no grouping"}
 
+    def ring_group_pass(batches, n=BATCH):
+        """The whole in-place path on the ring: the producer posts RX bursts, and every batch the ring
+        completes is grouped at once (nbg_ring_group: hist + group launches on a side stream, beside
+        the resident ring kernel; RING_GROUP_STREAMS side streams round-robin).  Whole-job time from
+        the first post to the last group's end; 80
+        distinct backend[] buffers, so no batch's backend[] is rewritten before its grouping ran."""
+        ring = mgs[0].ring(swap_macs=True, stream=streams[0])
+        from netbricks_amd._lib import NbgRingBatch
+
+        burst, poll, grp, rr = clib.nbg_ring_post_burst, clib.nbg_ring_poll, clib.nbg_ring_group, ring._r
+        nbe = 80
+        gbe = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(nbe)]
+        # whole batches, or (C4) the 8 contiguous shards of each batch: 64 distinct inputs
+        gpk = list(pk) if n == BATCH else [p + q * n * SLOT for p in pk for q in range(8)]
+        sides = [torch.cuda.Stream(dev) for _ in range(RING_GROUP_STREAMS)]
+        slots = nb._lib.NBG_RING_SLOTS
+        per = len(gpk) * nbe // int(np.gcd(len(gpk), nbe))
+        arr = (NbgRingBatch * (per + slots))()
+        for i in range(per + slots):
+            arr[i] = NbgRingBatch(gpk[i % len(gpk)], n, gbe[i % nbe].data_ptr())
+        esz, base_addr = C.sizeof(NbgRingBatch), C.addressof(arr)
+        k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
+        sps = [C.c_void_p(x.cuda_stream) for x in sides]
+        # one perm / counts set per side stream (each stream's groups run in its order)
+        gperm = [torch.empty(n, dtype=torch.uint32, device=dev) for _ in sides]
+        gcnt = [torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev) for _ in sides]
+        pps = [C.c_void_p(x.data_ptr()) for x in gperm]
+        cps = [C.c_void_p(x.data_ptr()) for x in gcnt]
+        try:
+            t0 = time.perf_counter()
+            posted = grouped = 0
+            while grouped < batches:
+                # a batch's slot (and record) is reused only once it is grouped
+                room = min(batches - posted, grouped + slots - posted)
+                if room > 0:
+                    if burst(rr, C.c_void_p(base_addr + (posted % per) * esz), room, C.byref(k), C.byref(tk)):
+                        raise RuntimeError(f"nbg_ring_post_burst: {nb._lib.last_error()}")
+                    posted += k.value
+                if poll(rr, C.byref(cc)):
+                    raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
+                while grouped < cc.value:
+                    q = grouped % len(sides)
+                    if grp(rr, grouped, pps[q], cps[q], sps[q]):
+                        raise RuntimeError(f"nbg_ring_group: {nb._lib.last_error()}")
+                    grouped += 1
+            for x in sides:
+                x.synchronize()
+            wall = time.perf_counter() - t0
+        finally:
+            ring.stop()
+        us = wall / batches * 1e6
+        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
+                "pkts_per_batch": n, "path_bytes_per_pkt": PATH_BYTES["in_place"], "group_streams": len(sides),
+                "frac": round(n * PATH_BYTES["in_place"] / us / 1e3 / HBM_PEAK_GBPS, 4),
+                "what": "C2 in place + grouping on the persistent ring: RX bursts posted to the resident classify "
+                        "kernel, each completed batch grouped at once by nbg_ring_group (hist + group launches on a "
+                        "side stream, co-running with the ring); whole-job wall time incl. the ring's ramp"}
+
     # ---- configs C3 / C5 (IMIX descriptors): handles, traces and one call per batch
     imix = {}
 
@@ -899,6 +958,8 @@ def run_rank(args) -> None:
                     variants[f"ring_{v}"] = ring_pass(v, max(args.steps * BATCHES_PER_STEP, 1024))
                 # C4's per-GPU shard on the ring: 131,072-packet batches without a launch per shard
                 variants["c4_shard_ring"] = ring_pass("in_place", 4096, n=C4_SHARD)
+                variants["ring_in_place_grouped"] = ring_group_pass(max(args.steps * BATCHES_PER_STEP, 1024))
+                variants["c4_shard_ring_grouped"] = ring_group_pass(4096, n=C4_SHARD)
                 variants["c4_shard_ring"]["what"] = (
                     "C4's per-GPU shard (131,072 packets: one 1M C2 batch in 8 contiguous shards, 64 distinct "
                     "shards rotating) through the persistent ring, MAC swap in place: no launch, LUT staging "

@@ -186,7 +186,9 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
  * launch or copy.  Per packet the results are those of nbg_maglev_classify_device_ex with the same
  * arguments and no grouping (perm / counts are not produced on the ring).  Everything a post names
  * stays untouched by the caller until the batch is complete.
- * The kernel owns its stream (and the LDS of every CU it occupies) until it ends: after
+ * The kernel runs on a private stream of the highest priority (a hardware queue no ordinary stream
+ * shares: work queued behind a resident kernel would wait for it) and starts after the work issued
+ * on `stream` so far.  It holds the LDS of every CU it occupies until it ends: after
  * nbg_ring_stop, or by itself after idle_ms without a post (its exit condition when the producer
  * goes away; 0 = 2000 ms; the next ring call then returns NBG_ETIMEDOUT).  nbg_ring_stop completes
  * every posted batch, waits for the kernel to end, and frees the ring.  One ring per handle; one
@@ -207,10 +209,11 @@ int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_b
                         uint64_t* first_ticket);
 /* Group a completed ring batch: perm (u32[n], packet indices grouped by backend, arrival order inside
  * a group) and counts (u32[nb+1]) from its backend[], as nbg_maglev_classify_device_ex would give them
- * (group_by.rs:46-51).  Two launches on `stream`, which must not be the ring's own (its kernel holds
- * it); they co-run with the resident ring kernel.  `ticket` must be complete and among the last
- * NBG_RING_SLOTS posted.  Calls share the ring's grouping scratch: a call on another stream than the
- * previous one waits for the previous one's work first. */
+ * (group_by.rs:46-51).  Two launches on `stream` (any caller stream); they co-run with the resident
+ * ring kernel.  `ticket` must be complete and among the last
+ * NBG_RING_SLOTS posted.  Up to 4 side streams group concurrently (one scratch set each; calls on
+ * one stream run in its order); a further stream takes over the least recently used set after that
+ * set's stream's work. */
 int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream);
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);

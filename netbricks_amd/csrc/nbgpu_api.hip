@@ -1100,7 +1100,7 @@ int nbg_maglev_check(nbg_maglev* h) {
 
 struct nbg_ring {
   nbg_maglev* h = nullptr;
-  hipStream_t stream = nullptr;        // the ring kernel's (the caller's)
+  hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
   uint8_t* host = nullptr;             // pinned, mapped: RingCtl | RingDesc[slots]
   uint8_t* dev = nullptr;              // uncached HBM: stop word (own line) | prog[grid] | RingDesc[reps][slots]
   volatile RingCtl* ctl = nullptr;
@@ -1112,10 +1112,18 @@ struct nbg_ring {
   uint64_t posted = 0, units = 0, completed = 0;
   // per slot, the batch posted there last (nbg_ring_group groups it from its backend[])
   std::vector<std::pair<uint16_t*, uint64_t>> rec;
-  uint32_t* d_rows = nullptr;    // nbg_ring_group: partition histograms [kMaxParts][nb+1]
-  uint32_t* d_prefix = nullptr;  // and, for the scan-kernel path, per-partition prefixes
-  uint32_t* d_totals = nullptr;  // and totals [nb+1]
-  hipStream_t group_stream = nullptr;  // the stream of the last nbg_ring_group (its scratch's user)
+  // nbg_ring_group's scratch, one set per side stream (up to kGroupSets streams group concurrently;
+  // a further stream takes over the least recently used set after that set's stream's work)
+  struct GroupSet {
+    hipStream_t s = nullptr;       // the stream that uses the set
+    uint64_t used = 0;             // last use (call count)
+    uint32_t* rows = nullptr;      // partition histograms [kMaxParts][nb+1]
+    uint32_t* prefix = nullptr;    // per-partition prefixes (scan-kernel path)
+    uint32_t* totals = nullptr;    // totals [nb+1]
+  };
+  static constexpr int kGroupSets = 4;
+  GroupSet gsets[kGroupSets];
+  uint64_t gcalls = 0;
   bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
   // hipStreamQuery is not cheap on a stream with a resident kernel, so the kernel's end is only
   // checked after the completed count has not moved for kStallCheck
@@ -1162,12 +1170,15 @@ void ring_pause(Clock::time_point t0) {
 }
 
 void ring_free(nbg_ring* r) {
-  if (r->group_stream) (void)hipStreamSynchronize(r->group_stream);  // its kernels use the scratch below
+  for (auto& g : r->gsets) {
+    if (g.s) (void)hipStreamSynchronize(g.s);  // its kernels use the scratch below
+    (void)hipFree(g.rows);
+    (void)hipFree(g.prefix);
+    (void)hipFree(g.totals);
+  }
   if (r->host) (void)hipHostFree(r->host);
   if (r->dev) (void)hipFree(r->dev);
-  (void)hipFree(r->d_rows);
-  (void)hipFree(r->d_prefix);
-  (void)hipFree(r->d_totals);
+  if (r->stream) (void)hipStreamDestroy(r->stream);
   delete r;
 }
 
@@ -1193,8 +1204,28 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   auto* r = new (std::nothrow) nbg_ring;
   if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
   r->h = h;
-  r->stream = s;
   r->grid = h->cus - 1;  // classify blocks; one more block, on a CU of its own, is the relay
+  // The kernel runs on a private stream of the highest priority: HIP maps streams onto at most
+  // GPU_MAX_HW_QUEUES hardware queues per priority, and work on any stream that shared the ring's
+  // queue would wait behind the resident kernel (measured: a third grouping stream did, until the
+  // ring's idle exit).  It starts after everything issued on `stream` so far.
+  {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    hipEvent_t ev = nullptr;
+    if (hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+      r->stream = nullptr;
+      ring_free(r);
+      return set_error(NBG_EIO, "ring_start: private stream");
+    }
+    const bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+                    hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent(r->stream, ev, 0) == hipSuccess;
+    if (ev) (void)hipEventDestroy(ev);
+    if (!ok) {
+      ring_free(r);
+      return set_error(NBG_EIO, "ring_start: ordering after the caller's stream");
+    }
+  }
   r->idle_ms = idle_ms ? idle_ms : 2000u;
   r->moved = Clock::now();
   if (const char* e = std::getenv("NBG_RING_REPS")) {  // measurement: replicas, a power of two <= 256
@@ -1220,11 +1251,12 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   }
   const size_t nbins = static_cast<size_t>(h->nb) + 1;
   r->rec.assign(r->slots, {nullptr, 0});
-  if (hipMalloc(&r->d_rows, kMaxParts * nbins * 4) != hipSuccess ||
-      hipMalloc(&r->d_prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&r->d_totals, nbins * 4) != hipSuccess) {
-    ring_free(r);
-    return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
-  }
+  for (auto& g : r->gsets)
+    if (hipMalloc(&g.rows, kMaxParts * nbins * 4) != hipSuccess ||
+        hipMalloc(&g.prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&g.totals, nbins * 4) != hipSuccess) {
+      ring_free(r);
+      return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
+    }
   {
     SetupStream st;
     (void)st.zero(r->dev, dbytes);
@@ -1258,7 +1290,7 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
   const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
   ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
-  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, s))) {
+  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, r->stream))) {
     ring_free(r);
     return rc;
   }
@@ -1350,7 +1382,6 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
 int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
   if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group: null argument");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (s == r->stream) return set_error(NBG_EINVAL, "ring_group: the ring's own stream is held by its kernel");
   if (ticket >= r->posted) return set_error(NBG_EINVAL, "ring_group: ticket %llu was not posted", (unsigned long long)ticket);
   if (r->posted - ticket > r->slots)
     return set_error(NBG_EINVAL, "ring_group: ticket %llu is older than the ring's %u slots", (unsigned long long)ticket,
@@ -1361,15 +1392,25 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
   DeviceGuard g(r->h->device);
   const auto [backend, n_pkts] = r->rec[ticket & (r->slots - 1)];
   const uint32_t nbins = r->h->nb + 1;
-  // one stream uses the scratch at a time: a new stream first waits for the previous one's work
-  if (r->group_stream && r->group_stream != s) {
-    hipEvent_t ev = nullptr;
-    NBG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    const hipError_t e1 = hipEventRecord(ev, r->group_stream), e2 = hipStreamWaitEvent(s, ev, 0);
-    (void)hipEventDestroy(ev);
-    if (e1 != hipSuccess || e2 != hipSuccess) return set_error(NBG_EIO, "ring_group: stream order");
+  // this stream's scratch set; a stream without one takes a free set, or the least recently used
+  // one after everything its previous stream has issued so far
+  nbg_ring::GroupSet* gs = nullptr;
+  for (auto& g : r->gsets)
+    if (g.s == s) gs = &g;
+  if (!gs) {
+    gs = &r->gsets[0];
+    for (auto& g : r->gsets)
+      if (!g.s || (gs->s && g.used < gs->used)) gs = &g;
+    if (gs->s) {
+      hipEvent_t ev = nullptr;
+      NBG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      const hipError_t e1 = hipEventRecord(ev, gs->s), e2 = hipStreamWaitEvent(s, ev, 0);
+      (void)hipEventDestroy(ev);
+      if (e1 != hipSuccess || e2 != hipSuccess) return set_error(NBG_EIO, "ring_group: stream order");
+    }
+    gs->s = s;
   }
-  r->group_stream = s;
+  gs->used = ++r->gcalls;
   if (n_pkts == 0) {
     NBG_HIP(hipMemsetAsync(d_counts, 0, nbins * 4, s));
     return NBG_OK;
@@ -1383,15 +1424,15 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
   ha.nb = r->h->nb;
   ha.part_pkts = part_pkts;
   ha.n_parts = n_parts;
-  ha.part_hist = r->d_rows;
+  ha.part_hist = gs->rows;
   int rc = launch_hist(ha, s);
   if (rc) return rc;
   const int scan = pick_group_scan(nbins, n_parts);
   if (scan == kScanKernel) {
     ScanArgs sa{};
-    sa.part_hist = r->d_rows;
-    sa.part_prefix = r->d_prefix;
-    sa.totals = r->d_totals;
+    sa.part_hist = gs->rows;
+    sa.part_prefix = gs->prefix;
+    sa.totals = gs->totals;
     sa.n_parts = n_parts;
     sa.nbins = nbins;
     if ((rc = launch_scan(sa, s))) return rc;
@@ -1405,9 +1446,9 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
   ga.bits = bits;
   ga.n_parts = n_parts;
   ga.part_pkts = part_pkts;
-  ga.part_hist = r->d_rows;
-  ga.part_prefix = r->d_prefix;
-  ga.totals = r->d_totals;
+  ga.part_hist = gs->rows;
+  ga.part_prefix = gs->prefix;
+  ga.totals = gs->totals;
   ga.hist16 = 0;
   ga.counts = d_counts;
   ga.perm = d_perm;

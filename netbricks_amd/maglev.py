@@ -338,7 +338,8 @@ class Ring:
     resident and classifies device-resident fixed-slot batches as they are posted (the RX queue that
     never stops, framework/src/operators/receive_batch.rs:26,52-61).  post() returns a ticket;
     wait(ticket) / poll() report completion, after which the batch's backend[] (and in-place swap)
-    are in HBM.  The kernel owns its stream until stop() (or idle_ms without a post)."""
+    are in HBM.  The kernel runs on a private high-priority stream, ordered after `stream`'s earlier
+    work, until stop() (or idle_ms without a post)."""
 
     def __init__(self, mg: "Maglev", *, stride: int, frame_len: int, swap_macs: bool, idle_ms: int, stream=None):
         import torch
@@ -395,7 +396,7 @@ class Ring:
 
     def group(self, ticket: int, perm, counts, stream=None) -> None:
         """perm / counts of a completed batch (nbg_ring_group) on `stream` (default: torch's current
-        stream; never the ring's own)."""
+        stream)."""
         import torch
 
         if self._r is None:

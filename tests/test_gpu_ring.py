@@ -112,7 +112,7 @@ def test_ring_post_burst(torch_cuda, swap):
 
 @pytest.mark.parametrize("swap", [False, True])
 def test_ring_group(torch_cuda, swap):
-    """nbg_ring_group: every completed batch grouped on a side stream while the ring keeps running
+    """nbg_ring_group: every completed batch grouped on side streams while the ring keeps running
     (the ring kernel stays resident), perm / counts bit-exact against the oracle's grouping of that
     batch; sizes from one packet to 1M (direct scan) and 2.1M (several chunks per partition)."""
     torch = torch_cuda
@@ -126,19 +126,21 @@ def test_ring_group(torch_cuda, swap):
     outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for n in sizes]
     perms = [torch.empty(n, dtype=torch.uint32, device="cuda") for n in sizes]
     counts = [torch.zeros(66, dtype=torch.uint32, device="cuda") for _ in sizes]
-    side = torch.cuda.Stream()
+    # five side streams round-robin: four own a scratch set, the fifth takes one over
+    sides = [torch.cuda.Stream() for _ in range(5)]
     torch.cuda.synchronize()
     with mg.ring(swap_macs=swap) as ring:
         for i, n in enumerate(sizes):
             t = ring.post(d[i], n, outs[i])
             if i:  # group each batch once complete, while the next one is still running
                 ring.wait(t - 1)
-                ring.group(t - 1, perms[i - 1], counts[i - 1], stream=side)
+                ring.group(t - 1, perms[i - 1], counts[i - 1], stream=sides[(i - 1) % 5])
         ring.wait(len(sizes) - 1)
-        ring.group(len(sizes) - 1, perms[-1], counts[-1], stream=side)
-        side.synchronize()
-        with pytest.raises(nb.NbgError):  # the ring's own stream is held by its kernel
-            ring.group(0, perms[0], counts[0], stream=ring._stream)
+        ring.group(len(sizes) - 1, perms[-1], counts[-1], stream=sides[(len(sizes) - 1) % 5])
+        for st in sides:
+            st.synchronize()
+        with pytest.raises(nb.NbgError):  # not complete: not posted
+            ring.group(len(sizes), perms[0], counts[0], stream=sides[0])
     for i, n in enumerate(sizes):
         be, _ = _expect(bufs[i], n, lut, swap)
         exp_perm, exp_cnt = orc.group(be, 65)

@@ -1,0 +1,6 @@
+#!/bin/bash
+# Round 3: the default bench line alone.
+cd "$GRAFT_REPO_ROOT" || exit 9
+mkdir -p gpurun_out
+timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+rc=$?; tail -3 gpurun_out/bench.err; exit $rc
