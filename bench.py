@@ -79,6 +79,7 @@ PMC_WARMUP, PMC_STEPS = 10, 40
 # the child's launch sequence, one classify dispatch per call, in this order
 PMC_ORDER = ("in_place", "in_place_lag", "records", "read_only", "c4_shard", "c3", "c5")
 PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
+PMC_RING_BATCHES = 64  # then one ring run (one dispatch) of this many in-place batches
 NBG_SWAP_MACS, NBG_DEFER_GROUP, NBG_GROUP_LAG = 0x1, 0x10, 0x80
 
 
@@ -260,8 +261,9 @@ class KernelTimer:
 # PMC traffic (launcher, N = 1): two rocprofv3 --pmc passes of a short child run
 # ---------------------------------------------------------------------------------------------
 
-def _pmc_rows(d, counter):
-    """Classify-kernel counter values (bytes) in dispatch order from one --pmc pass."""
+def _pmc_rows(d, counter, ring=False):
+    """Classify-kernel counter values (bytes) in dispatch order from one --pmc pass (ring: the
+    persistent ring kernel's dispatches instead)."""
     path = None
     for dp, _, files in os.walk(d):
         for f in files:
@@ -272,7 +274,8 @@ def _pmc_rows(d, counter):
     rows = []
     for row in csv.DictReader(open(path)):
         name = row.get("Kernel_Name", "")
-        if row.get("Counter_Name") == counter and ("classify_stream_kernel" in name or "classify_kernel" in name):
+        want = ("classify_ring_kernel" in name) if ring else ("classify_stream_kernel" in name or "classify_kernel" in name)
+        if row.get("Counter_Name") == counter and want:
             rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0,
                          name))
     rows.sort()
@@ -302,7 +305,7 @@ def pmc_traffic(timeout_s: int = 180):
     if shutil.which("rocprofv3") is None:
         return {"error": "rocprofv3 not found"}
     env = dict(os.environ, TMPDIR="/tmp")
-    vals, names = {}, []
+    vals, names, rvals = {}, [], {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"nbg_pmc_{counter}_", dir="/tmp")
         cmd = ["timeout", "-k", "5", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", counter, "--kernel-trace",
@@ -314,6 +317,7 @@ def pmc_traffic(timeout_s: int = 180):
             return {"error": f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr[-300:]}"}
         try:
             vals[counter], names = _pmc_rows(d, counter)
+            rvals[counter], _ = _pmc_rows(d, counter, ring=True)
         finally:
             shutil.rmtree(d, ignore_errors=True)
     seg = PMC_WARMUP + PMC_STEPS
@@ -334,6 +338,14 @@ def pmc_traffic(timeout_s: int = 180):
         out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
                      "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
                      "kernel": kname.replace("void nbg::(anonymous namespace)::", "").split("(nbg::")[0]}
+    if len(rvals.get("FETCH_SIZE", [])) == 1 and len(rvals.get("WRITE_SIZE", [])) == 1:
+        # the ring: one dispatch for PMC_RING_BATCHES batches (in place, no grouping beside it)
+        rd, wr = 2.0 * rvals["FETCH_SIZE"][0], rvals["WRITE_SIZE"][0]
+        alg = PMC_RING_BATCHES * BATCH * CLASSIFY_BYTES["in_place"]
+        out["ring"] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
+                                "batches": PMC_RING_BATCHES, "hbm_bytes_per_batch": round((rd + wr) / PMC_RING_BATCHES),
+                                "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
+                                "kernel": "classify_ring_kernel<true, 1>"}
     return out
 
 
@@ -390,7 +402,18 @@ def launch(args, argv) -> int:
         pmc = pmc_traffic()
         log(f"bench: PMC passes {time.time() - t0:.0f}s")
         line["pmc"] = pmc
-        if isinstance(pmc, dict) and "in_place" in pmc:
+        roof = line.get("roofline", {})
+        ring_v = line.get("variants", {}).get("ring_in_place")
+        if isinstance(pmc, dict) and "ring" in pmc and isinstance(ring_v, dict) and "us_per_batch" in ring_v:
+            ring_v["traffic_per_batch"] = pmc["ring"]["hbm_bytes_per_batch"]
+            ring_v["traffic_ratio"] = pmc["ring"]["ratio"]
+        if isinstance(pmc, dict) and roof.get("kernel", "").startswith("classify_ring_kernel") and "ring" in pmc:
+            # per launch, like `achieved`: the measured bytes per batch x the timed launch's batches
+            roof["traffic"] = pmc["ring"]["hbm_bytes_per_batch"] * roof["batches_per_launch"]
+            roof["traffic_ratio"] = pmc["ring"]["ratio"]
+            if "launch_in_place" in line.get("variants", {}) and "in_place" in pmc:
+                line["variants"]["launch_in_place"]["traffic"] = pmc["in_place"]["hbm_bytes"]
+        elif isinstance(pmc, dict) and "in_place" in pmc:
             line["roofline"]["traffic"] = pmc["in_place"]["hbm_bytes"]
             for k, v in line.get("variants", {}).items():
                 if k in pmc and isinstance(v, dict):
@@ -695,36 +718,40 @@ def run_rank(args) -> None:
                         "into HBM by the kernel's last block; per-batch time from the completion slope; "
                         "backend[] (+ in-place MAC swap) only, no grouping"}
 
-    def ring_group_pass(batches, n=BATCH):
-        """The whole in-place path on the ring: the producer posts RX bursts, and every batch the ring
-        completes is grouped at once (nbg_ring_group: hist + group launches on a side stream, beside
-        the resident ring kernel; RING_GROUP_STREAMS side streams round-robin).  Whole-job time from
-        the first post to the last group's end; 80
-        distinct backend[] buffers, so no batch's backend[] is rewritten before its grouping ran."""
-        ring = mgs[0].ring(swap_macs=True, stream=streams[0])
+    ring_res = {}
+
+    def ring_path(batches, n=BATCH):
+        """The whole in-place path on the ring: start the ring (its buffers are kept by the handle after
+        the first start), post RX bursts, group every batch the ring completes at once (nbg_ring_group:
+        hist + group launches on RING_GROUP_STREAMS side streams, beside the resident ring kernel), wait
+        for the last group, stop the ring.  80 distinct backend[] buffers, so no batch's backend[] is
+        rewritten before its grouping ran.  Returns (wall seconds, ring kernel ms by HIP events)."""
         from netbricks_amd._lib import NbgRingBatch
 
-        burst, poll, grp, rr = clib.nbg_ring_post_burst, clib.nbg_ring_poll, clib.nbg_ring_group, ring._r
-        nbe = 80
-        gbe = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(nbe)]
+        if not ring_res:
+            ring_res["sides"] = [torch.cuda.Stream(dev) for _ in range(RING_GROUP_STREAMS)]
+            ring_res["be"] = [torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(80)]
+            ring_res["perm"] = [torch.empty(BATCH, dtype=torch.uint32, device=dev) for _ in range(RING_GROUP_STREAMS)]
+            ring_res["cnt"] = [torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)
+                               for _ in range(RING_GROUP_STREAMS)]
+        sides, gbe = ring_res["sides"], ring_res["be"]
         # whole batches, or (C4) the 8 contiguous shards of each batch: 64 distinct inputs
         gpk = list(pk) if n == BATCH else [p + q * n * SLOT for p in pk for q in range(8)]
-        sides = [torch.cuda.Stream(dev) for _ in range(RING_GROUP_STREAMS)]
         slots = nb._lib.NBG_RING_SLOTS
-        per = len(gpk) * nbe // int(np.gcd(len(gpk), nbe))
+        per = len(gpk) * len(gbe) // int(np.gcd(len(gpk), len(gbe)))
         arr = (NbgRingBatch * (per + slots))()
         for i in range(per + slots):
-            arr[i] = NbgRingBatch(gpk[i % len(gpk)], n, gbe[i % nbe].data_ptr())
+            arr[i] = NbgRingBatch(gpk[i % len(gpk)], n, gbe[i % len(gbe)].data_ptr())
         esz, base_addr = C.sizeof(NbgRingBatch), C.addressof(arr)
         k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
         sps = [C.c_void_p(x.cuda_stream) for x in sides]
-        # one perm / counts set per side stream (each stream's groups run in its order)
-        gperm = [torch.empty(n, dtype=torch.uint32, device=dev) for _ in sides]
-        gcnt = [torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev) for _ in sides]
-        pps = [C.c_void_p(x.data_ptr()) for x in gperm]
-        cps = [C.c_void_p(x.data_ptr()) for x in gcnt]
+        pps = [C.c_void_p(x.data_ptr()) for x in ring_res["perm"]]
+        cps = [C.c_void_p(x.data_ptr()) for x in ring_res["cnt"]]
+        burst, poll, grp = clib.nbg_ring_post_burst, clib.nbg_ring_poll, clib.nbg_ring_group
+        t0 = time.perf_counter()
+        ring = mgs[0].ring(swap_macs=True, stream=streams[0])
+        rr = ring._r
         try:
-            t0 = time.perf_counter()
             posted = grouped = 0
             while grouped < batches:
                 # a batch's slot (and record) is reused only once it is grouped
@@ -740,18 +767,47 @@ def run_rank(args) -> None:
                     if grp(rr, grouped, pps[q], cps[q], sps[q]):
                         raise RuntimeError(f"nbg_ring_group: {nb._lib.last_error()}")
                     grouped += 1
-            for x in sides:
-                x.synchronize()
-            wall = time.perf_counter() - t0
         finally:
             ring.stop()
+        for x in sides:
+            x.synchronize()
+        wall = time.perf_counter() - t0
+        kms = C.c_float()
+        if clib.nbg_ring_kernel_ms(mgs[0]._h, C.byref(kms)):
+            raise RuntimeError(f"nbg_ring_kernel_ms: {nb._lib.last_error()}")
+        return wall, float(kms.value)
+
+    def ring_grouped(batches):
+        """variants.ring_in_place_grouped: ring_path over `batches` batches (the ring's buffers warmed
+        by a first short run), whole-job wall time and the ring kernel's own time."""
+        ring_path(2 * BATCHES_PER_STEP)
+        wall, kms = ring_path(batches)
         us = wall / batches * 1e6
-        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
-                "pkts_per_batch": n, "path_bytes_per_pkt": PATH_BYTES["in_place"], "group_streams": len(sides),
-                "frac": round(n * PATH_BYTES["in_place"] / us / 1e3 / HBM_PEAK_GBPS, 4),
+        ach = batches * BATCH * CLASSIFY_BYTES["in_place"] / (kms * 1e-3) / 1e9
+        return {"value": round(BATCH / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
+                "path_bytes_per_pkt": PATH_BYTES["in_place"], "group_streams": RING_GROUP_STREAMS,
+                "ring_kernel_us": round(kms * 1e3, 1), "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
                 "what": "C2 in place + grouping on the persistent ring: RX bursts posted to the resident classify "
-                        "kernel, each completed batch grouped at once by nbg_ring_group (hist + group launches on a "
-                        "side stream, co-running with the ring); whole-job wall time incl. the ring's ramp"}
+                        "kernel, each completed batch grouped at once by nbg_ring_group (hist + group launches on "
+                        "side streams, co-running with the ring); whole-job wall time incl. ring start/stop; frac "
+                        "from the ring kernel's HIP-event time (one launch for all batches)"}
+
+    def timed_ring(steps, warmup, barrier=False):
+        """The headline on the ring: `steps` rotations (steps x 8 batches) through ring_path, bracketed
+        by a barrier + device synchronisation (the ring is started and stopped inside the bracket);
+        warmed first by `warmup` rotations (the ring's buffers allocated, every input touched)."""
+        ring_path(max(1, warmup) * BATCHES_PER_STEP)
+        if barrier and world > 1:
+            dist.barrier()
+        sync_all()
+        t_start = time.perf_counter()
+        _, kms = ring_path(steps * BATCHES_PER_STEP)
+        sync_all()
+        el = time.perf_counter() - t_start
+        if barrier and world > 1:
+            dist.barrier()
+        mgs[0].check()
+        return el, kms
 
     # ---- configs C3 / C5 (IMIX descriptors): handles, traces and one call per batch
     imix = {}
@@ -858,6 +914,9 @@ def run_rank(args) -> None:
                     mcall(i, v, st)
                 sync_all()
                 mgs[0].check()
+        # then one ring run: the ring alone (the profiler may serialise dispatches, so no grouping
+        # launches beside it)
+        ring_pass("in_place", PMC_RING_BATCHES)
         return
 
     if args.multi_only:  # profiling run: only the multi-batch passes
@@ -865,15 +924,33 @@ def run_rank(args) -> None:
                           for v in ("read_only", "in_place")}), flush=True)
         return
 
-    # ---- timed region: K steps over all streams, bracketed by barrier + synchronize, max over ranks
-    elapsed_rank = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
+    # ---- timed region: K steps, bracketed by barrier + synchronize, max over ranks.  The headline
+    #      path is one launch per batch on S streams; --ring-headline makes it the persistent ring with
+    #      per-batch grouping (ring_path; measured slower for runs of a few hundred batches: the ring's
+    #      per-batch time drifts down over ~1,000 batches).
+    headline = "ring" if gpu and args.ring_headline else "launch"
+    ring_kms = None
+    if headline == "ring":
+        try:
+            elapsed_rank, ring_kms = timed_ring(args.steps, args.warmup, barrier=True)
+        except Exception as e:  # noqa: BLE001
+            if world > 1:
+                raise  # ranks must agree on the path: fail the job
+            log(f"ring headline failed; the launch path is the headline: {e}")
+            headline = f"launch (the ring failed: {str(e)[:200]})"
+    if headline != "ring":
+        elapsed_rank = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
     per_rank_s = gather_floats(elapsed_rank)
     elapsed = max(per_rank_s)
+    kms_max = max(gather_floats(ring_kms if ring_kms is not None else 0.0))
     # the same measurement at >= 50 steps (400 batches), in the same line: the K-step value is the
     # steady-state rate when the two agree
     steady = None
     if gpu and args.steady_steps > 0:
-        st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=False, barrier=True)))
+        if headline == "ring":
+            st_el = max(gather_floats(timed_ring(args.steady_steps, 1, barrier=True)[0]))
+        else:
+            st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=False, barrier=True)))
         steady = {"steps": args.steady_steps,
                   "value": round(BATCH * BATCHES_PER_STEP * args.steady_steps * world / st_el / 1e6, 1),
                   "ms_per_step": round(st_el / args.steady_steps * 1e3, 5)}
@@ -924,6 +1001,14 @@ def run_rank(args) -> None:
     if gpu:
         launches = args.steps * BATCHES_PER_STEP
         roof = kernel_pass("in_place", launches, lag=False)
+        if world == 1 and not args.no_variants and headline == "ring":
+            el = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
+            variants["launch_in_place"] = {
+                "value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
+                "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5), "streams": S, **roof,
+                "what": "the same path (C2 in place + grouping) with one streaming-classify launch + one group "
+                        "launch per 1M batch, round-robin on S streams (the round-1/2 headline); frac from the "
+                        "classify launch timed alone on one stream (HIP events)"}
         if world == 1 and not args.no_variants:
             el = timed("in_place", args.steps, args.warmup, lag=True)
             variants["in_place_lag"] = {
@@ -957,9 +1042,10 @@ def run_rank(args) -> None:
                 kb = max(args.steps * BATCHES_PER_STEP, 1024)
                 ring_runs = [("ring_read_only", lambda: ring_pass("read_only", kb)),
                              ("ring_in_place", lambda: ring_pass("in_place", kb)),
-                             ("ring_in_place_grouped", lambda: ring_group_pass(kb)),
                              # C4's per-GPU shard on the ring: 131,072-packet batches, no launch per shard
                              ("c4_shard_ring", lambda: ring_pass("in_place", 4096, n=C4_SHARD))]
+                if headline != "ring":
+                    ring_runs.append(("ring_in_place_grouped", lambda: ring_grouped(kb)))
                 for name, fn in ring_runs:
                     try:  # a ring variant that fails is reported in the line, beside the other figures
                         variants[name] = fn()
@@ -1009,7 +1095,12 @@ def run_rank(args) -> None:
                                    "1M-packet device-resident batch per GPU",
                        "backends": N_BACKENDS, "table_size": TABLE, "batch_pkts": BATCH, "slot_bytes": SLOT,
                        "frame_bytes": FRAME, "rotating_batches": N_BATCHES, "batches_per_step": BATCHES_PER_STEP,
-                       "mac_swap": "in place", "group_by": "perm + counts (group launch per batch)",
+                       "mac_swap": "in place",
+                       "group_by": ("perm + counts: nbg_ring_group (hist + group launches) per completed batch on "
+                                    f"{RING_GROUP_STREAMS} side streams" if headline == "ring"
+                                    else "perm + counts (group launch per batch)"),
+                       "path": ("persistent RX ring (nbg_ring_*): one resident classify kernel per GPU fed RX bursts"
+                                if headline == "ring" else headline),
                        "streams": S, "parallelism": f"shard{world}"},
             "per_gpu_mpps": [round(BATCH * BATCHES_PER_STEP * args.steps / s / 1e6, 1) for s in per_rank_s],
             "lut_digest": digest,
@@ -1021,7 +1112,24 @@ def run_rank(args) -> None:
         if steady is not None:
             steady["ratio"] = round(line["value"] / steady["value"], 4)
             line["steady_state"] = steady
-        if roof is not None:
+        if headline == "ring" and kms_max > 0:
+            nbt = args.steps * BATCHES_PER_STEP
+            bpp = CLASSIFY_BYTES["in_place"]
+            ach = nbt * BATCH * bpp / (kms_max * 1e-3) / 1e9
+            line["roofline"] = {
+                "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "kernel": "classify_ring_kernel<true, 1> (persistent RX ring: LUT staged in LDS once, LDS-DMA tile "
+                          "ring across batches, relay block for the descriptors)",
+                "bytes_per_pkt": bpp, "pkts_per_launch": nbt * BATCH, "batches_per_launch": nbt,
+                "avg_launch_us": round(kms_max * 1e3, 2), "us_per_batch": round(kms_max * 1e3 / nbt, 3),
+                "timing": "HIP events on the ring kernel's stream around its one launch in the timed region "
+                          "(nbg_ring_kernel_ms, max over ranks): that launch classifies all steps x 8 batches, its "
+                          "ramp and drain included",
+                "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts): physical traffic "
+                        "~1.7x the 78 algorithmic bytes (DESIGN.md section 5); variants.launch_in_place is the "
+                        "launch-per-batch path and its classify kernel's roofline"}
+        elif roof is not None:
             line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": roof["frac"], "traffic": None,
                                 "kernel": "classify_stream_kernel<F4,HIST,in place> (LDS LUT, LDS-DMA tile ring)",
@@ -1076,6 +1184,8 @@ def parse_args(argv):
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-batch variants")
     ap.add_argument("--no-imix", action="store_true", help="skip configs C3 / C5")
     ap.add_argument("--no-ring", action="store_true", help="skip the persistent-ring variants")
+    ap.add_argument("--ring-headline", action="store_true",
+                    help="headline = the persistent ring with per-batch grouping instead of one launch per batch")
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")

@@ -218,6 +218,10 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);
 int nbg_ring_stop(nbg_ring* r);
+/* The duration of the handle's last ring kernel (HIP events on its stream: start to end), valid after
+ * nbg_ring_stop.  A stopped ring's buffers and stream are kept by the handle for its next
+ * nbg_ring_start (freed by nbg_maglev_destroy). */
+int nbg_ring_kernel_ms(nbg_maglev* h, float* ms);
 
 /* Launch the grouping kernel of the last classify call made with NBG_DEFER_GROUP (or the pending
  * group of the last NBG_GROUP_LAG call) on `stream`; a stream other than the handle's last one is

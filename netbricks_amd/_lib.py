@@ -74,6 +74,7 @@ SIGNATURES = {
     "nbg_ring_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "nbg_ring_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
     "nbg_ring_stop": (C.c_int, [_P]),
+    "nbg_ring_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_float)]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_maglev_host_submit": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, C.POINTER(C.c_uint64)]),

@@ -91,6 +91,8 @@ struct nbg_maglev {
   uint32_t lag_idx = 0;
   uint32_t lag_dirty = 0;             // bit k: set k may hold counts (zeroed before it is accumulated into)
   nbg_ring* ring = nullptr;           // the running persistent ring (nbg_ring_start), if any
+  nbg_ring* ring_spare = nullptr;     // a stopped ring's buffers and stream, kept for the next start
+  float ring_kernel_ms = -1.f;        // the last ring kernel's duration (HIP events), after its stop
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
   bool issued = false;                // a launch has been issued on last_stream
   hipEvent_t order_ev = nullptr;      // cross-stream ordering of consecutive calls (order_after_last)
@@ -215,6 +217,8 @@ int order_after_last(nbg_maglev* h, hipStream_t s) {
   NBG_HIP(hipStreamWaitEvent(s, h->order_ev, 0));
   return NBG_OK;
 }
+
+void ring_free(nbg_ring* r);  // the persistent ring's resources (below)
 
 void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_idx);
@@ -490,6 +494,11 @@ int nbg_maglev_create_from_lut(const uint16_t* lut, uint64_t table_size, uint32_
 void nbg_maglev_destroy(nbg_maglev* h) {
   if (!h) return;
   if (h->ring) (void)nbg_ring_stop(h->ring);
+  if (h->ring_spare) {
+    DeviceGuard g(h->device);
+    ring_free(h->ring_spare);
+    h->ring_spare = nullptr;
+  }
   {
     DeviceGuard g(h->device);
     free_scratch(h);
@@ -1101,6 +1110,8 @@ int nbg_maglev_check(nbg_maglev* h) {
 struct nbg_ring {
   nbg_maglev* h = nullptr;
   hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
+  hipEvent_t ev_start = nullptr, ev_end = nullptr;  // around the kernel on `stream` (its duration)
+  size_t hbytes = 0, dbytes = 0;       // the pinned host ring and the uncached device ring
   uint8_t* host = nullptr;             // pinned, mapped: RingCtl | RingDesc[slots]
   uint8_t* dev = nullptr;              // uncached HBM: stop word (own line) | prog[grid] | RingDesc[reps][slots]
   volatile RingCtl* ctl = nullptr;
@@ -1179,7 +1190,61 @@ void ring_free(nbg_ring* r) {
   if (r->host) (void)hipHostFree(r->host);
   if (r->dev) (void)hipFree(r->dev);
   if (r->stream) (void)hipStreamDestroy(r->stream);
+  if (r->ev_start) (void)hipEventDestroy(r->ev_start);
+  if (r->ev_end) (void)hipEventDestroy(r->ev_end);
   delete r;
+}
+
+// The ring's buffers, private stream and events (nbg_ring_start keeps them across stops).
+int ring_alloc(nbg_maglev* h, nbg_ring** out) {
+  auto* r = new (std::nothrow) nbg_ring;
+  if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
+  r->h = h;
+  r->grid = h->cus - 1;  // classify blocks; one more block, on a CU of its own, is the relay
+  if (const char* e = std::getenv("NBG_RING_REPS")) {  // measurement: replicas, a power of two <= 256
+    const uint32_t v = static_cast<uint32_t>(std::atoi(e));
+    if (v && v <= 256 && (v & (v - 1)) == 0) r->reps = v;
+  }
+  // The kernel runs on a private stream of the highest priority: HIP maps streams onto at most
+  // GPU_MAX_HW_QUEUES hardware queues per priority, and work on any stream that shared the ring's
+  // queue would wait behind the resident kernel (measured: a third grouping stream did, until the
+  // ring's idle exit).
+  int least = 0, greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+    r->stream = nullptr;
+    ring_free(r);
+    return set_error(NBG_EIO, "ring_start: private stream");
+  }
+  if (hipEventCreate(&r->ev_start) != hipSuccess || hipEventCreate(&r->ev_end) != hipSuccess) {
+    ring_free(r);
+    return set_error(NBG_EIO, "ring_start: events");
+  }
+  r->hbytes = sizeof(RingCtl) + static_cast<size_t>(r->slots) * sizeof(RingDesc);
+  const size_t prog_off = 64, desc_off = prog_off + ((static_cast<size_t>(r->grid) * 4u + 63u) & ~size_t{63});
+  r->dbytes = desc_off + static_cast<size_t>(r->reps) * r->slots * sizeof(RingDesc);
+  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), r->hbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipSuccess) {
+    r->host = nullptr;
+    ring_free(r);
+    return set_error(NBG_ENOMEM, "ring_start: pinned ring of %zu B", r->hbytes);
+  }
+  r->ctl = reinterpret_cast<RingCtl*>(r->host);
+  r->desc = reinterpret_cast<RingDesc*>(r->host + sizeof(RingCtl));
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&r->dev), r->dbytes, hipDeviceMallocUncached) != hipSuccess) {
+    r->dev = nullptr;
+    ring_free(r);
+    return set_error(NBG_ENOMEM, "ring_start: uncached device ring of %zu B", r->dbytes);
+  }
+  const size_t nbins = static_cast<size_t>(h->nb) + 1;
+  for (auto& g : r->gsets)
+    if (hipMalloc(&g.rows, kMaxParts * nbins * 4) != hipSuccess ||
+        hipMalloc(&g.prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&g.totals, nbins * 4) != hipSuccess) {
+      ring_free(r);
+      return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
+    }
+  *out = r;
+  return NBG_OK;
 }
 
 }  // namespace
@@ -1201,69 +1266,34 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   hipStream_t s = static_cast<hipStream_t>(stream);
   int rc = order_after_last(h, s);  // the ring runs after the handle's earlier work
   if (rc) return rc;
-  auto* r = new (std::nothrow) nbg_ring;
-  if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
-  r->h = h;
-  r->grid = h->cus - 1;  // classify blocks; one more block, on a CU of its own, is the relay
-  // The kernel runs on a private stream of the highest priority: HIP maps streams onto at most
-  // GPU_MAX_HW_QUEUES hardware queues per priority, and work on any stream that shared the ring's
-  // queue would wait behind the resident kernel (measured: a third grouping stream did, until the
-  // ring's idle exit).  It starts after everything issued on `stream` so far.
+  // a stopped ring's buffers, stream and events are reused (a start then costs a memset and a launch)
+  nbg_ring* r = h->ring_spare;
+  h->ring_spare = nullptr;
+  if (!r && (rc = ring_alloc(h, &r))) return rc;
+  r->idle_ms = idle_ms ? idle_ms : 2000u;
+  r->moved = Clock::now();
+  r->posted = r->units = r->completed = 0;
+  r->ended = false;
+  r->rec.assign(r->slots, {nullptr, 0});
+  std::memset(r->host, 0, r->hbytes);
   {
-    int least = 0, greatest = 0;
-    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    // after everything issued on `stream` so far, in the private stream's order: zero the device
+    // ring, then the kernel
     hipEvent_t ev = nullptr;
-    if (hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
-      r->stream = nullptr;
-      ring_free(r);
-      return set_error(NBG_EIO, "ring_start: private stream");
-    }
     const bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
-                    hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent(r->stream, ev, 0) == hipSuccess;
+                    hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent(r->stream, ev, 0) == hipSuccess &&
+                    hipMemsetAsync(r->dev, 0, r->dbytes, r->stream) == hipSuccess;
     if (ev) (void)hipEventDestroy(ev);
     if (!ok) {
       ring_free(r);
       return set_error(NBG_EIO, "ring_start: ordering after the caller's stream");
     }
   }
-  r->idle_ms = idle_ms ? idle_ms : 2000u;
-  r->moved = Clock::now();
-  if (const char* e = std::getenv("NBG_RING_REPS")) {  // measurement: replicas, a power of two <= 256
-    const uint32_t v = static_cast<uint32_t>(std::atoi(e));
-    if (v && v <= 256 && (v & (v - 1)) == 0) r->reps = v;
-  }
-  const size_t hbytes = sizeof(RingCtl) + static_cast<size_t>(r->slots) * sizeof(RingDesc);
   const size_t prog_off = 64, desc_off = prog_off + ((static_cast<size_t>(r->grid) * 4u + 63u) & ~size_t{63});
-  const size_t dbytes = desc_off + static_cast<size_t>(r->reps) * r->slots * sizeof(RingDesc);
   uint8_t* hdev = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), hbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
-          hipSuccess ||
-      hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess) {
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess) {
     ring_free(r);
-    return set_error(NBG_ENOMEM, "ring_start: pinned ring of %zu B", hbytes);
-  }
-  std::memset(r->host, 0, hbytes);
-  r->ctl = reinterpret_cast<RingCtl*>(r->host);
-  r->desc = reinterpret_cast<RingDesc*>(r->host + sizeof(RingCtl));
-  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&r->dev), dbytes, hipDeviceMallocUncached) != hipSuccess) {
-    ring_free(r);
-    return set_error(NBG_ENOMEM, "ring_start: uncached device ring of %zu B", dbytes);
-  }
-  const size_t nbins = static_cast<size_t>(h->nb) + 1;
-  r->rec.assign(r->slots, {nullptr, 0});
-  for (auto& g : r->gsets)
-    if (hipMalloc(&g.rows, kMaxParts * nbins * 4) != hipSuccess ||
-        hipMalloc(&g.prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&g.totals, nbins * 4) != hipSuccess) {
-      ring_free(r);
-      return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
-    }
-  {
-    SetupStream st;
-    (void)st.zero(r->dev, dbytes);
-    if (st.finish() != hipSuccess) {
-      ring_free(r);
-      return set_error(NBG_EIO, "ring_start: zeroing the device ring");
-    }
+    return set_error(NBG_EIO, "ring_start: device address of the pinned ring");
   }
   ClassifyArgs a{};
   a.stride = stride;
@@ -1290,10 +1320,13 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
   const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
   ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
+  (void)hipEventRecord(r->ev_start, r->stream);
   if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, r->stream))) {
     ring_free(r);
     return rc;
   }
+  (void)hipEventRecord(r->ev_end, r->stream);
+  h->ring_kernel_ms = -1.f;
   h->ring = r;
   h->last_stream = s;
   h->issued = true;
@@ -1463,6 +1496,13 @@ int nbg_debug_ring_ctl(nbg_ring* r, uint32_t* out) {
   return NBG_OK;
 }
 
+int nbg_ring_kernel_ms(nbg_maglev* h, float* ms) {
+  if (!h || !ms) return set_error(NBG_EINVAL, "ring_kernel_ms: null argument");
+  if (h->ring_kernel_ms < 0.f) return set_error(NBG_EINVAL, "ring_kernel_ms: no stopped ring on this handle");
+  *ms = h->ring_kernel_ms;
+  return NBG_OK;
+}
+
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
   if (!r || !completed) return set_error(NBG_EINVAL, "ring_poll: null argument");
   ring_refresh(r);
@@ -1508,8 +1548,23 @@ int nbg_ring_stop(nbg_ring* r) {
   ring_refresh(r);
   if (e != hipSuccess) rc = set_error(NBG_EIO, "ring_stop: %s", hipGetErrorString(e));
   else if (r->completed < r->posted) rc = ring_state_error(r);
-  r->h->ring = nullptr;
-  ring_free(r);
+  nbg_maglev* h = r->h;
+  h->ring = nullptr;
+  float ms = -1.f;
+  if (e == hipSuccess && hipEventElapsedTime(&ms, r->ev_start, r->ev_end) == hipSuccess) h->ring_kernel_ms = ms;
+  if (e != hipSuccess) {
+    ring_free(r);
+    return rc;
+  }
+  // keep the buffers, stream and events for the next start; the grouping streams' work on the
+  // scratch is finished first
+  for (auto& g : r->gsets) {
+    if (g.s) (void)hipStreamSynchronize(g.s);
+    g.s = nullptr;
+    g.used = 0;
+  }
+  r->gcalls = 0;
+  h->ring_spare = r;
   return rc;
 }
 
