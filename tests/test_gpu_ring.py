@@ -177,6 +177,18 @@ def test_ring_post_while_running(torch_cuda):
         ring.stop()
     for i in range(6):
         np.testing.assert_array_equal(_got(torch, outs[i]), _expect(bufs[i], n, lut, False)[0])
+    import ctypes as C
+
+    from netbricks_amd._lib import lib
+
+    ms = C.c_float()
+    assert lib.nbg_ring_kernel_ms(mg._h, C.byref(ms)) == 0 and ms.value > 0  # the kernel's HIP-event time
+    # a second and third ring reuse the handle's ring buffers and stream
+    for rep in range(2):
+        outs[0].zero_()
+        with mg.ring(swap_macs=False) as ring:
+            ring.wait(ring.post(d[0], n, outs[0]))
+        np.testing.assert_array_equal(_got(torch, outs[0]), _expect(bufs[0], n, lut, False)[0], err_msg=f"rerun {rep}")
     r = mg.group_by(d[0], n, swap_macs=False)  # the handle after the ring
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_got(torch, r.backend), _expect(bufs[0], n, lut, False)[0])
