@@ -59,7 +59,7 @@ BATCHES_PER_STEP = N_BATCHES
 C4_SHARD = BATCH // 8   # config C4: a 1M batch in 8 contiguous shards, one per GPU
 IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the MALL)
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
-# flight); the environment overrides are for sweeps (tools/gpu_multi_sweep.sh)
+# flight); the environment overrides are for sweeps (tools/runs/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
 RING_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_RING_GROUP_STREAMS", "2"))  # side streams grouping ring batches
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))

@@ -691,7 +691,7 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
 }
 
 // The same with the streaming (non-temporal) policy, for packet windows (read once).  Measured on
-// classify_stream_kernel, 1M packets, one MI355X (tools/gpu_ab_ms.sh, profiles/r02_tile_nt_ab.txt):
+// classify_stream_kernel, 1M packets, one MI355X (tools/runs/gpu_ab_ms.sh, profiles/r02_tile_nt_ab.txt):
 // one stream, read-only 14.6 -> 13.5 us, in place 27.5 -> 25.5, records 17.0 -> 16.6; three streams
 // with grouping, read-only 16.1 -> 15.8, in place neutral, records 17.8 -> 18.9 (slower).  So nt for
 // read-only and in place (NT = true), the default policy for records.  The LUT pieces keep the

@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 9
 R0="$GRAFT_REPO_ROOT"
 bash tools/gpu_suite.sh || exit $?
-bash tools/gpu_bench_multi.sh || exit $?
+bash tools/runs/gpu_bench_multi.sh || exit $?
 python tools/ktrace_last.py gpurun_out/prof/multi/run_kernel_trace.csv 50
 cd "$R0"
 for L in tools/ab/lib_*.so; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3: cost of the lagged-grouping launch, by ablation build (NBG_LAG_ABL: 1 no prologue, 2 no
 # pieces in the unit loop, 3 neither, 4 no perm stores), two interleaved passes, one process per build.
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/r03_lag_abl.txt
 : > $O

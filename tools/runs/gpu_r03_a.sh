@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3, first GPU pass: the new lagged-grouping and C4-shard parity tests, then the whole GPU
 # suite, then the driver's bench command and a kernel-trace profile of it.
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_lag.py tests/test_gpu_c4_shards.py > gpurun_out/r03a_new_tests.log 2>&1 || { echo "new tests failed"; tail -40 gpurun_out/r03a_new_tests.log; exit 1; }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: whole GPU suite, the driver's bench command, and a kernel-trace profile of the bench.
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > gpurun_out/r03d_gpu_tests.log 2>&1 || { echo "gpu suite failed"; tail -40 gpurun_out/r03d_gpu_tests.log; exit 1; }

@@ -3,7 +3,7 @@
 # without the control wave's page touches ahead of each batch (NBG_RING_WARM), three interleaved
 # passes, one process per build (LD_LIBRARY_PATH puts the build's libnbgpu.so first); then the
 # per-wave timelines of both (SPROBE builds).
-cd "$(dirname "$0")/.." || exit 1
+cd "$(dirname "$0")/../.." || exit 1
 mkdir -p gpurun_out
 O=gpurun_out/r03_ring_ab.txt
 : > $O
