@@ -403,22 +403,28 @@ def launch(args, argv) -> int:
         log(f"bench: PMC passes {time.time() - t0:.0f}s")
         line["pmc"] = pmc
         roof = line.get("roofline", {})
-        ring_v = line.get("variants", {}).get("ring_in_place")
-        if isinstance(pmc, dict) and "ring" in pmc and isinstance(ring_v, dict) and "us_per_batch" in ring_v:
-            ring_v["traffic_per_batch"] = pmc["ring"]["hbm_bytes_per_batch"]
-            ring_v["traffic_ratio"] = pmc["ring"]["ratio"]
-        if isinstance(pmc, dict) and roof.get("kernel", "").startswith("classify_ring_kernel") and "ring" in pmc:
-            # per launch, like `achieved`: the measured bytes per batch x the timed launch's batches
-            roof["traffic"] = pmc["ring"]["hbm_bytes_per_batch"] * roof["batches_per_launch"]
-            roof["traffic_ratio"] = pmc["ring"]["ratio"]
-            if "launch_in_place" in line.get("variants", {}) and "in_place" in pmc:
-                line["variants"]["launch_in_place"]["traffic"] = pmc["in_place"]["hbm_bytes"]
-        elif isinstance(pmc, dict) and "in_place" in pmc:
-            line["roofline"]["traffic"] = pmc["in_place"]["hbm_bytes"]
-            for k, v in line.get("variants", {}).items():
+        variants = line.get("variants", {})
+        if isinstance(pmc, dict) and "in_place" in pmc:
+            for k, v in variants.items():
                 if k in pmc and isinstance(v, dict):
                     v["traffic"] = pmc[k]["hbm_bytes"]
                     v["kernel"] = pmc[k]["kernel"]
+            if isinstance(variants.get("launch_in_place"), dict):
+                variants["launch_in_place"]["traffic"] = pmc["in_place"]["hbm_bytes"]
+        ring_v = variants.get("ring_in_place")
+        if isinstance(pmc, dict) and "ring" in pmc and isinstance(ring_v, dict) and "us_per_batch" in ring_v:
+            ring_v["traffic_per_batch"] = pmc["ring"]["hbm_bytes_per_batch"]
+            ring_v["traffic_ratio"] = pmc["ring"]["ratio"]
+        if not isinstance(pmc, dict) or not roof:
+            pass
+        elif roof.get("kernel", "").startswith("classify_ring_kernel") and "ring" in pmc:
+            # per launch, like `achieved`: the measured bytes per batch x the timed launch's batches
+            roof["traffic"] = pmc["ring"]["hbm_bytes_per_batch"] * roof["batches_per_launch"]
+            roof["traffic_ratio"] = pmc["ring"]["ratio"]
+        elif roof.get("batches_per_launch", 1) > 1 and f"in_place_multi{roof['batches_per_launch']}" in pmc:
+            roof["traffic"] = pmc[f"in_place_multi{roof['batches_per_launch']}"]["hbm_bytes"]
+        elif "in_place" in pmc:
+            roof["traffic"] = pmc["in_place"]["hbm_bytes"]
     print(json.dumps(line), flush=True)
     return 0
 
@@ -596,7 +602,8 @@ def run_rank(args) -> None:
     # ---- several batches per launch (nbg_maglev_classify_device_multi): MULTI_K batches of 1M in
     #      one streaming-classify launch and one group launch, each batch with its own outputs
     m_arrs = {}
-    if gpu and world == 1 and not args.no_variants and not args.no_multi and N_BATCHES % MULTI_K == 0:
+    if gpu and N_BATCHES % MULTI_K == 0 and (args.headline == "multi" or (world == 1 and not args.no_variants
+                                                                          and not args.no_multi)):
         from netbricks_amd._lib import NbgBatch
         m_outs = [(torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
                    torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(N_BATCHES)]
@@ -652,6 +659,54 @@ def run_rank(args) -> None:
                 "what": f"{MULTI_K} batches of 1M (one per RX-queue pipeline) per launch of the streaming classify "
                         "kernel and one group launch (nbg_maglev_classify_device_multi); every batch keeps its own "
                         "backend / perm / counts; frac from the multi-batch classify launch timed alone"}
+
+    def multi_kernel(variant, calls):
+        """The multi-batch classify launch alone: one stream, HIP events around each launch (grouping
+        deferred and launched after the stop event)."""
+        st = sts[0]
+        kt = KernelTimer(calls + 1)
+        for i in range(calls + 1):
+            kt.start(i, st)
+            mcall(i, variant, st, defer=True)
+            kt.stop(i, st)
+            finish(hs[0], st)
+        sync_all()
+        c_ms = kt.ms()[1:]
+        kt.close()
+        bpp = CLASSIFY_BYTES[variant]
+        ach = MULTI_K * BATCH * bpp / (c_ms.mean() / 1e3) / 1e9
+        return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_pkt": bpp, "pkts_per_launch": MULTI_K * BATCH}
+
+    def timed_multi(steps, warmup, barrier=False):
+        """The headline with several RX queues' batches per launch: each step's 8 batches as
+        BATCHES_PER_STEP / MULTI_K calls of nbg_maglev_classify_device_multi (MULTI_K batches of 1M,
+        each with its own backend / perm / counts) round-robin on MULTI_STREAMS streams; bracketed
+        like timed()."""
+        ms = min(MULTI_STREAMS, len(m_arrs), S)
+        cps = BATCHES_PER_STEP // MULTI_K
+        for i in range(max(1, warmup) * cps):
+            mcall(i, "in_place", sts[i % ms], j=i % ms)
+        sync_all()
+        for m in mgs:
+            m.check()
+        if barrier and world > 1:
+            dist.barrier()
+        sync_all()
+        start_ev = torch.cuda.Event()
+        start_ev.record(torch.cuda.current_stream(dev))
+        for st in streams[:ms]:
+            st.wait_event(start_ev)
+        t_start = time.perf_counter()
+        for i in range(steps * cps):
+            mcall(i, "in_place", sts[i % ms], j=i % ms)
+        sync_all()
+        el = time.perf_counter() - t_start
+        if barrier and world > 1:
+            dist.barrier()
+        for m in mgs:
+            m.check()
+        return el
 
     # ---- the persistent RX ring (nbg_ring_*): one resident classify kernel fed batch descriptors
     def ring_pass(variant, batches, n=BATCH):
@@ -925,12 +980,17 @@ def run_rank(args) -> None:
         return
 
     # ---- timed region: K steps, bracketed by barrier + synchronize, max over ranks.  The headline
-    #      path is one launch per batch on S streams; --ring-headline makes it the persistent ring with
-    #      per-batch grouping (ring_path; measured slower for runs of a few hundred batches: the ring's
-    #      per-batch time drifts down over ~1,000 batches).
-    headline = "ring" if gpu and args.ring_headline else "launch"
+    #      path (--headline): MULTI_K RX queues' 1M batches per launch (default), one launch per batch
+    #      on S streams, or the persistent ring with per-batch grouping (measured slower for runs of a
+    #      few hundred batches: the ring's per-batch time drifts down over ~1,000 batches, DESIGN.md
+    #      section 4).
+    headline = args.headline if gpu else "launch"
+    if headline == "multi" and not m_arrs:
+        headline = "launch"
     ring_kms = None
-    if headline == "ring":
+    if headline == "multi":
+        elapsed_rank = timed_multi(args.steps, args.warmup, barrier=True)
+    elif headline == "ring":
         try:
             elapsed_rank, ring_kms = timed_ring(args.steps, args.warmup, barrier=True)
         except Exception as e:  # noqa: BLE001
@@ -938,7 +998,7 @@ def run_rank(args) -> None:
                 raise  # ranks must agree on the path: fail the job
             log(f"ring headline failed; the launch path is the headline: {e}")
             headline = f"launch (the ring failed: {str(e)[:200]})"
-    if headline != "ring":
+    if headline not in ("ring", "multi"):
         elapsed_rank = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
     per_rank_s = gather_floats(elapsed_rank)
     elapsed = max(per_rank_s)
@@ -949,6 +1009,8 @@ def run_rank(args) -> None:
     if gpu and args.steady_steps > 0:
         if headline == "ring":
             st_el = max(gather_floats(timed_ring(args.steady_steps, 1, barrier=True)[0]))
+        elif headline == "multi":
+            st_el = max(gather_floats(timed_multi(args.steady_steps, 1, barrier=True)))
         else:
             st_el = max(gather_floats(timed("in_place", args.steady_steps, 1, lag=False, barrier=True)))
         steady = {"steps": args.steady_steps,
@@ -997,11 +1059,12 @@ def run_rank(args) -> None:
         del recv, glob, gb, gc
 
     # ---- roofline: the headline launch timed alone; labelled variants beside (N = 1)
-    roof, variants = None, {}
+    roof, mroof, variants = None, None, {}
     if gpu:
         launches = args.steps * BATCHES_PER_STEP
         roof = kernel_pass("in_place", launches, lag=False)
-        if world == 1 and not args.no_variants and headline == "ring":
+        mroof = multi_kernel("in_place", max(launches // MULTI_K, 10)) if headline == "multi" else None
+        if world == 1 and not args.no_variants and headline in ("ring", "multi"):
             el = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
             variants["launch_in_place"] = {
                 "value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
@@ -1098,10 +1161,16 @@ def run_rank(args) -> None:
                        "mac_swap": "in place",
                        "group_by": ("perm + counts: nbg_ring_group (hist + group launches) per completed batch on "
                                     f"{RING_GROUP_STREAMS} side streams" if headline == "ring"
-                                    else "perm + counts (group launch per batch)"),
+                                    else f"perm + counts (one group launch per {MULTI_K} batches, per-batch outputs)"
+                                    if headline == "multi" else "perm + counts (group launch per batch)"),
                        "path": ("persistent RX ring (nbg_ring_*): one resident classify kernel per GPU fed RX bursts"
-                                if headline == "ring" else headline),
-                       "streams": S, "parallelism": f"shard{world}"},
+                                if headline == "ring" else
+                                f"{MULTI_K} RX queues' 1M batches per launch (nbg_maglev_classify_device_multi) on "
+                                f"{min(MULTI_STREAMS, S)} streams" if headline == "multi" else
+                                f"one launch per 1M batch on {S} streams" if headline == "launch" else headline),
+                       "batches_per_launch": MULTI_K if headline == "multi" else 1,
+                       "streams": min(MULTI_STREAMS, S) if headline == "multi" else S,
+                       "parallelism": f"shard{world}"},
             "per_gpu_mpps": [round(BATCH * BATCHES_PER_STEP * args.steps / s / 1e6, 1) for s in per_rank_s],
             "lut_digest": digest,
             "lut_digest_per_rank": digests,
@@ -1129,6 +1198,21 @@ def run_rank(args) -> None:
                 "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts): physical traffic "
                         "~1.7x the 78 algorithmic bytes (DESIGN.md section 5); variants.launch_in_place is the "
                         "launch-per-batch path and its classify kernel's roofline"}
+        elif headline == "multi" and mroof is not None:
+            line["roofline"] = {
+                "bound": "hbm", "achieved": mroof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": mroof["frac"], "traffic": None,
+                "kernel": f"classify_stream_kernel<F4,HIST,in place> over {MULTI_K} batches per launch (LDS LUT, "
+                          "LDS-DMA tile ring, per-batch partition rows)",
+                "bytes_per_pkt": mroof["bytes_per_pkt"], "pkts_per_launch": mroof["pkts_per_launch"],
+                "batches_per_launch": MULTI_K, "avg_launch_us": mroof["avg_launch_us"],
+                "us_per_batch": round(mroof["avg_launch_us"] / MULTI_K, 3),
+                "timing": "single-stream pass, HIP events around each multi-batch classify launch (grouping "
+                          "deferred); `value` is the multi-stream rate, where the grouping of one launch's batches "
+                          "overlaps the next launch's classify",
+                "note": "in place, every 64-B slot is written back whole (HBM writes whole bursts): physical traffic "
+                        "~1.7x the 78 algorithmic bytes (DESIGN.md section 5); variants.launch_in_place is one launch "
+                        "per 1M batch"}
         elif roof is not None:
             line["roofline"] = {"bound": "hbm", "achieved": roof["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": roof["frac"], "traffic": None,
@@ -1184,8 +1268,10 @@ def parse_args(argv):
     ap.add_argument("--no-multi", action="store_true", help="skip the multi-batch variants")
     ap.add_argument("--no-imix", action="store_true", help="skip configs C3 / C5")
     ap.add_argument("--no-ring", action="store_true", help="skip the persistent-ring variants")
-    ap.add_argument("--ring-headline", action="store_true",
-                    help="headline = the persistent ring with per-batch grouping instead of one launch per batch")
+    ap.add_argument("--headline", choices=("multi", "launch", "ring"), default="multi",
+                    help="headline path: multi = MULTI_K RX queues' 1M batches per launch on MULTI_STREAMS streams "
+                         "(default); launch = one launch per 1M batch on --streams streams; ring = the persistent "
+                         "ring with per-batch grouping")
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
