@@ -3,14 +3,17 @@
 
 Workload (BASELINE.json configs[1], "C2"): 65 backends, 65537-slot LUT, 1,048,576 synthetic
 64-B UDP frames (60-B frames in 64-B slots) per batch, resident in HBM, MAC swap in place.
-One step = one rotation over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache), i.e. 8
-batches, each through one `nbg_maglev_classify_device_ex` call (streaming classify launch + group
-launch) made straight through ctypes with prebuilt arguments.  Batches are issued round-robin on
-`--streams` (default 3) HIP streams, one handle per stream (NetBricks runs one pipeline per RX
-queue, scheduler/context.rs:241-255), so one batch's latency-bound grouping overlaps the next
-batch's bandwidth-bound classify; every batch of the K steps is fully classified and grouped
-between the two synchronisations.  `variants.in_place_lag` is the same with NBG_GROUP_LAG (batch
-i grouped inside batch i+1's classify launch; measured slower).
+One step = one rotation over 8 distinct batches (512 MiB > the 256 MiB Infinity Cache).  NetBricks
+runs one pipeline per RX queue (scheduler/context.rs:241-255); the headline path (--headline):
+  multi  (default) each step's 8 batches as 2 `nbg_maglev_classify_device_multi` calls of 4 RX
+         queues' 1M batches (one streaming classify launch + one group launch per call, every batch
+         with its own backend / perm / counts) round-robin on 2 streams;
+  launch one `nbg_maglev_classify_device_ex` call per batch round-robin on `--streams` (3) streams
+         (rounds 1-2's headline; also reported as variants.launch_in_place);
+  ring   the persistent RX ring (nbg_ring_*) with every completed batch grouped on side streams.
+Calls are made straight through ctypes with prebuilt arguments; every batch of the K steps is fully
+classified and grouped between the two synchronisations.  `variants.in_place_lag` is the launch
+path with NBG_GROUP_LAG (batch i grouped inside batch i+1's classify launch; slower).
 
 Process model.  `python bench.py --gpus N` is a launcher: it never touches the GPU, spawns N
 rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 in their environment),
@@ -20,12 +23,12 @@ owns its own batches (weak scaling, no data-path collective in the timed region)
 built on rank 0 and broadcast once over RCCL (setup, untimed).  `--selftest` runs the same
 launcher and rank logic on the CPU with gloo and no HIP call (the CPU test of the launcher).
 
-Roofline: the dominant kernel (the streaming classify launch) is timed with HIP events around each
-launch in a separate single-stream pass (grouping deferred past the stop event);
+Roofline: the dominant kernel (the headline path's classify launch) is timed with HIP events around
+each launch in a separate single-stream pass (grouping deferred past the stop event);
 its HBM traffic is measured in the same invocation by two rocprofv3 --pmc passes (FETCH_SIZE,
 WRITE_SIZE) of a short child run, at N = 1.  Variants beside the headline: lagged grouping,
-records / read-only, several batches per launch, config C4's per-GPU shard (131,072 packets per
-launch), and configs C3 / C5 (IMIX).
+records / read-only, several batches per launch, the persistent ring, config C4's per-GPU shard
+(131,072 packets per launch or ring batch), and configs C3 / C5 (IMIX).
 
 Prints ONE JSON line (rank 0 / the launcher; see DESIGN.md "Measurement").
 """
