@@ -353,6 +353,7 @@ class Ring:
                                  C.byref(h)), "nbg_ring_start")
         self._r = h
         self._held = {}  # ticket -> tensors the kernel reads or writes until the batch is complete
+        self._sizes = {}  # ticket -> n_pkts, for the last NBG_RING_SLOTS posts (group() checks perm)
         mg._ring = self  # Maglev.close() stops the ring first (the handle frees it otherwise)
 
     def post(self, pkts, n_pkts: int, backend) -> int:
@@ -369,7 +370,12 @@ class Ring:
         t = C.c_uint64()
         check(lib.nbg_ring_post(self._r, _ptr(pkts), n_pkts, _ptr(backend), C.byref(t)), "nbg_ring_post")
         self._held[t.value] = (pkts, backend)
+        self._remember(t.value, n_pkts)
         return t.value
+
+    def _remember(self, ticket: int, n_pkts: int) -> None:
+        self._sizes[ticket] = n_pkts
+        self._sizes.pop(ticket - _lib.NBG_RING_SLOTS, None)
 
     def post_burst(self, batches) -> tuple:
         """Post the first batches of `batches` ((pkts, n_pkts, backend) triples, an RX burst) without
@@ -392,6 +398,7 @@ class Ring:
         check(lib.nbg_ring_post_burst(self._r, arr, len(batches), C.byref(k), C.byref(t)), "nbg_ring_post_burst")
         for i in range(k.value):
             self._held[t.value + i] = (batches[i][0], batches[i][2])
+            self._remember(t.value + i, batches[i][1])
         return k.value, t.value
 
     def group(self, ticket: int, perm, counts, stream=None) -> None:
@@ -402,7 +409,7 @@ class Ring:
         if self._r is None:
             raise RuntimeError("ring: stopped")
         dev = torch.device("cuda", self._mg.device)
-        _check_dev("perm", perm, torch.uint32, 0, dev)
+        _check_dev("perm", perm, torch.uint32, self._sizes.get(ticket, 0), dev)
         _check_dev("counts", counts, torch.uint32, self._mg.n_backends + 1, dev)
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         st = st.cuda_stream if hasattr(st, "cuda_stream") else st
