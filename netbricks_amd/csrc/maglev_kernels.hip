@@ -637,6 +637,9 @@ __device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32
 #ifndef NBG_SW
 #define NBG_SW 8
 #endif
+#ifndef NBG_STREAM_WT  // 1: the streaming kernel's in-place window stores write-through (sc1) instead of nt (A/B)
+#define NBG_STREAM_WT 0
+#endif
 #ifndef NBG_SEQWAIT  // 0: the round-2 tile-count waits (A/B)
 #define NBG_SEQWAIT 1
 #endif
@@ -1198,7 +1201,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
-    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE, kRow>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE, kRow, NBG_STREAM_WT != 0>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
                                                                     p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
