@@ -11,6 +11,8 @@ runs one pipeline per RX queue (scheduler/context.rs:241-255); the headline path
   launch one `nbg_maglev_classify_device_ex` call per batch round-robin on `--streams` (3) streams
          (rounds 1-2's headline; also reported as variants.launch_in_place);
   ring   the persistent RX ring (nbg_ring_*) with every completed batch grouped on side streams.
+The headline is warmed for max(--warmup, 100) steps (about 20 ms of the path; it runs 3-6 % faster
+once the memory system has been under load that long) and the count run is in the line.
 Calls are made straight through ctypes with prebuilt arguments; every batch of the K steps is fully
 classified and grouped between the two synchronisations.  `variants.in_place_lag` is the launch
 path with NBG_GROUP_LAG (batch i grouped inside batch i+1's classify launch; slower).
@@ -64,6 +66,7 @@ IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the 
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
 # flight); the environment overrides are for sweeps (tools/runs/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
+MIN_WARM_STEPS = 100  # headline warm-up floor (steps of 8 batches)
 RING_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_RING_GROUP_STREAMS", "2"))  # side streams grouping ring batches
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
@@ -987,22 +990,25 @@ def run_rank(args) -> None:
     #      on S streams, or the persistent ring with per-batch grouping (measured slower for runs of a
     #      few hundred batches: the ring's per-batch time drifts down over ~1,000 batches, DESIGN.md
     #      section 4).
+    # the headline's warm-up: --warmup steps, but at least MIN_WARM_STEPS (the path runs ~3-6 % faster
+    # once the memory system has been under load for ~20 ms: profiles/r03_warm_ab.txt)
+    warm = max(args.warmup, MIN_WARM_STEPS) if gpu else args.warmup
     headline = args.headline if gpu else "launch"
     if headline == "multi" and not m_arrs:
         headline = "launch"
     ring_kms = None
     if headline == "multi":
-        elapsed_rank = timed_multi(args.steps, args.warmup, barrier=True)
+        elapsed_rank = timed_multi(args.steps, warm, barrier=True)
     elif headline == "ring":
         try:
-            elapsed_rank, ring_kms = timed_ring(args.steps, args.warmup, barrier=True)
+            elapsed_rank, ring_kms = timed_ring(args.steps, warm, barrier=True)
         except Exception as e:  # noqa: BLE001
             if world > 1:
                 raise  # ranks must agree on the path: fail the job
             log(f"ring headline failed; the launch path is the headline: {e}")
             headline = f"launch (the ring failed: {str(e)[:200]})"
     if headline not in ("ring", "multi"):
-        elapsed_rank = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
+        elapsed_rank = timed("in_place", args.steps, warm, lag=False, barrier=True)
     per_rank_s = gather_floats(elapsed_rank)
     elapsed = max(per_rank_s)
     kms_max = max(gather_floats(ring_kms if ring_kms is not None else 0.0))
@@ -1068,7 +1074,7 @@ def run_rank(args) -> None:
         roof = kernel_pass("in_place", launches, lag=False)
         mroof = multi_kernel("in_place", max(launches // MULTI_K, 10)) if headline == "multi" else None
         if world == 1 and not args.no_variants and headline in ("ring", "multi"):
-            el = timed("in_place", args.steps, args.warmup, lag=False, barrier=True)
+            el = timed("in_place", args.steps, warm, lag=False, barrier=True)
             variants["launch_in_place"] = {
                 "value": round(BATCH * BATCHES_PER_STEP * args.steps / el / 1e6, 1), "unit": "Mpps",
                 "ms_per_batch": round(el / (args.steps * BATCHES_PER_STEP) * 1e3, 5), "streams": S, **roof,
@@ -1150,6 +1156,7 @@ def run_rank(args) -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "ms_per_batch": round(elapsed / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
             "higher_is_better": True,
