@@ -210,6 +210,15 @@ struct SetupStream {
 // another stream, a host submit after device calls, or a caller that moves the handle between
 // streams): when the stream changes, the new stream waits for everything issued so far on the
 // previous one.  Calls that stay on one stream pay nothing.
+// Blocks of a streaming-classify launch: one per CU, or NBG_STREAM_GRID (measurement: 1..CUs).
+int stream_grid(const nbg_maglev* h) {
+  static const int forced = [] {
+    const char* e = std::getenv("NBG_STREAM_GRID");
+    return e ? std::atoi(e) : 0;
+  }();
+  return forced > 0 && forced <= h->cus ? forced : h->cus;
+}
+
 int order_after_last(nbg_maglev* h, hipStream_t s) {
   if (!h->issued || h->last_stream == s) return NBG_OK;
   if (!h->order_ev) NBG_HIP(hipEventCreateWithFlags(&h->order_ev, hipEventDisableTiming));
@@ -800,7 +809,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     if (capturing && a.part_hist)
       if ((rc = zero_captured(a.part_hist, static_cast<size_t>(n_parts) * nbins, stream))) return rc;
     if (lag) return classify_lag(h, a, fuse, n_parts, part_pkts, d_perm, d_counts, static_cast<hipStream_t>(stream));
-    rc = launch_classify_stream(a, h->cus, stream);
+    rc = launch_classify_stream(a, stream_grid(h), stream);
   } else if (d_off && d_len && a.win_owned && !lds && (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0 &&
              use_stream_desc(h, n_pkts, flags, lpm != nullptr, lpm || !a.swap ? 0 : (a.mac_out ? 2 : 1))) {
     if (!h->wide) {
@@ -995,7 +1004,7 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
   a.backend = sb.backend[0];
   h->last_stream = static_cast<hipStream_t>(stream);
   h->issued = true;
-  if ((rc = launch_classify_stream_multi(a, sb, h->cus, stream))) return rc;
+  if ((rc = launch_classify_stream_multi(a, sb, stream_grid(h), stream))) return rc;
   if (group) {
     h->mparity ^= 1u;
     gm.per = n_parts_max;
