@@ -67,6 +67,7 @@ IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the 
 # flight); the environment overrides are for sweeps (tools/runs/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
 MIN_WARM_STEPS = 100  # headline warm-up floor (steps of 8 batches)
+RING_BATCHES = 4096   # batches per ring pass (variants.ring_*)
 RING_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_RING_GROUP_STREAMS", "2"))  # side streams grouping ring batches
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
@@ -1111,9 +1112,12 @@ def run_rank(args) -> None:
                         "on the same streams; below the streaming kernel's 262,144-packet threshold, so the "
                         "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
             if not args.no_ring:
+                # the ring's per-batch time settles after ~1,000 batches: 4,096
+                # batches per ring pass, slope over the middle three quarters
                 kb = max(args.steps * BATCHES_PER_STEP, 1024)
-                ring_runs = [("ring_read_only", lambda: ring_pass("read_only", kb)),
-                             ("ring_in_place", lambda: ring_pass("in_place", kb)),
+                kr = max(args.steps * BATCHES_PER_STEP, RING_BATCHES)
+                ring_runs = [("ring_read_only", lambda: ring_pass("read_only", kr)),
+                             ("ring_in_place", lambda: ring_pass("in_place", kr)),
                              # C4's per-GPU shard on the ring: 131,072-packet batches, no launch per shard
                              ("c4_shard_ring", lambda: ring_pass("in_place", 4096, n=C4_SHARD))]
                 if headline != "ring":
@@ -1240,13 +1244,16 @@ def run_rank(args) -> None:
                                         "parse + hash + lookup"}
         if variants:
             line["variants"] = variants
-            ro = variants.get(f"read_only_multi{MULTI_K}") or variants.get("read_only")
-            if ro:  # BASELINE.json north_star: parse + hash + lookup at >= 70 % of the HBM roofline
+            cands = [k for k in (f"read_only_multi{MULTI_K}", "ring_read_only", "read_only")
+                     if isinstance(variants.get(k), dict) and "frac" in variants[k]]
+            if cands:  # BASELINE.json north_star: parse + hash + lookup at >= 70 % of the HBM roofline
+                best = max(cands, key=lambda k: variants[k]["frac"])
+                ro = variants[best]
                 line["north_star"] = {"target_frac": 0.70, "frac": float(ro["frac"]), "met": bool(ro["frac"] >= 0.70),
-                                      "variant": f"read_only_multi{MULTI_K}" if f"read_only_multi{MULTI_K}" in variants
-                                      else "read_only",
+                                      "variant": best,
                                       "single_batch_frac": variants.get("read_only", {}).get("frac"),
-                                      "ring_single_batch_frac": variants.get("ring_read_only", {}).get("frac")}
+                                      "ring_single_batch_frac": variants.get("ring_read_only", {}).get("frac"),
+                                      "multi_batch_frac": variants.get(f"read_only_multi{MULTI_K}", {}).get("frac")}
         line["cpu_baseline"] = cpu
         if scatter is not None:
             line["scatter_inclusive"] = scatter
