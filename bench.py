@@ -11,8 +11,7 @@ runs one pipeline per RX queue (scheduler/context.rs:241-255); the headline path
   launch one `nbg_maglev_classify_device_ex` call per batch round-robin on `--streams` (3) streams
          (rounds 1-2's headline; also reported as variants.launch_in_place);
   ring   the persistent RX ring (nbg_ring_*) with every completed batch grouped on side streams.
-The headline is warmed for max(--warmup, 100) steps (about 20 ms of the path; it runs 3-6 % faster
-once the memory system has been under load that long) and the count run is in the line.
+The headline runs exactly --warmup untimed steps before its K timed steps.
 Calls are made straight through ctypes with prebuilt arguments; every batch of the K steps is fully
 classified and grouped between the two synchronisations.  `variants.in_place_lag` is the launch
 path with NBG_GROUP_LAG (batch i grouped inside batch i+1's classify launch; slower).
@@ -66,9 +65,17 @@ IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the 
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
 # flight); the environment overrides are for sweeps (tools/runs/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
-MIN_WARM_STEPS = 100  # headline warm-up floor (steps of 8 batches)
 RING_BATCHES = 4096   # batches per ring pass (variants.ring_*)
 RING_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_RING_GROUP_STREAMS", "2"))  # side streams grouping ring batches
+# the ring passes' inputs: RING_ROTATE dedicated 1M batches (32 x 64 MiB = 2 GiB, 8x the 256 MiB
+# Infinity Cache, so no figure rides on cache hits), checked against pristine copies after every pass
+RING_ROTATE = int(os.environ.get("NBG_BENCH_RING_ROTATE", "32"))
+WS_SWEEP = tuple(int(x) for x in os.environ.get("NBG_BENCH_WS_SWEEP", "8,16,32").split(","))  # working-set sweep
+RING_BACKENDS = 128   # backend[] buffers a ring pass rotates over (more than the 64 slots + the grouping lag)
+RING_CHECK = 16       # the last batches of every ring pass, checked against the launch path
+RING_GROUP_BURST = int(os.environ.get("NBG_BENCH_RING_GROUP_BURST", "1"))  # 1M batches per nbg_ring_group_burst
+C4_GROUP_BURST = int(os.environ.get("NBG_BENCH_C4_GROUP_BURST", "8"))      # C4 shards per nbg_ring_group_burst
+C4_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_C4_GROUP_STREAMS", "2"))
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet of the classify kernel per variant:
@@ -86,7 +93,7 @@ PMC_WARMUP, PMC_STEPS = 10, 40
 # the child's launch sequence, one classify dispatch per call, in this order
 PMC_ORDER = ("in_place", "in_place_lag", "records", "read_only", "c4_shard", "c3", "c5")
 PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
-PMC_RING_BATCHES = 64  # then one ring run (one dispatch) of this many in-place batches
+PMC_RING_BATCHES = RING_BATCHES  # then the ring runs (one dispatch each, read only then in place), as timed
 NBG_SWAP_MACS, NBG_DEFER_GROUP, NBG_GROUP_LAG = 0x1, 0x10, 0x80
 
 
@@ -345,14 +352,18 @@ def pmc_traffic(timeout_s: int = 180):
         out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
                      "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
                      "kernel": kname.replace("void nbg::(anonymous namespace)::", "").split("(nbg::")[0]}
-    if len(rvals.get("FETCH_SIZE", [])) == 1 and len(rvals.get("WRITE_SIZE", [])) == 1:
-        # the ring: one dispatch for PMC_RING_BATCHES batches (in place, no grouping beside it)
-        rd, wr = 2.0 * rvals["FETCH_SIZE"][0], rvals["WRITE_SIZE"][0]
-        alg = PMC_RING_BATCHES * BATCH * CLASSIFY_BYTES["in_place"]
-        out["ring"] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
-                                "batches": PMC_RING_BATCHES, "hbm_bytes_per_batch": round((rd + wr) / PMC_RING_BATCHES),
-                                "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
-                                "kernel": "classify_ring_kernel<true, 1>"}
+    rf, rw = rvals.get("FETCH_SIZE", []), rvals.get("WRITE_SIZE", [])
+    if len(rf) == 2 and len(rw) == 2:
+        # the ring: one dispatch per pass (read only, then in place), RING_BATCHES batches over
+        # RING_ROTATE inputs each: the same batch count and working set as the timed passes
+        for k, (name, v) in enumerate((("ring_read_only", "read_only"), ("ring_in_place", "in_place"))):
+            rd, wr = 2.0 * rf[k], rw[k]
+            alg = PMC_RING_BATCHES * BATCH * CLASSIFY_BYTES[v]
+            out[name] = {"read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
+                         "batches": PMC_RING_BATCHES, "working_set_mib": RING_ROTATE * BATCH * SLOT >> 20,
+                         "hbm_bytes_per_batch": round((rd + wr) / PMC_RING_BATCHES),
+                         "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
+                         "kernel": f"classify_ring_kernel<true, {k}>"}
     return out
 
 
@@ -418,16 +429,20 @@ def launch(args, argv) -> int:
                     v["kernel"] = pmc[k]["kernel"]
             if isinstance(variants.get("launch_in_place"), dict):
                 variants["launch_in_place"]["traffic"] = pmc["in_place"]["hbm_bytes"]
-        ring_v = variants.get("ring_in_place")
-        if isinstance(pmc, dict) and "ring" in pmc and isinstance(ring_v, dict) and "us_per_batch" in ring_v:
-            ring_v["traffic_per_batch"] = pmc["ring"]["hbm_bytes_per_batch"]
-            ring_v["traffic_ratio"] = pmc["ring"]["ratio"]
+        for name in ("ring_read_only", "ring_in_place"):
+            ring_v = variants.get(name)
+            if isinstance(pmc, dict) and name in pmc and isinstance(ring_v, dict) and "us_per_batch" in ring_v:
+                # physical bytes per batch (PMC of the same batch count and working set) over the timed
+                # per-batch time: must stay within what HBM can move
+                ring_v["traffic_per_batch"] = pmc[name]["hbm_bytes_per_batch"]
+                ring_v["traffic_ratio"] = pmc[name]["ratio"]
+                ring_v["physical_tbps"] = round(pmc[name]["hbm_bytes_per_batch"] / ring_v["us_per_batch"] / 1e6, 2)
         if not isinstance(pmc, dict) or not roof:
             pass
-        elif roof.get("kernel", "").startswith("classify_ring_kernel") and "ring" in pmc:
+        elif roof.get("kernel", "").startswith("classify_ring_kernel") and "ring_in_place" in pmc:
             # per launch, like `achieved`: the measured bytes per batch x the timed launch's batches
-            roof["traffic"] = pmc["ring"]["hbm_bytes_per_batch"] * roof["batches_per_launch"]
-            roof["traffic_ratio"] = pmc["ring"]["ratio"]
+            roof["traffic"] = pmc["ring_in_place"]["hbm_bytes_per_batch"] * roof["batches_per_launch"]
+            roof["traffic_ratio"] = pmc["ring_in_place"]["ratio"]
         elif roof.get("batches_per_launch", 1) > 1 and f"in_place_multi{roof['batches_per_launch']}" in pmc:
             roof["traffic"] = pmc[f"in_place_multi{roof['batches_per_launch']}"]["hbm_bytes"]
         elif "in_place" in pmc:
@@ -716,22 +731,105 @@ def run_rank(args) -> None:
         return el
 
     # ---- the persistent RX ring (nbg_ring_*): one resident classify kernel fed batch descriptors
-    def ring_pass(variant, batches, n=BATCH):
-        """Per-batch time of the ring in steady state: the producer posts the rotating batches whenever
+    ring_data = {}
+
+    def ring_setup():
+        """RING_ROTATE dedicated 1M batches with pristine copies (the output check), RING_BACKENDS
+        backend[] buffers, scratch outputs for the launch-path check."""
+        if not ring_data:
+            t0 = time.time()
+            bufs, orig = [], []
+            for b in range(RING_ROTATE):
+                buf, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(rank, 100 + b))
+                bufs.append(torch.from_numpy(buf).to(dev))
+                orig.append(bufs[-1].clone())
+            ring_data.update(
+                bufs=bufs, orig=orig,
+                be=[torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(RING_BACKENDS)],
+                sbe=torch.empty(BATCH, dtype=torch.uint16, device=dev),
+                sperm=torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                scnt=torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev))
+            sync_all()
+            log(f"[rank {rank}] ring inputs ({RING_ROTATE} x 64 MiB + copies) ready in {time.time() - t0:.1f}s")
+        return ring_data
+
+    def ring_inputs(rotate, n):
+        """(buffer, shard) of every distinct input of a pass: whole batches, or (C4) each batch's
+        BATCH // n contiguous shards; post i takes input i % len."""
+        return [(w, q) for w in range(rotate) for q in range(BATCH // n)]
+
+    def ring_restore(rotate):
+        rd = ring_setup()
+        for w in range(rotate):
+            rd["bufs"][w].copy_(rd["orig"][w])
+        sync_all()
+
+    def launch_ref(pkts, n, group=False):
+        """The launch path's read-only classification of n packets at pkts (backend[], and with group
+        perm / counts) into the scratch outputs: the reference the ring's outputs are checked against."""
+        rd = ring_setup()
+        st = torch.cuda.current_stream(dev).cuda_stream
+        rc = classify(hs[0], pkts, None, None, SLOT, FRAME, n, 0, rd["sbe"].data_ptr(),
+                      rd["sperm"].data_ptr() if group else None, rd["scnt"].data_ptr() if group else None, None, st)
+        if rc:
+            raise RuntimeError(f"launch-path check classify: {rc}: {nb._lib.last_error()}")
+        sync_all()
+
+    def ring_check(swap, rotate, n, total, be_of, groups=()):
+        """What a ring run of `total` posts left behind: the backend[] of its last RING_CHECK batches
+        against the launch path's classification of the same inputs; every input buffer's bytes
+        against its pristine copy, MACs swapped iff the run swapped it an odd number of times (in
+        place) or untouched (read only); `groups`: (post, perm, counts) of groupings to check."""
+        rd = ring_setup()
+        ins = ring_inputs(rotate, n)
+        bad = []
+        for i in range(max(0, total - RING_CHECK), total):
+            w, q = ins[i % len(ins)]
+            launch_ref(rd["bufs"][w].data_ptr() + q * n * SLOT, n)
+            if not torch.equal(rd["sbe"][:n], be_of(i)[:n]):
+                bad.append(f"backend of post {i}")
+        for i, perm, cnt in groups:
+            w, q = ins[i % len(ins)]
+            launch_ref(rd["bufs"][w].data_ptr() + q * n * SLOT, n, group=True)
+            if not (torch.equal(rd["sperm"][:n], perm[:n]) and torch.equal(rd["scnt"], cnt)):
+                bad.append(f"perm/counts of post {i}")
+        times = np.bincount(np.arange(total) % len(ins), minlength=len(ins))
+        per = BATCH // n
+        for w in range(rotate):
+            exp = rd["orig"][w]
+            odd = [q for q in range(per) if swap and times[w * per + q] % 2]
+            if odd:
+                exp = exp.clone()
+                v, o = exp.view(BATCH, SLOT), rd["orig"][w].view(BATCH, SLOT)
+                for q in odd:
+                    r0, r1 = q * n, (q + 1) * n
+                    v[r0:r1, 0:6] = o[r0:r1, 6:12]
+                    v[r0:r1, 6:12] = o[r0:r1, 0:6]
+            if not torch.equal(rd["bufs"][w], exp):
+                bad.append(f"bytes of buffer {w}")
+        out = {"backend_batches": min(RING_CHECK, total), "groupings": len(groups), "buffers": rotate,
+               "ok": not bad}
+        if bad:
+            out["mismatch"] = bad[:8]
+            log(f"ring output check FAILED: {bad[:8]}")
+        return out
+
+    def ring_pass(variant, batches, n=BATCH, rotate=RING_ROTATE):
+        """Per-batch time of the ring in steady state: the producer posts the rotating inputs whenever
         a slot is free (bare ctypes, prebuilt arguments) and stamps every change of the completed
         count; the time per batch is the slope of completions over the middle three quarters of the
         run (no launch, LUT staging or ramp per batch; HIP events cannot bracket a batch inside one
-        resident kernel).  No grouping on the ring: backend[] (and the in-place swap) only."""
+        resident kernel).  No grouping: backend[] (and the in-place swap) only.  The run's outputs are
+        checked afterwards (ring_check)."""
         swap = variant == "in_place"
-        ring = mgs[0].ring(swap_macs=swap, stream=streams[0])
+        rd = ring_setup()
+        ring_restore(rotate)
         from netbricks_amd._lib import NbgRingBatch
 
-        burst, poll, rr = clib.nbg_ring_post_burst, clib.nbg_ring_poll, ring._r
-        bes = [o[par]["backend"].data_ptr() for o in outs for par in (0, 1)]
-        # whole batches, or (C4) the 8 contiguous shards of each batch: 64 distinct inputs
-        pks = list(pk) if n == BATCH else [p + s * n * SLOT for p in pk for s in range(8)]
+        bes = [b.data_ptr() for b in rd["be"]]
+        pks = [rd["bufs"][w].data_ptr() + q * n * SLOT for w, q in ring_inputs(rotate, n)]
         slots = nb._lib.NBG_RING_SLOTS
-        # the producer's descriptors, prebuilt: batch i of the run is entry i % len(arr); an RX burst
+        # the producer's descriptors, prebuilt: post i of the run is entry i % len(arr); an RX burst
         # is a window of it (nbg_ring_post_burst posts as many as there are free slots)
         per = len(pks) * len(bes) // int(np.gcd(len(pks), len(bes)))
         arr = (NbgRingBatch * (per + slots))()
@@ -740,6 +838,8 @@ def run_rank(args) -> None:
         esz = C.sizeof(NbgRingBatch)
         base_addr = C.addressof(arr)
         k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
+        ring = mgs[0].ring(swap_macs=swap, stream=streams[0])
+        burst, poll, rr = clib.nbg_ring_post_burst, clib.nbg_ring_poll, ring._r
 
         def post_upto(first, count):
             if burst(rr, C.c_void_p(base_addr + (first % per) * esz), count, C.byref(k), C.byref(tk)):
@@ -765,8 +865,14 @@ def run_rank(args) -> None:
             wall = time.perf_counter() - t0
         finally:
             ring.stop()
+        total = 16 + batches
+        check = ring_check(swap, rotate, n, total, lambda i: rd["be"][i % len(bes)])
         ts = np.array([x[0] for x in stamps])
         cs = np.array([x[1] for x in stamps])
+        if os.environ.get("NBG_BENCH_DUMP"):  # the completion stamps behind us_per_batch (profiles/)
+            fn = os.path.join(os.environ["NBG_BENCH_DUMP"], f"ring_{variant}_n{n}_rot{rotate}_b{batches}.csv")
+            np.savetxt(fn, np.stack([(ts - ts[0]) * 1e6, cs], 1), fmt="%.3f,%d", header="us_since_first,completed",
+                       comments="")
         i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
         us = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]) * 1e6)
         bpp = CLASSIFY_BYTES[variant]
@@ -774,61 +880,76 @@ def run_rank(args) -> None:
         return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
                 "wall_us_per_batch": round(wall / batches * 1e6, 2), "batches": batches, "bytes_per_pkt": bpp,
                 "pkts_per_batch": n, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "working_set_mib": rotate * BATCH * SLOT >> 20, "rotating_inputs": len(pks),
+                "output_check": check,
                 "kernel": f"classify_ring_kernel<true, {1 if swap else 0}>",
                 "what": "persistent RX ring (nbg_ring_*): one resident classify kernel (LUT staged once) takes "
-                        "1M-packet batches as the producer posts them through a pinned descriptor ring, relayed "
-                        "into HBM by the kernel's last block; per-batch time from the completion slope; "
-                        "backend[] (+ in-place MAC swap) only, no grouping"}
+                        "batches as the producer posts them through a pinned descriptor ring, relayed into HBM by "
+                        "the kernel's last block; per-batch time from the completion slope (middle 3/4 of the "
+                        "run); backend[] (+ in-place MAC swap) only, no grouping; outputs checked after the run"}
 
     ring_res = {}
 
-    def ring_path(batches, n=BATCH):
+    def ring_path(batches, n=BATCH, rotate=RING_ROTATE, gstreams=RING_GROUP_STREAMS, gburst=RING_GROUP_BURST,
+                  check=False):
         """The whole in-place path on the ring: start the ring (its buffers are kept by the handle after
-        the first start), post RX bursts, group every batch the ring completes at once (nbg_ring_group:
-        hist + group launches on RING_GROUP_STREAMS side streams, beside the resident ring kernel), wait
-        for the last group, stop the ring.  80 distinct backend[] buffers, so no batch's backend[] is
-        rewritten before its grouping ran.  Returns (wall seconds, ring kernel ms by HIP events)."""
+        the first start), post RX bursts, and enqueue each burst's grouping right away
+        (nbg_ring_group_burst: a gate kernel on the side stream waits for the batches' completion in
+        HBM, then hist + group launches co-run with the resident ring kernel) round-robin on `gstreams`
+        side streams: no host poll between completion and grouping.  A backend[] buffer is reused only
+        after the grouping that reads it has run (an event per group burst).  Waits for the last
+        grouping and stops the ring.  Returns (wall seconds, ring kernel ms, output check)."""
         from netbricks_amd._lib import NbgRingBatch
 
+        rd = ring_setup()
         if not ring_res:
-            ring_res["sides"] = [torch.cuda.Stream(dev) for _ in range(RING_GROUP_STREAMS)]
-            ring_res["be"] = [torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(80)]
-            ring_res["perm"] = [torch.empty(BATCH, dtype=torch.uint32, device=dev) for _ in range(RING_GROUP_STREAMS)]
-            ring_res["cnt"] = [torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)
-                               for _ in range(RING_GROUP_STREAMS)]
-        sides, gbe = ring_res["sides"], ring_res["be"]
-        # whole batches, or (C4) the 8 contiguous shards of each batch: 64 distinct inputs
-        gpk = list(pk) if n == BATCH else [p + q * n * SLOT for p in pk for q in range(8)]
+            ring_res["sides"] = [torch.cuda.Stream(dev) for _ in range(4)]
+            ring_res["perm"] = [[torch.empty(BATCH, dtype=torch.uint32, device=dev) for _ in range(8)]
+                                for _ in range(4)]
+            ring_res["cnt"] = [[torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev) for _ in range(8)]
+                               for _ in range(4)]
+        sides = ring_res["sides"][:gstreams]
+        nbe = len(rd["be"])
+        pks = [rd["bufs"][w].data_ptr() + q * n * SLOT for w, q in ring_inputs(rotate, n)]
         slots = nb._lib.NBG_RING_SLOTS
-        per = len(gpk) * len(gbe) // int(np.gcd(len(gpk), len(gbe)))
+        per = len(pks) * nbe // int(np.gcd(len(pks), nbe))
         arr = (NbgRingBatch * (per + slots))()
         for i in range(per + slots):
-            arr[i] = NbgRingBatch(gpk[i % len(gpk)], n, gbe[i % len(gbe)].data_ptr())
+            arr[i] = NbgRingBatch(pks[i % len(pks)], n, rd["be"][i % nbe].data_ptr())
         esz, base_addr = C.sizeof(NbgRingBatch), C.addressof(arr)
-        k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
+        k, tk = C.c_uint32(), C.c_uint64()
         sps = [C.c_void_p(x.cuda_stream) for x in sides]
-        pps = [C.c_void_p(x.data_ptr()) for x in ring_res["perm"]]
-        cps = [C.c_void_p(x.data_ptr()) for x in ring_res["cnt"]]
-        burst, poll, grp = clib.nbg_ring_post_burst, clib.nbg_ring_poll, clib.nbg_ring_group
+        pps = [(C.c_void_p * gburst)(*[p.data_ptr() for p in ring_res["perm"][q][:gburst]]) for q in range(gstreams)]
+        cps = [(C.c_void_p * gburst)(*[c.data_ptr() for c in ring_res["cnt"][q][:gburst]]) for q in range(gstreams)]
+        burst, grp = clib.nbg_ring_post_burst, clib.nbg_ring_group_burst
+        evs = {}  # first post of a group burst -> (event after it on its side stream, posts in it)
+        last_on = [None] * gstreams  # (first post, count) of the last burst grouped on each side stream
+        if check:
+            ring_restore(rotate)
         t0 = time.perf_counter()
         ring = mgs[0].ring(swap_macs=True, stream=streams[0])
         rr = ring._r
         try:
-            posted = grouped = 0
+            posted = grouped = safe = 0  # safe: every grouping of posts < safe has run
             while grouped < batches:
-                # a batch's slot (and record) is reused only once it is grouped
-                room = min(batches - posted, grouped + slots - posted)
-                if room > 0:
-                    if burst(rr, C.c_void_p(base_addr + (posted % per) * esz), room, C.byref(k), C.byref(tk)):
-                        raise RuntimeError(f"nbg_ring_post_burst: {nb._lib.last_error()}")
-                    posted += k.value
-                if poll(rr, C.byref(cc)):
-                    raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
-                while grouped < cc.value:
-                    q = grouped % len(sides)
-                    if grp(rr, grouped, pps[q], cps[q], sps[q]):
-                        raise RuntimeError(f"nbg_ring_group: {nb._lib.last_error()}")
-                    grouped += 1
+                want = min(batches - posted, slots, safe + nbe - posted)
+                if want <= 0:  # the backend[] buffers of the next posts still wait for their grouping
+                    while safe in evs and evs[safe][0].query():
+                        safe += evs.pop(safe)[1]
+                    continue
+                if burst(rr, C.c_void_p(base_addr + (posted % per) * esz), want, C.byref(k), C.byref(tk)):
+                    raise RuntimeError(f"nbg_ring_post_burst: {nb._lib.last_error()}")
+                posted += k.value
+                while grouped + gburst <= posted or (grouped < posted and posted == batches):
+                    cnt = min(gburst, posted - grouped)
+                    q = (grouped // gburst) % gstreams
+                    if grp(rr, grouped, cnt, pps[q], cps[q], sps[q]):
+                        raise RuntimeError(f"nbg_ring_group_burst: {nb._lib.last_error()}")
+                    ev = torch.cuda.Event()
+                    ev.record(sides[q])
+                    evs[grouped] = (ev, cnt)
+                    last_on[q] = (grouped, cnt)
+                    grouped += cnt
         finally:
             ring.stop()
         for x in sides:
@@ -837,22 +958,33 @@ def run_rank(args) -> None:
         kms = C.c_float()
         if clib.nbg_ring_kernel_ms(mgs[0]._h, C.byref(kms)):
             raise RuntimeError(f"nbg_ring_kernel_ms: {nb._lib.last_error()}")
-        return wall, float(kms.value)
+        out_check = None
+        if check:
+            groups = [(f + j, ring_res["perm"][q][j], ring_res["cnt"][q][j])
+                      for q, lo in enumerate(last_on) if lo is not None for f, c in [lo] for j in range(c)]
+            out_check = ring_check(True, rotate, n, batches, lambda i: rd["be"][i % nbe], groups)
+        return wall, float(kms.value), out_check
 
-    def ring_grouped(batches):
-        """variants.ring_in_place_grouped: ring_path over `batches` batches (the ring's buffers warmed
-        by a first short run), whole-job wall time and the ring kernel's own time."""
-        ring_path(2 * BATCHES_PER_STEP)
-        wall, kms = ring_path(batches)
+    def ring_grouped(batches, n=BATCH, gstreams=RING_GROUP_STREAMS, gburst=RING_GROUP_BURST):
+        """variants.ring_in_place_grouped / c4_shard_ring_grouped: ring_path over `batches` batches (the
+        ring's buffers warmed by a first short run), whole-job wall time, the ring kernel's own time and
+        the output check of the timed run."""
+        ring_path(2 * BATCHES_PER_STEP, n=n, gstreams=gstreams, gburst=gburst)
+        wall, kms, chk = ring_path(batches, n=n, gstreams=gstreams, gburst=gburst, check=True)
         us = wall / batches * 1e6
-        ach = batches * BATCH * CLASSIFY_BYTES["in_place"] / (kms * 1e-3) / 1e9
-        return {"value": round(BATCH / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
-                "path_bytes_per_pkt": PATH_BYTES["in_place"], "group_streams": RING_GROUP_STREAMS,
+        ach_path = n * PATH_BYTES["in_place"] / us / 1e3
+        ach = batches * n * CLASSIFY_BYTES["in_place"] / (kms * 1e-3) / 1e9
+        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
+                "pkts_per_batch": n, "path_bytes_per_pkt": PATH_BYTES["in_place"],
+                "path_frac": round(ach_path / HBM_PEAK_GBPS, 4),
+                "group_streams": gstreams, "group_burst": gburst, "working_set_mib": RING_ROTATE * BATCH * SLOT >> 20,
                 "ring_kernel_us": round(kms * 1e3, 1), "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                "what": "C2 in place + grouping on the persistent ring: RX bursts posted to the resident classify "
-                        "kernel, each completed batch grouped at once by nbg_ring_group (hist + group launches on "
-                        "side streams, co-running with the ring); whole-job wall time incl. ring start/stop; frac "
-                        "from the ring kernel's HIP-event time (one launch for all batches)"}
+                "output_check": chk,
+                "what": "in place + grouping on the persistent ring: RX bursts posted to the resident classify kernel, "
+                        "each burst's grouping enqueued right after the post (nbg_ring_group_burst: a gate kernel "
+                        "waits on the side stream for the batches' completion word in HBM, then hist + group co-run "
+                        "with the ring), no host poll; whole-job wall time incl. ring start/stop (path_frac at 82 "
+                        "B/pkt); frac from the ring kernel's HIP-event time"}
 
     def timed_ring(steps, warmup, barrier=False):
         """The headline on the ring: `steps` rotations (steps x 8 batches) through ring_path, bracketed
@@ -863,13 +995,174 @@ def run_rank(args) -> None:
             dist.barrier()
         sync_all()
         t_start = time.perf_counter()
-        _, kms = ring_path(steps * BATCHES_PER_STEP)
+        _, kms, _ = ring_path(steps * BATCHES_PER_STEP)
         sync_all()
         el = time.perf_counter() - t_start
         if barrier and world > 1:
             dist.barrier()
         mgs[0].check()
         return el, kms
+
+    def multi_rot_kernel(variant, rotate, calls):
+        """The multi-batch classify launch alone (HIP events, grouping deferred) over the ring's inputs
+        rotated through `rotate` batches (MULTI_K per launch): the working-set sweep's launch path."""
+        from netbricks_amd._lib import NbgBatch
+
+        rd = ring_setup()
+        ring_restore(rotate)
+        outs_ = [(torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
+                  torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(2 * MULTI_K)]
+        arrs = []
+        for g0 in range(rotate // MULTI_K):
+            arr = (NbgBatch * MULTI_K)()
+            for q in range(MULTI_K):
+                be, pm, ct = outs_[(g0 & 1) * MULTI_K + q]
+                arr[q] = NbgBatch(rd["bufs"][g0 * MULTI_K + q].data_ptr(), BATCH, be.data_ptr(), pm.data_ptr(),
+                                  ct.data_ptr(), None)
+            arrs.append(arr)
+        flags = (NBG_SWAP_MACS if variant == "in_place" else 0) | NBG_DEFER_GROUP
+        st = sts[0]
+        kt = KernelTimer(calls + 1)
+        for i in range(calls + 1):
+            kt.start(i, st)
+            if clib.nbg_maglev_classify_device_multi(hs[0], arrs[i % len(arrs)], MULTI_K, SLOT, FRAME, flags, st):
+                raise RuntimeError(f"nbg_maglev_classify_device_multi: {nb._lib.last_error()}")
+            kt.stop(i, st)
+            finish(hs[0], st)
+        sync_all()
+        c_ms = kt.ms()[1:]
+        kt.close()
+        bpp = CLASSIFY_BYTES[variant]
+        ach = MULTI_K * BATCH * bpp / (c_ms.mean() / 1e3) / 1e9
+        return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "us_per_batch": round(c_ms.mean() * 1e3 / MULTI_K, 2),
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_pkt": bpp,
+                "working_set_mib": rotate * BATCH * SLOT >> 20, "launches": calls}
+
+    def ws_sweep(batches):
+        """The working-set sweep: the ring (read only, in place) and the multi-batch launch (in place,
+        read only) over 8 / 16 / 32 rotating 1M batches (0.5 / 1 / 2 GiB against the 256 MiB Infinity
+        Cache).  Every ring pass's outputs are checked."""
+        out = {}
+        for rot in WS_SWEEP:
+            if rot > RING_ROTATE or rot % MULTI_K:
+                continue
+            row = {}
+            for v in ("read_only", "in_place"):
+                try:
+                    row[f"ring_{v}"] = ring_pass(v, batches, rotate=rot)
+                except Exception as e:  # noqa: BLE001
+                    log(f"ring_{v} at {rot} failed: {e}")
+                    row[f"ring_{v}"] = {"error": str(e)[:300]}
+            for v in ("in_place", "read_only"):
+                row[f"{v}_multi{MULTI_K}"] = multi_rot_kernel(v, rot, max(40, 2 * rot // MULTI_K))
+            out[str(rot)] = row
+        return out
+
+    def c4_block(n_batches, scatter_steps):
+        """SURVEY.md section 8(e)'s C4: a 1M batch in `world` contiguous shards, one per rank (see the call
+        site).  Returns the line's `c4` block; raises on any check failure."""
+        shard_n = BATCH // world
+        gburst = C4_GROUP_BURST if shard_n <= 262144 else RING_GROUP_BURST
+        gstreams = C4_GROUP_STREAMS if shard_n <= 262144 else RING_GROUP_STREAMS
+        blk = {"shards": world, "shard_pkts": shard_n, "batch_pkts": BATCH,
+               "path": "per rank: persistent ring (in place) + nbg_ring_group_burst on side streams"}
+        if gpu:
+            ring_path(2 * BATCHES_PER_STEP, n=shard_n, gstreams=gstreams, gburst=gburst)  # warm
+            if world > 1:
+                dist.barrier()
+            sync_all()
+            t1 = time.perf_counter()
+            _, _, chk = ring_path(n_batches, n=shard_n, gstreams=gstreams, gburst=gburst, check=True)
+            sync_all()
+            el = time.perf_counter() - t1
+            if not chk["ok"]:
+                raise RuntimeError(f"C4 device-resident output check failed on rank {rank}: {chk}")
+        else:  # --selftest: no HIP; the timing fields are not a measurement
+            el = 1e-3
+        els = gather_floats(el)
+        worst = max(els)
+        total = world * shard_n * n_batches
+        blk["device_resident"] = {
+            "value": round(total / worst / 1e6, 1), "unit": "Mpps", "shards_per_rank": n_batches,
+            "per_gpu_mpps": [round(shard_n * n_batches / e / 1e6, 1) for e in els],
+            "us_per_shard": round(worst / n_batches * 1e6, 3),
+            "aggregate_frac": aggregate_frac(total, worst, PATH_BYTES["in_place"], world),
+            "group_burst": gburst, "group_streams": gstreams,
+            "what": "every rank streams its own resident 1M/N-packet shards through its ring (MAC swap in place + "
+                    "grouping), max-over-ranks time, no collective; aggregate_frac at 82 B/pkt over N x 8 TB/s"}
+        if world == 1 or scatter_steps <= 0:
+            return blk
+        # scatter-inclusive: two global batches alternate on rank 0; two shard buffers per rank
+        glob = None
+        if rank == 0:
+            glob = []
+            for b in range(2):
+                buf, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(0, 900 + b))
+                glob.append(torch.from_numpy(buf).to(dev) if gpu else torch.from_numpy(buf))
+        recv = [torch.empty(shard_n * SLOT, dtype=torch.uint8, device=dev) for _ in range(2)]
+        be = [torch.empty(shard_n, dtype=torch.uint16, device=dev) for _ in range(2)]
+        pm = [torch.empty(shard_n, dtype=torch.uint32, device=dev) for _ in range(2)]
+        ct = [torch.zeros(N_BACKENDS + 1, dtype=torch.uint32, device=dev) for _ in range(2)]
+        gb = torch.empty(world * shard_n * 2, dtype=torch.uint8, device=dev) if rank == 0 else None
+        gc = torch.empty(world * (N_BACKENDS + 1), dtype=torch.int32, device=dev) if rank == 0 else None
+        steps_run = 3 + scatter_steps
+        if gpu:
+            side = torch.cuda.Stream(dev)
+            ring = mgs[0].ring(swap_macs=True, stream=streams[0])
+            tk = [None, None]
+            gev = [None, None]
+        t1 = None
+        try:
+            for step in range(steps_run):
+                if step == 3:  # 3 untimed steps, then the timed ones
+                    if gpu:
+                        side.synchronize()
+                    dist.barrier()
+                    sync_all()
+                    t1 = time.perf_counter()
+                x = step & 1
+                if gpu:  # the buffers of step - 2: classified and gathered before they are reused
+                    if tk[x] is not None:
+                        ring.wait(tk[x])
+                        gev[x].synchronize()
+                scatter_shard(glob[x] if rank == 0 else None, recv[x], rank, world)
+                if gpu:
+                    torch.cuda.current_stream(dev).synchronize()  # the ring reads the shard
+                    tk[x] = ring.post(recv[x], shard_n, be[x])
+                    ring.group(tk[x], pm[x], ct[x], stream=side)
+                    with torch.cuda.stream(side):
+                        gather_results(be[x], ct[x], gb, gc, rank, world)
+                    gev[x] = torch.cuda.Event()
+                    gev[x].record(side)
+                else:  # selftest stand-in for the ring: every packet in group 0
+                    be[x].zero_()
+                    ct[x].zero_()
+                    ct[x][0] = shard_n
+                    gather_results(be[x], ct[x], gb, gc, rank, world)
+            if gpu:
+                side.synchronize()
+            el = time.perf_counter() - t1
+        finally:
+            if gpu:
+                ring.stop()
+        st_s = max(gather_floats(el))
+        ok = True
+        if rank == 0:  # the last step's gathered results against the launch path on the whole batch
+            if int(gc.sum()) != BATCH:
+                raise RuntimeError(f"C4 scatter pass: gathered counts sum {int(gc.sum())} != {BATCH}")
+            if gpu:
+                launch_ref(glob[(steps_run - 1) & 1].data_ptr(), BATCH)
+                if not torch.equal(ring_data["sbe"], gb.view(torch.uint16)):
+                    raise RuntimeError("C4 scatter pass: gathered backend[] differs from the launch path")
+        blk["scatter_inclusive"] = {
+            "value": round(BATCH * scatter_steps / st_s / 1e6, 1), "unit": "Mpps", "steps": scatter_steps,
+            "ms_per_batch": round(st_s / scatter_steps * 1e3, 4),
+            "root_egress_GBps": round(BATCH * SLOT * (world - 1) / world * scatter_steps / st_s / 1e9, 1),
+            "checked": ok,
+            "what": "rank 0 scatters one 1M 64-B batch in world contiguous shards (ncclScatter over xGMI), each "
+                    "rank's ring classifies + groups its shard, ncclGather returns backend[] + counts to rank 0 "
+                    "(two batches in flight); rank 0 checks the last batch against its own launch-path result"}
+        return blk
 
     # ---- configs C3 / C5 (IMIX descriptors): handles, traces and one call per batch
     imix = {}
@@ -976,9 +1269,12 @@ def run_rank(args) -> None:
                     mcall(i, v, st)
                 sync_all()
                 mgs[0].check()
-        # then one ring run: the ring alone (the profiler may serialise dispatches, so no grouping
-        # launches beside it)
-        ring_pass("in_place", PMC_RING_BATCHES)
+        # then the ring runs exactly as variants.ring_read_only / ring_in_place are timed (RING_BATCHES
+        # batches over RING_ROTATE inputs, one dispatch each): the ring alone (the profiler may
+        # serialise dispatches, so no grouping launches beside it)
+        if not args.no_ring:
+            for v in ("read_only", "in_place"):
+                ring_pass(v, PMC_RING_BATCHES)
         return
 
     if args.multi_only:  # profiling run: only the multi-batch passes
@@ -991,9 +1287,7 @@ def run_rank(args) -> None:
     #      on S streams, or the persistent ring with per-batch grouping (measured slower for runs of a
     #      few hundred batches: the ring's per-batch time drifts down over ~1,000 batches, DESIGN.md
     #      section 4).
-    # the headline's warm-up: --warmup steps, but at least MIN_WARM_STEPS (the path runs ~3-6 % faster
-    # once the memory system has been under load for ~20 ms: profiles/r03_warm_ab.txt)
-    warm = max(args.warmup, MIN_WARM_STEPS) if gpu else args.warmup
+    warm = args.warmup  # exactly the steps the line reports (the contract's W)
     headline = args.headline if gpu else "launch"
     if headline == "multi" and not m_arrs:
         headline = "launch"
@@ -1027,46 +1321,16 @@ def run_rank(args) -> None:
                   "value": round(BATCH * BATCHES_PER_STEP * args.steady_steps * world / st_el / 1e6, 1),
                   "ms_per_step": round(st_el / args.steady_steps * 1e3, 5)}
 
-    # ---- C4 scatter-inclusive pass (N > 1): every step rank 0 scatters world x 1M packets over
-    #      xGMI and each rank classifies its shard; reported beside the device-resident value.  A
-    #      failure here fails the job (exit code != 0), never a silent {"error"}.
-    scatter = None
-    if gpu and world > 1 and args.scatter_steps > 0:
-        recv = torch.empty(BATCH * SLOT, dtype=torch.uint8, device=dev)
-        glob = torch.cat([dbufs[0]] + [torch.empty_like(dbufs[0]) for _ in range(world - 1)]) if rank == 0 else None
-        if rank == 0:
-            for r in range(1, world):  # rank 0 holds every rank's first shard (same seeds as the ranks own)
-                buf_r, _, _ = nb.make_trace(BATCH, 0, seed=shard_seed(r, 0))
-                glob[r * BATCH * SLOT:(r + 1) * BATCH * SLOT].copy_(torch.from_numpy(buf_r))
-        cur = torch.cuda.current_stream(dev).cuda_stream
-        gb = torch.empty(world * BATCH * 2, dtype=torch.uint8, device=dev) if rank == 0 else None
-        gc = torch.empty(world * (N_BACKENDS + 1), dtype=torch.int32, device=dev) if rank == 0 else None
-        o0 = outs[0][0]
-
-        def sstep():
-            scatter_shard(glob, recv, rank, world)
-            mgs[0].group_by(recv, BATCH, stride=SLOT, frame_len=FRAME, swap_macs=True, stream=cur, **o0)
-            gather_results(o0["backend"], o0["counts"], gb, gc, rank, world)
-
-        for _ in range(3):
-            sstep()
-        sync_all()
-        dist.barrier()
-        sync_all()
-        t1 = time.perf_counter()
-        for _ in range(args.scatter_steps):
-            sstep()
-        sync_all()
-        st_s = max(gather_floats(time.perf_counter() - t1))
-        if rank == 0 and int(gc.sum()) != world * BATCH:
-            raise RuntimeError(f"gathered counts sum {int(gc.sum())} != {world * BATCH}")
-        scatter = {"value": round(BATCH * world * args.scatter_steps / st_s / 1e6, 1), "unit": "Mpps",
-                   "ms_per_step": round(st_s / args.scatter_steps * 1e3, 4), "steps": args.scatter_steps,
-                   "root_egress_GBps": round(BATCH * SLOT * (world - 1) * args.scatter_steps / st_s / 1e9, 1),
-                   "what": "rank 0 scatters world x 1M 64-B packets (ncclScatter over xGMI), each rank classifies "
-                           "its shard (MAC swap + grouping), rank 0 gathers every shard's backend[] and counts "
-                           "(ncclGather); single stream per rank"}
-        del recv, glob, gb, gc
+    # ---- config C4 as SURVEY.md section 8(e) defines it: ONE 1M batch split into `world` contiguous
+    #      shards (131,072 packets at 8 GPUs), one per rank, each classified + grouped through the
+    #      rank's persistent ring.  Device-resident: every rank streams its own resident shards (no
+    #      collective in the timed region).  Scatter-inclusive (N > 1): rank 0 holds the 1M batch,
+    #      ncclScatter hands each rank its shard, the rank's ring classifies + groups it, ncclGather
+    #      returns backend[] + counts to rank 0, which checks them against its own launch-path
+    #      classification of the batch.  Any failure fails the job.
+    c4 = None
+    if not args.no_c4:
+        c4 = c4_block(args.c4_batches, args.scatter_steps)
 
     # ---- roofline: the headline launch timed alone; labelled variants beside (N = 1)
     roof, mroof, variants = None, None, {}
@@ -1112,14 +1376,26 @@ def run_rank(args) -> None:
                         "on the same streams; below the streaming kernel's 262,144-packet threshold, so the "
                         "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
             if not args.no_ring:
-                # the ring's per-batch time settles after ~1,000 batches: 4,096
-                # batches per ring pass, slope over the middle three quarters
-                kb = max(args.steps * BATCHES_PER_STEP, 1024)
+                # the working-set sweep (0.5 / 1 / 2 GiB of rotating 1M batches): the ring read only and
+                # in place, RING_BATCHES batches per pass, slope over the middle three quarters, outputs
+                # checked after every pass; the multi-batch launch beside.  variants.ring_read_only /
+                # ring_in_place are the sweep's RING_ROTATE row (2 GiB).
                 kr = max(args.steps * BATCHES_PER_STEP, RING_BATCHES)
-                ring_runs = [("ring_read_only", lambda: ring_pass("read_only", kr)),
-                             ("ring_in_place", lambda: ring_pass("in_place", kr)),
-                             # C4's per-GPU shard on the ring: 131,072-packet batches, no launch per shard
-                             ("c4_shard_ring", lambda: ring_pass("in_place", 4096, n=C4_SHARD))]
+                try:
+                    sweep = ws_sweep(kr)
+                except Exception as e:  # noqa: BLE001
+                    log(f"working-set sweep failed: {e}")
+                    sweep = {"error": str(e)[:300]}
+                variants["ws_sweep"] = sweep
+                top = sweep.get(str(RING_ROTATE), {}) if isinstance(sweep, dict) else {}
+                for name in ("ring_read_only", "ring_in_place"):
+                    variants[name] = top.get(name, {"error": "not measured"})
+                kb = max(args.steps * BATCHES_PER_STEP, 1024)
+                ring_runs = [  # C4's per-GPU shard on the ring: 131,072-packet batches, no launch per shard
+                    ("c4_shard_ring", lambda: ring_pass("in_place", RING_BATCHES, n=C4_SHARD)),
+                    ("c4_shard_ring_grouped", lambda: ring_grouped(RING_BATCHES, n=C4_SHARD,
+                                                                    gstreams=C4_GROUP_STREAMS,
+                                                                    gburst=C4_GROUP_BURST))]
                 if headline != "ring":
                     ring_runs.append(("ring_in_place_grouped", lambda: ring_grouped(kb)))
                 for name, fn in ring_runs:
@@ -1130,9 +1406,15 @@ def run_rank(args) -> None:
                         variants[name] = {"error": str(e)[:300]}
                 if "us_per_batch" in variants["c4_shard_ring"]:
                     variants["c4_shard_ring"]["what"] = (
-                        "C4's per-GPU shard (131,072 packets: one 1M C2 batch in 8 contiguous shards, 64 distinct "
-                        "shards rotating) through the persistent ring, MAC swap in place: no launch, LUT staging "
-                        "or ramp per shard; backend[] + swap only")
+                        "C4's per-GPU shard (131,072 packets: one 1M C2 batch in 8 contiguous shards) through the "
+                        "persistent ring, MAC swap in place: no launch, LUT staging or ramp per shard; backend[] + "
+                        "swap only")
+                checks = [v.get("output_check") for k, v in variants.items()
+                          if isinstance(v, dict) and isinstance(v.get("output_check"), dict)]
+                checks += [r.get("output_check") for row in (sweep.values() if isinstance(sweep, dict) else [])
+                           if isinstance(row, dict) for r in row.values()
+                           if isinstance(r, dict) and isinstance(r.get("output_check"), dict)]
+                variants["ring_output_checks"] = {"passes": len(checks), "ok": all(c["ok"] for c in checks)}
 
             if m_arrs:
                 calls = max(args.steps * BATCHES_PER_STEP // MULTI_K, 10)
@@ -1160,7 +1442,6 @@ def run_rank(args) -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "warmup_steps_run": warm,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "ms_per_batch": round(elapsed / (args.steps * BATCHES_PER_STEP) * 1e3, 5),
             "higher_is_better": True,
@@ -1244,19 +1525,17 @@ def run_rank(args) -> None:
                                         "parse + hash + lookup"}
         if variants:
             line["variants"] = variants
-            cands = [k for k in (f"read_only_multi{MULTI_K}", "ring_read_only", "read_only")
-                     if isinstance(variants.get(k), dict) and "frac" in variants[k]]
-            if cands:  # BASELINE.json north_star: parse + hash + lookup at >= 70 % of the HBM roofline
-                best = max(cands, key=lambda k: variants[k]["frac"])
-                ro = variants[best]
+            ro = variants.get(f"read_only_multi{MULTI_K}")
+            if isinstance(ro, dict) and "frac" in ro:  # BASELINE.json north_star: parse + hash + lookup >= 70 %
+                rr_ = variants.get("ring_read_only", {})
                 line["north_star"] = {"target_frac": 0.70, "frac": float(ro["frac"]), "met": bool(ro["frac"] >= 0.70),
-                                      "variant": best,
+                                      "variant": f"read_only_multi{MULTI_K}",
                                       "single_batch_frac": variants.get("read_only", {}).get("frac"),
-                                      "ring_single_batch_frac": variants.get("ring_read_only", {}).get("frac"),
-                                      "multi_batch_frac": variants.get(f"read_only_multi{MULTI_K}", {}).get("frac")}
+                                      "ring_slope_frac": rr_.get("frac"),
+                                      "ring_working_set_mib": rr_.get("working_set_mib")}
         line["cpu_baseline"] = cpu
-        if scatter is not None:
-            line["scatter_inclusive"] = scatter
+        if c4 is not None:
+            line["c4"] = c4
         if args.selftest:
             line["selftest"] = True
             line["data"] = "synthetic (launcher selftest on CPU: no HIP call, steps are empty)"
@@ -1298,7 +1577,11 @@ def parse_args(argv):
                     help="launcher + rank logic on the CPU with gloo, no HIP call (tests)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--scatter-steps", type=int, default=50,
-                    help="N>1: steps of the scatter-inclusive pass (RCCL scatter from rank 0 + classify); 0 = skip")
+                    help="N>1: steps of C4's scatter-inclusive pass (RCCL scatter of one 1M batch from rank 0, "
+                         "ring classify + group, RCCL gather); 0 = skip")
+    ap.add_argument("--c4-batches", type=int, default=RING_BATCHES,
+                    help="shards per rank in C4's device-resident pass (through the rank's ring)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 block")
     return ap.parse_args(argv)
 
 

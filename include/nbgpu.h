@@ -42,6 +42,7 @@ extern "C" {
 #define NBG_ENOMEM (-12)
 #define NBG_ENODEV (-19)
 #define NBG_EIO (-5)
+#define NBG_EBUSY (-16)
 #define NBG_ETIMEDOUT (-110)
 
 /* backend value for a packet on which the reference would panic:
@@ -50,22 +51,37 @@ extern "C" {
  * Such packets land in group n_backends (the last of n_backends+1 groups). */
 #define NBG_SENTINEL 0xFFFFu
 
+/*
+ * Recommended path per configuration (BASELINE.json configs; DESIGN.md has the measurements):
+ *   C1  host mbufs, 10k-packet pcap      nbg_maglev_host_submit / _wait (or nbg_host_register + zero copy)
+ *   C2  1M fixed 64-B slots, 65 backends several RX queues resident: nbg_maglev_classify_device_multi;
+ *                                         a stream of batches: the persistent ring (nbg_ring_*) with
+ *                                         nbg_ring_group_burst; one batch: nbg_maglev_classify_device
+ *   C3  IMIX descriptors, 1000 backends  nbg_maglev_classify_device with NBG_OWNED_WINDOWS
+ *   C4  C2 in 8 shards, one per GPU      per rank: the persistent ring + nbg_ring_group_burst
+ *   C5  lpm -> maglev, IMIX              nbg_chain_lpm_maglev_device with NBG_OWNED_WINDOWS
+ */
+
 /* classify flags */
 #define NBG_SWAP_MACS 0x1u      /* apply MacHeader::swap_addresses in place (nf.rs:94-98) */
-#define NBG_LUT_LDS 0x2u        /* stage the LUT in LDS per workgroup instead of gathering from L2
-                                   (u8/u16 LUT <= 72 KiB; lower occupancy, kept as a measured variant) */
 #define NBG_OWNED_WINDOWS 0x4u  /* descriptor mode: the 64 B at every packet start belong to that
                                    packet (true for DPDK mbufs, whose data room is >= 2 KiB) */
-#define NBG_WB_PARTIAL 0x8u     /* write back only the 16 B holding the MACs (measurement knob) */
+#define NBG_WB_PARTIAL 0x8u     /* write back only the 16 B holding the MACs: the zero-copy host path
+                                   (nbg_host_register), where the rewrite crosses PCIe */
 #define NBG_DEFER_GROUP 0x10u   /* launch only the classify kernel; nbg_maglev_finish_group launches
                                    the grouping kernel (e.g. on another stream, after an event) */
+
+/* Measured variants: not the recommended paths (each measured slower than the default on the
+ * bench's workloads, DESIGN.md "Measured variants"), kept as named A/B alternatives and covered by
+ * the parity fuzz.  NBG_LUT_TILED is BASELINE config C3's named "LDS-tiled table". */
+#define NBG_LUT_LDS 0x2u        /* stage the LUT in LDS per workgroup instead of gathering from L2
+                                   (u8/u16 LUT <= 72 KiB; lower occupancy) */
 #define NBG_LUT_TILED 0x20u     /* u16 LUTs (> 256 backends): instead of gathering from L2, bucket the
-                                   packets by 64-KiB LUT tile and look them up per tile in LDS
-                                   (BASELINE config C3's named variant; measured slower) */
+                                   packets by 64-KiB LUT tile and look them up per tile in LDS */
 #define NBG_STREAM_DESC 0x40u   /* descriptor layouts with NBG_OWNED_WINDOWS, >= 262144 packets: the
                                    streaming classify kernel (one block per CU, everything fetched by
-                                   LDS-DMA).  Faster on one stream (C5 classify -5 %), slower when
-                                   several streams share the GPU (it cannot co-run): DESIGN.md §4 */
+                                   LDS-DMA).  Faster on one stream, slower when several streams share
+                                   the GPU (it cannot co-run) */
 #define NBG_GROUP_LAG 0x80u     /* pipelined grouping for a producer that calls the handle back to back
                                    (GroupByProducer::execute, operators/group_by.rs:43-55): the call
                                    classifies its batch (backend[], MAC swap) and leaves the batch's
@@ -191,9 +207,18 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
  * on `stream` so far.  It holds the LDS of every CU it occupies until it ends: after
  * nbg_ring_stop, or by itself after idle_ms without a post (its exit condition when the producer
  * goes away; 0 = 2000 ms; the next ring call then returns NBG_ETIMEDOUT).  nbg_ring_stop completes
- * every posted batch, waits for the kernel to end, and frees the ring.  One ring per handle; one
- * producer thread per ring.  Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
+ * every posted batch, waits for the kernel to end, and frees the ring (NBG_EBUSY if the kernel did
+ * not end within idle_ms + 5 s: then nothing it may touch is freed, and the device stays busy).
+ * ONE ring per GPU: a second nbg_ring_start on a device whose ring runs (from any handle) returns
+ * NBG_EBUSY at once.  Several RX queues share the device's ring through nbg_ring_queue_* below.
+ * While a handle's ring runs, that handle's classify calls (device, multi, host, chain) return
+ * NBG_EBUSY: their kernels would queue behind the resident one.  Other handles' batches on the same
+ * device co-run in the LDS the ring leaves free (about 30 KB per CU in place): while a ring runs they
+ * take the tile-per-wave classify kernel (never the streaming ones or NBG_LUT_LDS, which need a whole
+ * CU's LDS), with identical results.
+ * Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
  * flags: 0 (read only) or NBG_SWAP_MACS (in place).
+ * The nbg_ring_* calls of one ring are thread-safe (one mutex per ring).
  */
 #define NBG_RING_SLOTS 64u
 typedef struct nbg_ring nbg_ring;
@@ -207,17 +232,45 @@ typedef struct nbg_ring_batch {
 } nbg_ring_batch;
 int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
                         uint64_t* first_ticket);
-/* Group a completed ring batch: perm (u32[n], packet indices grouped by backend, arrival order inside
- * a group) and counts (u32[nb+1]) from its backend[], as nbg_maglev_classify_device_ex would give them
- * (group_by.rs:46-51).  Two launches on `stream` (any caller stream); they co-run with the resident
- * ring kernel.  `ticket` must be complete and among the last
- * NBG_RING_SLOTS posted.  Up to 4 side streams group concurrently (one scratch set each; calls on
- * one stream run in its order); a further stream takes over the least recently used set after that
- * set's stream's work. */
+/* Group a ring batch: perm (u32[n], packet indices grouped by backend, arrival order inside a group)
+ * and counts (u32[nb+1]) from its backend[], as nbg_maglev_classify_device_ex would give them
+ * (group_by.rs:46-51).  Launches on `stream` (any caller stream) that co-run with the resident ring
+ * kernel.  `ticket` must be among the last NBG_RING_SLOTS posted; it need not be complete yet: a
+ * one-wave gate kernel ahead of the grouping waits on the stream for the ring's completion word in
+ * HBM, so a producer enqueues a batch's grouping right after posting it, without polling (the
+ * reference classifies and enqueues in one loop, operators/group_by.rs:43-55).  If the ring ends
+ * before completing the batch (stop, idle exit), the gate opens anyway and perm / counts group
+ * whatever backend[] holds (always inside perm's n entries); the ring's next call reports the end.
+ * The batch's backend[] must stay untouched until the grouping has run on `stream`.
+ * Up to 4 side streams group concurrently (one scratch set each; calls on one stream run in its
+ * order); a further stream takes over the least recently used set after that set's stream's work. */
 int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream);
+/* The same for the n_batches (1..NBG_MAX_MULTI) consecutive tickets first_ticket.. of an RX burst, with
+ * one gate, one hist and one group launch for all of them (d_perm[j] / d_counts[j]: batch j's outputs):
+ * a burst of shard-size batches costs the producer three launches instead of three per batch. */
+int nbg_ring_group_burst(nbg_ring* r, uint64_t first_ticket, uint32_t n_batches, uint32_t* const* d_perm,
+                         uint32_t* const* d_counts, void* stream);
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed);
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms);
 int nbg_ring_stop(nbg_ring* r);
+
+/*
+ * RX queues on the device's ring: NetBricks runs one pipeline per RSS queue, each on its own core
+ * (scheduler/context.rs:241-255; RSS in native/pmd.c:16).  Each queue's producer thread posts its
+ * own batches into the one resident ring kernel and sees its own tickets (0, 1, 2, ... per queue),
+ * its own completion count and its own grouping; the batches of all queues share the ring's
+ * NBG_RING_SLOTS slots in the order they were posted.  Up to NBG_RING_MAX_QUEUES per ring; a queue
+ * is used by one thread at a time (different queues from different threads).  nbg_ring_stop closes
+ * every queue of the ring (their handles become invalid); nbg_ring_queue_close closes one earlier.
+ */
+#define NBG_RING_MAX_QUEUES 16u
+typedef struct nbg_ring_queue nbg_ring_queue;
+int nbg_ring_queue_open(nbg_ring* r, nbg_ring_queue** out);
+int nbg_ring_queue_post(nbg_ring_queue* q, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket);
+int nbg_ring_queue_poll(nbg_ring_queue* q, uint64_t* completed);
+int nbg_ring_queue_wait(nbg_ring_queue* q, uint64_t ticket, uint32_t timeout_ms);
+int nbg_ring_queue_group(nbg_ring_queue* q, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream);
+int nbg_ring_queue_close(nbg_ring_queue* q);
 /* The duration of the handle's last ring kernel (HIP events on its stream: start to end), valid after
  * nbg_ring_stop.  A stopped ring's buffers and stream are kept by the handle for its next
  * nbg_ring_start (freed by nbg_maglev_destroy). */

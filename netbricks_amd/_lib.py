@@ -34,6 +34,8 @@ NBG_GROUP_LAG = 0x80
 NBG_HOST_SLOTS = 3
 NBG_MAX_MULTI = 8
 NBG_RING_SLOTS = 64
+NBG_RING_MAX_QUEUES = 16
+NBG_EBUSY = -16
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
@@ -71,10 +73,17 @@ SIGNATURES = {
     "nbg_ring_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),
     "nbg_ring_post_burst": (C.c_int, [_P, _P, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "nbg_ring_group": (C.c_int, [_P, C.c_uint64, _P, _P, _P]),
+    "nbg_ring_group_burst": (C.c_int, [_P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_ring_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "nbg_ring_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
     "nbg_ring_stop": (C.c_int, [_P]),
     "nbg_ring_kernel_ms": (C.c_int, [_P, C.POINTER(C.c_float)]),
+    "nbg_ring_queue_open": (C.c_int, [_P, C.POINTER(_P)]),
+    "nbg_ring_queue_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),
+    "nbg_ring_queue_poll": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "nbg_ring_queue_wait": (C.c_int, [_P, C.c_uint64, C.c_uint32]),
+    "nbg_ring_queue_group": (C.c_int, [_P, C.c_uint64, _P, _P, _P]),
+    "nbg_ring_queue_close": (C.c_int, [_P]),
     "nbg_maglev_check": (C.c_int, [_P]),
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_maglev_host_submit": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, C.POINTER(C.c_uint64)]),

@@ -1480,7 +1480,10 @@ __device__ __forceinline__ void ring_relay(const RingArgs& r, uint32_t lane) {
 #endif
     if (c != done) {
       done = c;
-      if (lane == 0) __hip_atomic_store(&r.ctl->completed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == 0) {
+        __hip_atomic_store(r.dcomp, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // the gate kernels
+        __hip_atomic_store(&r.ctl->completed, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       moved = true;
     }
     if (moved) {
@@ -1761,6 +1764,27 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
 #undef RING_PUBLISH
 #undef RING_TAKE_STAGED
   if (!ctl) { SPROBE(19) }
+  // the block's exit, once every wave's stores have retired: a gate kernel waiting for a batch this
+  // ring will never complete (stop, idle exit) returns when every classify block has exited
+  wait_vm<0>();
+  lds_sync();
+  if (tid == 0) __hip_atomic_fetch_add(r.dexit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The gate of a ring batch's grouping (nbg_ring_group before the batch is complete): one wave that
+// polls the relay's completion word in uncached HBM and returns once batch target - 1 is complete,
+// or once every classify block has exited (the ring ended; the grouping then reads what backend[]
+// holds, which no kernel writes any more).  Every path ends: the ring itself always ends (stop or
+// idle_ms).  Launched ahead of the batch's hist / group kernels on the caller's stream, so the
+// producer needs no host poll between the ring's completion and the grouping.
+__global__ __launch_bounds__(64) void ring_gate_kernel(const uint32_t* dcomp, const uint32_t* dexit, uint32_t target,
+                                                       uint32_t grid) {
+  for (uint32_t nap = 1;; nap = min(2u * nap, 4u)) {
+    const uint32_t c = rfl(__hip_atomic_load(dcomp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    if (static_cast<int32_t>(c - target) >= 0) return;
+    if (rfl(__hip_atomic_load(dexit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >= grid) return;
+    for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 // ---- streaming classify for descriptor layouts (IMIX: u32 offsets + u16 lengths, owned windows) ----
@@ -2032,9 +2056,13 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
 // Many backends: the partition histograms come from this kernel instead of the classify kernel
 // (whose per-block flush would cost about one global atomic per packet at ~1000 bins).  One
 // 512-thread block per partition counts its packets' backends in LDS and stores the whole row.
-__global__ __launch_bounds__(kGBlock) void hist_kernel(HistArgs a) {
+// Blocks [j * hm.per, j * hm.per + h[j].n_parts) count batch j (a single batch: j = 0).
+__global__ __launch_bounds__(kGBlock) void hist_kernel(HistMulti hm) {
   extern __shared__ __align__(16) uint32_t hs[];
-  const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c = blockIdx.x;
+  const uint32_t bj = blockIdx.x / hm.per;
+  const HistArgs a = hm.h[bj];
+  const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c = blockIdx.x - bj * hm.per;
+  if (c >= a.n_parts) return;
   const uint32_t pbeg = c * a.part_pkts, pend = min(pbeg + a.part_pkts, a.n_pkts);
   for (uint32_t b = tid; b < nbins; b += kGBlock) hs[b] = 0;
   lds_sync();
@@ -2045,7 +2073,9 @@ __global__ __launch_bounds__(kGBlock) void hist_kernel(HistArgs a) {
     for (int k = 0; k < kGRounds; ++k) v[k] = ld_u16(a.backend, min(i0 + k * kGBlock + tid, a.n_pkts - 1u) * 2u);
 #pragma unroll
     for (int k = 0; k < kGRounds; ++k) {
-      if (i0 + k * kGBlock + tid < pend) atomicAdd(&hs[v[k] == NBG_SENTINEL ? a.nb : v[k]], 1u);
+      // min: the sentinel (0xFFFF) is bin nb; so is any other value > nb, which no classify writes
+      // but a ring batch's backend[] can hold after a ring that ended before completing it
+      if (i0 + k * kGBlock + tid < pend) atomicAdd(&hs[min(v[k], a.nb)], 1u);
     }
   }
   lds_sync();
@@ -2590,7 +2620,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
     for (int r = 0; r < kGRounds; ++r) {
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
-      const uint32_t bin = pre_bin[r] == NBG_SENTINEL ? a.nb : pre_bin[r];
+      const uint32_t bin = min(pre_bin[r], a.nb);  // the sentinel (and any value > nb, as in hist_kernel)
       // lanes with my bin (and my validity): per bit, keep the lanes whose ballot bit equals mine
       const uint32_t mv = valid ? ~0u : 0u;
       const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
@@ -2886,6 +2916,14 @@ int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int
   return NBG_OK;
 }
 
+int launch_ring_gate(const uint32_t* dcomp, const uint32_t* dexit, uint32_t target, uint32_t grid, void* stream) {
+  hipLaunchKernelGGL(ring_gate_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), dcomp, dexit, target,
+                     grid);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "ring gate launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
 int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
   StreamBatches sb{};
   sb.pkts[0] = a.pkts;
@@ -2937,9 +2975,22 @@ int launch_hist(const HistArgs& a, void* stream) {
       attr = true;
     }
   }
-  hipLaunchKernelGGL(hist_kernel, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), a);
+  HistMulti hm{};
+  hm.h[0] = a;
+  hm.per = a.n_parts;
+  hipLaunchKernelGGL(hist_kernel, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), hm);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "hist launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+int launch_hist_multi(const HistMulti& hm, uint32_t n, void* stream) {
+  if (n == 0 || n > kMaxMulti) return set_error(NBG_EINVAL, "hist (multi): %u batches", n);
+  if ((hm.h[0].nb + 1) * 4 > 64 * 1024) return set_error(NBG_EINVAL, "hist (multi): at most 16383 bins");
+  hipLaunchKernelGGL(hist_kernel, dim3(hm.per * n), dim3(kGBlock), (hm.h[0].nb + 1) * 4,
+                     static_cast<hipStream_t>(stream), hm);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "hist launch (multi): %s", hipGetErrorString(e));
   return NBG_OK;
 }
 
@@ -3148,3 +3199,26 @@ extern "C" int nbg_debug_cprobe(unsigned long long* out, uint64_t n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_cprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
 }
 #endif
+
+// Diagnostics (not in include/nbgpu.h; tests only): `blocks` one-wave workgroups that each hold
+// `lds_bytes` of a CU's LDS for `us` microseconds (100 MHz wall clock; every wave exits by time) —
+// other work occupying CUs when a persistent ring starts (tests/test_gpu_ring.py).
+namespace nbg {
+__global__ __launch_bounds__(64) void hold_cus_kernel(uint64_t ticks, uint32_t* sink) {
+  extern __shared__ uint32_t held[];
+  const uint64_t t0 = wall_clock64();
+  held[threadIdx.x] = threadIdx.x;
+  while (static_cast<uint64_t>(wall_clock64()) - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+  if (held[threadIdx.x] == 0xdeadbeefu) sink[0] = 1u;
+}
+}  // namespace nbg
+
+extern "C" int nbg_debug_hold_cus(uint32_t blocks, uint32_t lds_bytes, uint32_t us, void* stream) {
+  if (blocks == 0 || blocks > 4096 || lds_bytes < 256 || lds_bytes > 160u * 1024u || us > 10000000u) return NBG_EINVAL;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(nbg::hold_cus_kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    return NBG_EIO;
+  hipLaunchKernelGGL(nbg::hold_cus_kernel, dim3(blocks), dim3(64), lds_bytes, static_cast<hipStream_t>(stream),
+                     static_cast<uint64_t>(us) * 100u, static_cast<uint32_t*>(nullptr));
+  return hipGetLastError() == hipSuccess ? NBG_OK : NBG_EIO;
+}

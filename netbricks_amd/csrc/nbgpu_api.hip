@@ -92,6 +92,7 @@ struct nbg_maglev {
   uint32_t lag_dirty = 0;             // bit k: set k may hold counts (zeroed before it is accumulated into)
   nbg_ring* ring = nullptr;           // the running persistent ring (nbg_ring_start), if any
   nbg_ring* ring_spare = nullptr;     // a stopped ring's buffers and stream, kept for the next start
+  bool ring_leaked = false;           // a ring's kernel did not end at stop: never free what it may touch
   float ring_kernel_ms = -1.f;        // the last ring kernel's duration (HIP events), after its stop
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
   bool issued = false;                // a launch has been issued on last_stream
@@ -173,6 +174,15 @@ int check_device(int device) {
                      ndev);
   if (device < 0 || device >= ndev) return set_error(NBG_ENODEV, "device %d out of range (%d devices)", device, ndev);
   return NBG_OK;
+}
+
+// The running persistent ring of each device (one per GPU: its kernel holds every CU's LDS).
+std::mutex g_dev_ring_mu;
+std::vector<nbg_ring*> g_dev_ring;
+
+bool device_ring_running(int device) {
+  std::lock_guard<std::mutex> g(g_dev_ring_mu);
+  return device >= 0 && static_cast<size_t>(device) < g_dev_ring.size() && g_dev_ring[device] != nullptr;
 }
 
 struct DeviceGuard {
@@ -329,8 +339,11 @@ int upload(nbg_maglev* h) {
 
 // The LUT is gathered from L2 by default (measured faster: the LDS-staged copy costs
 // occupancy); NBG_LUT_LDS stages it in LDS when it fits.
+// While a persistent ring runs on the device, kernels that need a whole CU's LDS (the streaming
+// kernels, the LDS-staged LUT) would wait for it to end: batches of other handles then take the
+// tile-per-wave kernel, which co-runs in the LDS the ring leaves free.
 bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
-  return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024;
+  return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024 && !device_ring_running(h->device);
 }
 
 // The streaming classify kernel serves fixed 64-B-aligned slots with a u8 LUT of at most 65537
@@ -342,7 +355,7 @@ bool use_stream(const nbg_maglev* h, uint64_t n_pkts) {
     const char* e = std::getenv("NBG_STREAM");
     return !e || std::atoi(e) != 0;
   }();
-  return on && !h->wide && h->m <= 65537 && n_pkts >= 262144;
+  return on && !h->wide && h->m <= 65537 && n_pkts >= 262144 && !device_ring_running(h->device);
 }
 
 // NBG_STREAM_DESC: descriptor layouts (IMIX offsets + lengths) with owned windows take the
@@ -352,7 +365,7 @@ bool use_stream(const nbg_maglev* h, uint64_t n_pkts) {
 // holds all LDS of every CU, so with three streams the tile-per-wave kernels co-running beat it
 // (profiles/r02_stream_desc_ab.txt).
 bool use_stream_desc(const nbg_maglev* h, uint64_t n_pkts, uint32_t flags, bool chain, int mode) {
-  if (!(flags & NBG_STREAM_DESC) || n_pkts < 262144) return false;
+  if (!(flags & NBG_STREAM_DESC) || n_pkts < 262144 || device_ring_running(h->device)) return false;
   if (h->wide) return !chain;
   return h->m <= 65537 && mode != 1;
 }
@@ -503,6 +516,12 @@ int nbg_maglev_create_from_lut(const uint16_t* lut, uint64_t table_size, uint32_
 void nbg_maglev_destroy(nbg_maglev* h) {
   if (!h) return;
   if (h->ring) (void)nbg_ring_stop(h->ring);
+  if (h->ring_leaked) {
+    // a ring kernel that did not end at its stop may still read the LUT and the ring's buffers: leak
+    // the handle's device memory rather than free it under the kernel (the host struct goes)
+    delete h;
+    return;
+  }
   if (h->ring_spare) {
     DeviceGuard g(h->device);
     ring_free(h->ring_spare);
@@ -591,9 +610,9 @@ int classify_lag(nbg_maglev* h, ClassifyArgs& a, bool fuse, uint32_t n_parts, ui
   LagGroup lg = fuse ? h->pending_lg : LagGroup{};
   lg.zero = h->d_part_lag + z * set_words;
   lg.zero_words = static_cast<uint32_t>(set_words);
-  h->pending = h->pending_lag = false;
   const int rc = launch_classify_stream_lag(a, lg, h->cus, s);
-  if (rc) return rc;
+  if (rc) return rc;  // the pending group (if any) stays pending: finish_group or the next call launches it
+  h->pending = h->pending_lag = false;
   h->lag_dirty = (h->lag_dirty | (1u << k)) & ~(1u << z);
   h->lag_idx = z;
   LagGroup& p = h->pending_lg;
@@ -631,6 +650,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
                     uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
                     uint16_t* d_gate, void* stream) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
+  if (h->ring) return set_error(NBG_EBUSY, "classify: the handle's persistent ring is running (nbg_ring_stop first)");
   if (h->pending && !h->pending_lag)
     return set_error(NBG_EINVAL, "classify: a deferred group is pending (nbg_maglev_finish_group)");
   if ((flags & NBG_GROUP_LAG) && (flags & NBG_DEFER_GROUP))
@@ -895,6 +915,7 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
     return set_error(NBG_EINVAL, "classify (multi): 1..%u batches", NBG_MAX_MULTI);
   if (flags & ~(NBG_SWAP_MACS | NBG_DEFER_GROUP))
     return set_error(NBG_EINVAL, "classify (multi): flags other than NBG_SWAP_MACS and NBG_DEFER_GROUP");
+  if (h->ring) return set_error(NBG_EBUSY, "classify (multi): the handle's persistent ring is running");
   if (h->pending_lag) {  // a pending lagged group is launched alone first
     const int rc = nbg_maglev_finish_group(h, stream);
     if (rc) return rc;
@@ -1116,13 +1137,21 @@ int nbg_maglev_check(nbg_maglev* h) {
 // ---- persistent RX ring (nbg_ring_*) ---------------------------------------------------------------
 }  // extern "C"
 
+// An RX queue's view of the device's ring: its own tickets over the ring's shared sequence.
+struct nbg_ring_queue {
+  nbg_ring* r = nullptr;
+  uint64_t posted = 0, done = 0;        // this queue's batches posted / complete
+  uint64_t gidx[NBG_RING_SLOTS] = {};   // the ring ticket of this queue's ticket t, at t % NBG_RING_SLOTS
+};
+
 struct nbg_ring {
   nbg_maglev* h = nullptr;
+  std::mutex mu;                       // posts, completion, queues, grouping: several producer threads
   hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
   hipEvent_t ev_start = nullptr, ev_end = nullptr;  // around the kernel on `stream` (its duration)
   size_t hbytes = 0, dbytes = 0;       // the pinned host ring and the uncached device ring
   uint8_t* host = nullptr;             // pinned, mapped: RingCtl | RingDesc[slots]
-  uint8_t* dev = nullptr;              // uncached HBM: stop word (own line) | prog[grid] | RingDesc[reps][slots]
+  uint8_t* dev = nullptr;              // uncached HBM: stop | completion | exits (a line each) | prog[grid] | RingDesc[reps][slots]
   volatile RingCtl* ctl = nullptr;
   RingDesc* desc = nullptr;
   uint32_t slots = NBG_RING_SLOTS;
@@ -1133,17 +1162,20 @@ struct nbg_ring {
   // per slot, the batch posted there last (nbg_ring_group groups it from its backend[])
   std::vector<std::pair<uint16_t*, uint64_t>> rec;
   // nbg_ring_group's scratch, one set per side stream (up to kGroupSets streams group concurrently;
-  // a further stream takes over the least recently used set after that set's stream's work)
+  // a further stream takes over the least recently used set after that set's stream's work).  A set
+  // is owned through `claimed`, not through the stream value: the null stream is a stream too.
   struct GroupSet {
-    hipStream_t s = nullptr;       // the stream that uses the set
+    bool claimed = false;
+    hipStream_t s = nullptr;       // the owning stream (nullptr: the null stream)
     uint64_t used = 0;             // last use (call count)
-    uint32_t* rows = nullptr;      // partition histograms [kMaxParts][nb+1]
+    uint32_t* rows = nullptr;      // partition histograms [kMaxMulti][kMaxParts][nb+1] (a burst: one set per batch)
     uint32_t* prefix = nullptr;    // per-partition prefixes (scan-kernel path)
     uint32_t* totals = nullptr;    // totals [nb+1]
   };
   static constexpr int kGroupSets = 4;
   GroupSet gsets[kGroupSets];
   uint64_t gcalls = 0;
+  std::vector<nbg_ring_queue*> queues;  // open RX queues (closed by nbg_ring_stop)
   bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
   // hipStreamQuery is not cheap on a stream with a resident kernel, so the kernel's end is only
   // checked after the completed count has not moved for kStallCheck
@@ -1154,13 +1186,23 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// The uncached device buffer: the stop word, the completion word and the exit count on lines of
+// their own, then the blocks' progress words, then the descriptor replicas.
+constexpr size_t kDevStop = 0, kDevComp = 64, kDevExit = 128, kDevProg = 192;
+size_t ring_desc_off(int grid) { return kDevProg + ((static_cast<size_t>(grid) * 4u + 63u) & ~size_t{63}); }
+
 // Completed batches: the relay reports the minimum over the blocks' counts (mod 2^32, so taken as
-// a lag behind `posted`).
+// a lag behind `posted`).  Under r->mu.
 void ring_refresh(nbg_ring* r) {
   const uint32_t lag = static_cast<uint32_t>(r->posted) - r->ctl->completed;
   const uint64_t c = lag <= r->posted - r->completed ? r->posted - lag : r->completed;
   if (c != r->completed) r->moved = Clock::now();
   r->completed = c;
+}
+
+// A queue's completed tickets: its batches complete in ring order.  Under r->mu.
+void queue_refresh(nbg_ring_queue* q) {
+  while (q->done < q->posted && q->gidx[q->done % NBG_RING_SLOTS] < q->r->completed) ++q->done;
 }
 
 constexpr auto kStallCheck = std::chrono::milliseconds(2);
@@ -1189,13 +1231,30 @@ void ring_pause(Clock::time_point t0) {
   if (Clock::now() - t0 > std::chrono::microseconds(200)) std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
-void ring_free(nbg_ring* r) {
+void ring_close_queues(nbg_ring* r) {
+  for (auto* q : r->queues) delete q;
+  r->queues.clear();
+}
+
+// Wait for the grouping streams' work on the scratch sets and release them.
+void ring_release_sets(nbg_ring* r) {
   for (auto& g : r->gsets) {
-    if (g.s) (void)hipStreamSynchronize(g.s);  // its kernels use the scratch below
+    if (g.claimed) (void)hipStreamSynchronize(g.s);
+    g.claimed = false;
+    g.s = nullptr;
+    g.used = 0;
+  }
+  r->gcalls = 0;
+}
+
+void ring_free(nbg_ring* r) {
+  ring_release_sets(r);  // their kernels use the scratch below
+  for (auto& g : r->gsets) {
     (void)hipFree(g.rows);
     (void)hipFree(g.prefix);
     (void)hipFree(g.totals);
   }
+  ring_close_queues(r);
   if (r->host) (void)hipHostFree(r->host);
   if (r->dev) (void)hipFree(r->dev);
   if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -1230,8 +1289,7 @@ int ring_alloc(nbg_maglev* h, nbg_ring** out) {
     return set_error(NBG_EIO, "ring_start: events");
   }
   r->hbytes = sizeof(RingCtl) + static_cast<size_t>(r->slots) * sizeof(RingDesc);
-  const size_t prog_off = 64, desc_off = prog_off + ((static_cast<size_t>(r->grid) * 4u + 63u) & ~size_t{63});
-  r->dbytes = desc_off + static_cast<size_t>(r->reps) * r->slots * sizeof(RingDesc);
+  r->dbytes = ring_desc_off(r->grid) + static_cast<size_t>(r->reps) * r->slots * sizeof(RingDesc);
   if (hipHostMalloc(reinterpret_cast<void**>(&r->host), r->hbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
       hipSuccess) {
     r->host = nullptr;
@@ -1247,7 +1305,7 @@ int ring_alloc(nbg_maglev* h, nbg_ring** out) {
   }
   const size_t nbins = static_cast<size_t>(h->nb) + 1;
   for (auto& g : r->gsets)
-    if (hipMalloc(&g.rows, kMaxParts * nbins * 4) != hipSuccess ||
+    if (hipMalloc(&g.rows, kMaxMulti * kMaxParts * nbins * 4) != hipSuccess ||
         hipMalloc(&g.prefix, kMaxParts * nbins * 4) != hipSuccess || hipMalloc(&g.totals, nbins * 4) != hipSuccess) {
       ring_free(r);
       return set_error(NBG_ENOMEM, "ring_start: grouping scratch");
@@ -1255,97 +1313,6 @@ int ring_alloc(nbg_maglev* h, nbg_ring** out) {
   *out = r;
   return NBG_OK;
 }
-
-}  // namespace
-
-extern "C" {
-
-int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms, void* stream,
-                   nbg_ring** out) {
-  if (!h || !out) return set_error(NBG_EINVAL, "ring_start: null argument");
-  *out = nullptr;
-  if (h->ring) return set_error(NBG_EINVAL, "ring_start: the handle already runs a ring");
-  if (h->wide || h->m > 65537) return set_error(NBG_EINVAL, "ring_start: needs <= 255 backends and M <= 65537");
-  if (stride % 16 || stride < 64 || stride >= (1u << 24) || fixed_len < 48)
-    return set_error(NBG_EINVAL, "ring_start: fixed slots with stride %% 16 == 0, 64 <= stride < 2^24, fixed_len >= 48");
-  if (flags & ~NBG_SWAP_MACS) return set_error(NBG_EINVAL, "ring_start: flags other than NBG_SWAP_MACS");
-  if (h->pending) return set_error(NBG_EINVAL, "ring_start: a deferred or lagged group is pending");
-  if (h->cus < 2) return set_error(NBG_EINVAL, "ring_start: needs a CU for the relay beside the classify blocks");
-  DeviceGuard g(h->device);
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  int rc = order_after_last(h, s);  // the ring runs after the handle's earlier work
-  if (rc) return rc;
-  // a stopped ring's buffers, stream and events are reused (a start then costs a memset and a launch)
-  nbg_ring* r = h->ring_spare;
-  h->ring_spare = nullptr;
-  if (!r && (rc = ring_alloc(h, &r))) return rc;
-  r->idle_ms = idle_ms ? idle_ms : 2000u;
-  r->moved = Clock::now();
-  r->posted = r->units = r->completed = 0;
-  r->ended = false;
-  r->rec.assign(r->slots, {nullptr, 0});
-  std::memset(r->host, 0, r->hbytes);
-  {
-    // after everything issued on `stream` so far, in the private stream's order: zero the device
-    // ring, then the kernel
-    hipEvent_t ev = nullptr;
-    const bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
-                    hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent(r->stream, ev, 0) == hipSuccess &&
-                    hipMemsetAsync(r->dev, 0, r->dbytes, r->stream) == hipSuccess;
-    if (ev) (void)hipEventDestroy(ev);
-    if (!ok) {
-      ring_free(r);
-      return set_error(NBG_EIO, "ring_start: ordering after the caller's stream");
-    }
-  }
-  const size_t prog_off = 64, desc_off = prog_off + ((static_cast<size_t>(r->grid) * 4u + 63u) & ~size_t{63});
-  uint8_t* hdev = nullptr;
-  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess) {
-    ring_free(r);
-    return set_error(NBG_EIO, "ring_start: device address of the pinned ring");
-  }
-  ClassifyArgs a{};
-  a.stride = stride;
-  a.fixed_len = fixed_len;
-  a.lut = h->d_lut;
-  a.m = static_cast<uint32_t>(h->m);
-  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
-  a.nb = h->nb;
-  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
-  a.win_owned = 1;
-  a.wb_full = 1;
-  a.lean = 1;
-  a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
-  a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
-  RingArgs ra{};
-  ra.ctl = reinterpret_cast<RingCtl*>(hdev);
-  ra.hdesc = reinterpret_cast<const RingDesc*>(hdev + sizeof(RingCtl));
-  ra.dstop = reinterpret_cast<uint32_t*>(r->dev);
-  ra.prog = reinterpret_cast<uint32_t*>(r->dev + prog_off);
-  ra.desc = reinterpret_cast<RingDesc*>(r->dev + desc_off);
-  ra.slots = r->slots;
-  ra.reps = r->reps;
-  ra.grid = static_cast<uint32_t>(r->grid);
-  ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
-  const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
-  ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
-  (void)hipEventRecord(r->ev_start, r->stream);
-  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, r->stream))) {
-    ring_free(r);
-    return rc;
-  }
-  (void)hipEventRecord(r->ev_end, r->stream);
-  h->ring_kernel_ms = -1.f;
-  h->ring = r;
-  h->last_stream = s;
-  h->issued = true;
-  *out = r;
-  return NBG_OK;
-}
-
-}  // extern "C"
-
-namespace {
 
 int ring_check_batch(uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
   if (n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "ring_post: n_pkts must be < 2^30");
@@ -1355,8 +1322,9 @@ int ring_check_batch(uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
   return NBG_OK;
 }
 
-// Write batch `posted` into its host slot (the caller found the slot free).
-void ring_put(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
+// Write batch `posted` into its host slot (the caller found the slot free) and return its ring
+// ticket.  Under r->mu.
+uint64_t ring_put(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend) {
   const uint64_t j = r->posted;
   if (r->completed == j) r->moved = Clock::now();  // the stall clock starts with the first outstanding batch
   const uint64_t units = ((n_pkts + 63) / 64 + 7) / 8;  // 512-packet units of 8 waves' tiles
@@ -1376,86 +1344,93 @@ void ring_put(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend
   r->rec[j & (r->slots - 1)] = {d_backend, n_pkts};
   r->posted = j + 1;
   r->units += units;
+  return j;
 }
 
-}  // namespace
-
-extern "C" {
-
-int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
-                        uint64_t* first_ticket) {
-  if (!r || !n_posted || !first_ticket || (n_batches && !batches))
-    return set_error(NBG_EINVAL, "ring_post_burst: null argument");
-  *n_posted = 0;
-  *first_ticket = r->posted;
-  for (uint32_t i = 0; i < n_batches; ++i) {
-    const int rc = ring_check_batch(batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
-    if (rc) return rc;
-  }
-  ring_refresh(r);
-  if (ring_gone(r)) return ring_state_error(r);
-  const uint64_t room = r->slots - (r->posted - r->completed);
-  const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(room, n_batches));
-  for (uint32_t i = 0; i < k; ++i) ring_put(r, batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
-  *n_posted = k;
-  return NBG_OK;
-}
-
-int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
-  if (!r || !ticket) return set_error(NBG_EINVAL, "ring_post: null argument");
+// One batch into the ring, waiting for a free slot (the batch NBG_RING_SLOTS back complete); with a
+// queue, *ticket is the queue's ticket.  The ring's mutex is held only while the state is touched.
+int ring_post_one(nbg_ring* r, nbg_ring_queue* q, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend,
+                  uint64_t* ticket) {
   int rc = ring_check_batch(d_pkts, n_pkts, d_backend);
   if (rc) return rc;
-  // a free slot: the batch `slots` back is complete
   const auto t0 = Clock::now();
-  while (r->posted - r->completed >= r->slots) {
-    ring_refresh(r);
-    if (r->posted - r->completed < r->slots) break;
-    if (ring_gone(r)) return ring_state_error(r);
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> g(r->mu);
+      ring_refresh(r);
+      if (ring_gone(r)) return ring_state_error(r);
+      if (r->posted - r->completed < r->slots) {
+        const uint64_t gt = ring_put(r, d_pkts, n_pkts, d_backend);
+        if (q) {
+          queue_refresh(q);  // frees the entry of the queue's ticket NBG_RING_SLOTS back (complete by now)
+          q->gidx[q->posted % NBG_RING_SLOTS] = gt;
+          *ticket = q->posted++;
+        } else {
+          *ticket = gt;
+        }
+        return NBG_OK;
+      }
+    }
     if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 1000u))
       return set_error(NBG_ETIMEDOUT, "ring_post: no slot freed in %u ms", r->idle_ms + 1000u);
     ring_pause(t0);
   }
-  if (ring_gone(r)) return ring_state_error(r);
-  *ticket = r->posted;
-  ring_put(r, d_pkts, n_pkts, d_backend);
-  return NBG_OK;
 }
 
-int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
-  if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group: null argument");
-  hipStream_t s = static_cast<hipStream_t>(stream);
-  if (ticket >= r->posted) return set_error(NBG_EINVAL, "ring_group: ticket %llu was not posted", (unsigned long long)ticket);
-  if (r->posted - ticket > r->slots)
-    return set_error(NBG_EINVAL, "ring_group: ticket %llu is older than the ring's %u slots", (unsigned long long)ticket,
-                     r->slots);
-  ring_refresh(r);
-  if (ticket >= r->completed)
-    return set_error(NBG_EINVAL, "ring_group: batch %llu is not complete", (unsigned long long)ticket);
-  DeviceGuard g(r->h->device);
-  const auto [backend, n_pkts] = r->rec[ticket & (r->slots - 1)];
-  const uint32_t nbins = r->h->nb + 1;
-  // this stream's scratch set; a stream without one takes a free set, or the least recently used
-  // one after everything its previous stream has issued so far
+// Stream s's scratch set; a stream without one takes a free set, or the least recently used one
+// after everything its previous stream has issued so far.  Under r->mu.
+int ring_gset(nbg_ring* r, hipStream_t s, nbg_ring::GroupSet** out) {
   nbg_ring::GroupSet* gs = nullptr;
-  for (auto& g : r->gsets)
-    if (g.s == s) gs = &g;
+  for (auto& x : r->gsets)
+    if (x.claimed && x.s == s) gs = &x;
   if (!gs) {
-    gs = &r->gsets[0];
-    for (auto& g : r->gsets)
-      if (!g.s || (gs->s && g.used < gs->used)) gs = &g;
-    if (gs->s) {
+    for (auto& x : r->gsets)
+      if (!x.claimed) {
+        gs = &x;
+        break;
+      }
+    if (!gs) {
+      gs = &r->gsets[0];
+      for (auto& x : r->gsets)
+        if (x.used < gs->used) gs = &x;
       hipEvent_t ev = nullptr;
       NBG_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       const hipError_t e1 = hipEventRecord(ev, gs->s), e2 = hipStreamWaitEvent(s, ev, 0);
       (void)hipEventDestroy(ev);
       if (e1 != hipSuccess || e2 != hipSuccess) return set_error(NBG_EIO, "ring_group: stream order");
     }
+    gs->claimed = true;
     gs->s = s;
   }
   gs->used = ++r->gcalls;
+  *out = gs;
+  return NBG_OK;
+}
+
+// The grouping of ring ticket `ticket` on stream s (gated on its completion when not complete yet).
+// Under r->mu.
+int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, hipStream_t s) {
+  if (ticket >= r->posted)
+    return set_error(NBG_EINVAL, "ring_group: ticket %llu was not posted", (unsigned long long)ticket);
+  if (r->posted - ticket > r->slots)
+    return set_error(NBG_EINVAL, "ring_group: ticket %llu is older than the ring's %u slots", (unsigned long long)ticket,
+                     r->slots);
+  ring_refresh(r);
+  DeviceGuard g(r->h->device);
+  const auto [backend, n_pkts] = r->rec[ticket & (r->slots - 1)];
+  const uint32_t nbins = r->h->nb + 1;
+  nbg_ring::GroupSet* gs = nullptr;
+  int rc = ring_gset(r, s, &gs);
+  if (rc) return rc;
   if (n_pkts == 0) {
     NBG_HIP(hipMemsetAsync(d_counts, 0, nbins * 4, s));
     return NBG_OK;
+  }
+  if (ticket >= r->completed) {  // not complete yet: the stream waits for it on the device
+    const uint32_t* dcomp = reinterpret_cast<const uint32_t*>(r->dev + kDevComp);
+    const uint32_t* dexit = reinterpret_cast<const uint32_t*>(r->dev + kDevExit);
+    if ((rc = launch_ring_gate(dcomp, dexit, static_cast<uint32_t>(ticket + 1), static_cast<uint32_t>(r->grid), s)))
+      return rc;
   }
   const uint64_t per = (n_pkts + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
   const uint32_t part_pkts = static_cast<uint32_t>(per * kChunk);
@@ -1467,8 +1442,7 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
   ha.part_pkts = part_pkts;
   ha.n_parts = n_parts;
   ha.part_hist = gs->rows;
-  int rc = launch_hist(ha, s);
-  if (rc) return rc;
+  if ((rc = launch_hist(ha, s))) return rc;
   const int scan = pick_group_scan(nbins, n_parts);
   if (scan == kScanKernel) {
     ScanArgs sa{};
@@ -1497,6 +1471,241 @@ int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_c
   return launch_group(ga, scan, s);
 }
 
+// Batches first .. first + n - 1 grouped by one gate, one hist and one group launch on s (a
+// producer's burst: launches per batch would cost more host time than a shard-size batch takes on
+// the device).  Falls back to one grouping per batch where the multi-batch launches do not apply
+// (an empty batch, grouping through the scan kernel).  Under r->mu.
+int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* const* d_perm,
+                            uint32_t* const* d_counts, hipStream_t s) {
+  if (n == 0 || n > kMaxMulti) return set_error(NBG_EINVAL, "ring_group_burst: 1..%u batches", kMaxMulti);
+  const uint64_t last = first + n - 1;
+  if (last >= r->posted)
+    return set_error(NBG_EINVAL, "ring_group_burst: ticket %llu was not posted", (unsigned long long)last);
+  if (r->posted - first > r->slots)
+    return set_error(NBG_EINVAL, "ring_group_burst: ticket %llu is older than the ring's %u slots",
+                     (unsigned long long)first, r->slots);
+  for (uint32_t j = 0; j < n; ++j)
+    if (!d_perm[j] || !d_counts[j]) return set_error(NBG_EINVAL, "ring_group_burst: null output of batch %u", j);
+  const uint32_t nbins = r->h->nb + 1;
+  uint64_t max_n = 0;
+  bool empty = false;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t m = r->rec[(first + j) & (r->slots - 1)].second;
+    max_n = std::max(max_n, m);
+    empty = empty || m == 0;
+  }
+  const uint64_t per = (max_n + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
+  const uint32_t part_pkts = static_cast<uint32_t>(std::max<uint64_t>(per, 1) * kChunk);
+  const uint32_t n_parts_max = static_cast<uint32_t>((max_n + part_pkts - 1) / part_pkts);
+  const int scan = pick_group_scan(nbins, n_parts_max);
+  if (empty || scan == kScanKernel || n == 1) {
+    for (uint32_t j = 0; j < n; ++j) {
+      const int rc = ring_group_locked(r, first + j, d_perm[j], d_counts[j], s);
+      if (rc) return rc;
+    }
+    return NBG_OK;
+  }
+  ring_refresh(r);
+  DeviceGuard g(r->h->device);
+  nbg_ring::GroupSet* gs = nullptr;
+  int rc = ring_gset(r, s, &gs);
+  if (rc) return rc;
+  if (last >= r->completed) {  // batches complete in ring order: waiting for the last covers all
+    const uint32_t* dcomp = reinterpret_cast<const uint32_t*>(r->dev + kDevComp);
+    const uint32_t* dexit = reinterpret_cast<const uint32_t*>(r->dev + kDevExit);
+    if ((rc = launch_ring_gate(dcomp, dexit, static_cast<uint32_t>(last + 1), static_cast<uint32_t>(r->grid), s)))
+      return rc;
+  }
+  HistMulti hm{};
+  GroupMulti gm{};
+  uint32_t bits = 0;
+  while ((1u << bits) < nbins) ++bits;
+  for (uint32_t j = 0; j < n; ++j) {
+    const auto [backend, n_pkts] = r->rec[(first + j) & (r->slots - 1)];
+    uint32_t* rows = gs->rows + static_cast<size_t>(j) * kMaxParts * nbins;
+    HistArgs& ha = hm.h[j];
+    ha.backend = backend;
+    ha.n_pkts = static_cast<uint32_t>(n_pkts);
+    ha.nb = r->h->nb;
+    ha.part_pkts = part_pkts;
+    ha.n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
+    ha.part_hist = rows;
+    GroupArgs& ga = gm.g[j];
+    ga.backend = backend;
+    ga.n_pkts = static_cast<uint32_t>(n_pkts);
+    ga.nb = r->h->nb;
+    ga.bits = bits;
+    ga.n_parts = ha.n_parts;
+    ga.part_pkts = part_pkts;
+    ga.part_hist = rows;
+    ga.hist16 = 0;
+    ga.counts = d_counts[j];
+    ga.perm = d_perm[j];
+  }
+  hm.per = n_parts_max;
+  gm.per = n_parts_max;
+  if ((rc = launch_hist_multi(hm, n, s))) return rc;
+  return launch_group_multi(gm, n, scan, s);
+}
+
+// Wait until `done()` holds, the ring has gone, or timeout_ms (0: none).  `done` runs under r->mu
+// after a refresh.
+template <typename F>
+int ring_wait_for(nbg_ring* r, uint32_t timeout_ms, const char* what, uint64_t ticket, F done) {
+  const auto t0 = Clock::now();
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> g(r->mu);
+      ring_refresh(r);
+      if (done()) return NBG_OK;
+      if (ring_gone(r)) {
+        ring_refresh(r);  // progress stored before the kernel ended
+        if (done()) return NBG_OK;
+        return ring_state_error(r);
+      }
+    }
+    if (timeout_ms && Clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+      return set_error(NBG_ETIMEDOUT, "%s: batch %llu not complete after %u ms", what, (unsigned long long)ticket,
+                       timeout_ms);
+    ring_pause(t0);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t flags, uint32_t idle_ms, void* stream,
+                   nbg_ring** out) {
+  if (!h || !out) return set_error(NBG_EINVAL, "ring_start: null argument");
+  *out = nullptr;
+  if (h->ring) return set_error(NBG_EBUSY, "ring_start: the handle already runs a ring");
+  if (h->wide || h->m > 65537) return set_error(NBG_EINVAL, "ring_start: needs <= 255 backends and M <= 65537");
+  if (stride % 16 || stride < 64 || stride >= (1u << 24) || fixed_len < 48)
+    return set_error(NBG_EINVAL, "ring_start: fixed slots with stride %% 16 == 0, 64 <= stride < 2^24, fixed_len >= 48");
+  if (flags & ~NBG_SWAP_MACS) return set_error(NBG_EINVAL, "ring_start: flags other than NBG_SWAP_MACS");
+  if (h->pending) return set_error(NBG_EINVAL, "ring_start: a deferred or lagged group is pending");
+  if (h->cus < 2) return set_error(NBG_EINVAL, "ring_start: needs a CU for the relay beside the classify blocks");
+  // one ring per GPU: a second one's blocks could never all become resident beside the first
+  std::lock_guard<std::mutex> dev_lock(g_dev_ring_mu);
+  if (static_cast<size_t>(h->device) < g_dev_ring.size() && g_dev_ring[h->device])
+    return set_error(NBG_EBUSY,
+                     "ring_start: device %d already runs a persistent ring (one per GPU; RX queues share it through "
+                     "nbg_ring_queue_open)",
+                     h->device);
+  DeviceGuard g(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  int rc = order_after_last(h, s);  // the ring runs after the handle's earlier work
+  if (rc) return rc;
+  // a stopped ring's buffers, stream and events are reused (a start then costs a memset and a launch)
+  nbg_ring* r = h->ring_spare;
+  h->ring_spare = nullptr;
+  if (!r && (rc = ring_alloc(h, &r))) return rc;
+  r->idle_ms = idle_ms ? idle_ms : 2000u;
+  r->moved = Clock::now();
+  r->posted = r->units = r->completed = 0;
+  r->ended = false;
+  r->rec.assign(r->slots, {nullptr, 0});
+  std::memset(r->host, 0, r->hbytes);
+  {
+    // after everything issued on `stream` so far, in the private stream's order: zero the device
+    // ring, then the kernel
+    hipEvent_t ev = nullptr;
+    const bool ok = hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess &&
+                    hipEventRecord(ev, s) == hipSuccess && hipStreamWaitEvent(r->stream, ev, 0) == hipSuccess &&
+                    hipMemsetAsync(r->dev, 0, r->dbytes, r->stream) == hipSuccess;
+    if (ev) (void)hipEventDestroy(ev);
+    if (!ok) {
+      ring_free(r);
+      return set_error(NBG_EIO, "ring_start: ordering after the caller's stream");
+    }
+  }
+  uint8_t* hdev = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess) {
+    ring_free(r);
+    return set_error(NBG_EIO, "ring_start: device address of the pinned ring");
+  }
+  ClassifyArgs a{};
+  a.stride = stride;
+  a.fixed_len = fixed_len;
+  a.lut = h->d_lut;
+  a.m = static_cast<uint32_t>(h->m);
+  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
+  a.nb = h->nb;
+  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  a.win_owned = 1;
+  a.wb_full = 1;
+  a.lean = 1;
+  a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
+  a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
+  RingArgs ra{};
+  ra.ctl = reinterpret_cast<RingCtl*>(hdev);
+  ra.hdesc = reinterpret_cast<const RingDesc*>(hdev + sizeof(RingCtl));
+  ra.dstop = reinterpret_cast<uint32_t*>(r->dev + kDevStop);
+  ra.dcomp = reinterpret_cast<uint32_t*>(r->dev + kDevComp);
+  ra.dexit = reinterpret_cast<uint32_t*>(r->dev + kDevExit);
+  ra.prog = reinterpret_cast<uint32_t*>(r->dev + kDevProg);
+  ra.desc = reinterpret_cast<RingDesc*>(r->dev + ring_desc_off(r->grid));
+  ra.slots = r->slots;
+  ra.reps = r->reps;
+  ra.grid = static_cast<uint32_t>(r->grid);
+  ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
+  const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
+  ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
+  (void)hipEventRecord(r->ev_start, r->stream);
+  if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, r->stream))) {
+    ring_free(r);
+    return rc;
+  }
+  (void)hipEventRecord(r->ev_end, r->stream);
+  if (static_cast<size_t>(h->device) >= g_dev_ring.size()) g_dev_ring.resize(h->device + 1, nullptr);
+  g_dev_ring[h->device] = r;
+  h->ring_kernel_ms = -1.f;
+  h->ring = r;
+  h->last_stream = s;
+  h->issued = true;
+  *out = r;
+  return NBG_OK;
+}
+
+int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_batches, uint32_t* n_posted,
+                        uint64_t* first_ticket) {
+  if (!r || !n_posted || !first_ticket || (n_batches && !batches))
+    return set_error(NBG_EINVAL, "ring_post_burst: null argument");
+  *n_posted = 0;
+  for (uint32_t i = 0; i < n_batches; ++i) {
+    const int rc = ring_check_batch(batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
+    if (rc) return rc;
+  }
+  std::lock_guard<std::mutex> g(r->mu);
+  *first_ticket = r->posted;
+  ring_refresh(r);
+  if (ring_gone(r)) return ring_state_error(r);
+  const uint64_t room = r->slots - (r->posted - r->completed);
+  const uint32_t k = static_cast<uint32_t>(std::min<uint64_t>(room, n_batches));
+  for (uint32_t i = 0; i < k; ++i) ring_put(r, batches[i].d_pkts, batches[i].n_pkts, batches[i].d_backend);
+  *n_posted = k;
+  return NBG_OK;
+}
+
+int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
+  if (!r || !ticket) return set_error(NBG_EINVAL, "ring_post: null argument");
+  return ring_post_one(r, nullptr, d_pkts, n_pkts, d_backend, ticket);
+}
+
+int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
+  if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group: null argument");
+  std::lock_guard<std::mutex> g(r->mu);
+  return ring_group_locked(r, ticket, d_perm, d_counts, static_cast<hipStream_t>(stream));
+}
+
+int nbg_ring_group_burst(nbg_ring* r, uint64_t first_ticket, uint32_t n_batches, uint32_t* const* d_perm,
+                         uint32_t* const* d_counts, void* stream) {
+  if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group_burst: null argument");
+  std::lock_guard<std::mutex> g(r->mu);
+  return ring_group_burst_locked(r, first_ticket, n_batches, d_perm, d_counts, static_cast<hipStream_t>(stream));
+}
+
 // Diagnostics (not in include/nbgpu.h): the host control line's 16 words.
 int nbg_debug_ring_ctl(nbg_ring* r, uint32_t* out) {
   if (!r || !out) return NBG_EINVAL;
@@ -1514,6 +1723,7 @@ int nbg_ring_kernel_ms(nbg_maglev* h, float* ms) {
 
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
   if (!r || !completed) return set_error(NBG_EINVAL, "ring_poll: null argument");
+  std::lock_guard<std::mutex> g(r->mu);
   ring_refresh(r);
   *completed = r->completed;
   if (r->completed < r->posted && ring_gone(r)) return ring_state_error(r);
@@ -1522,21 +1732,12 @@ int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
 
 int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms) {
   if (!r) return set_error(NBG_EINVAL, "ring_wait: null ring");
-  if (ticket >= r->posted) return set_error(NBG_EINVAL, "ring_wait: ticket %llu was not posted", (unsigned long long)ticket);
-  const auto t0 = Clock::now();
-  for (;;) {
-    ring_refresh(r);
-    if (r->completed > ticket) return NBG_OK;
-    if (ring_gone(r)) {
-      ring_refresh(r);  // progress stored before the kernel ended
-      if (r->completed > ticket) return NBG_OK;
-      return ring_state_error(r);
-    }
-    if (timeout_ms && Clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
-      return set_error(NBG_ETIMEDOUT, "ring_wait: batch %llu not complete after %u ms", (unsigned long long)ticket,
-                       timeout_ms);
-    ring_pause(t0);
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    if (ticket >= r->posted)
+      return set_error(NBG_EINVAL, "ring_wait: ticket %llu was not posted", (unsigned long long)ticket);
   }
+  return ring_wait_for(r, timeout_ms, "ring_wait", ticket, [&] { return r->completed > ticket; });
 }
 
 int nbg_ring_stop(nbg_ring* r) {
@@ -1545,13 +1746,21 @@ int nbg_ring_stop(nbg_ring* r) {
   __atomic_store_n(&const_cast<RingCtl*>(const_cast<volatile RingCtl*>(r->ctl))->stop, 1u, __ATOMIC_RELEASE);
   const auto t0 = Clock::now();
   int rc = NBG_OK;
+  std::unique_lock<std::mutex> lk(r->mu);
   while (!ring_ended(r)) {
     if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 5000u)) {
-      // never free memory a running kernel may still read: leak the ring instead
+      // never free memory a running kernel may still read: leak the ring (and the handle's device
+      // memory, nbg_maglev_destroy) instead; the device stays marked busy
       r->h->ring = nullptr;
-      return set_error(NBG_ETIMEDOUT, "ring_stop: the kernel did not end");
+      r->h->ring_leaked = true;
+      return set_error(NBG_EBUSY, "ring_stop: the kernel did not end (its memory is leaked, the device stays busy)");
     }
     ring_pause(t0);
+  }
+  {
+    std::lock_guard<std::mutex> dg(g_dev_ring_mu);
+    if (static_cast<size_t>(r->h->device) < g_dev_ring.size() && g_dev_ring[r->h->device] == r)
+      g_dev_ring[r->h->device] = nullptr;
   }
   const hipError_t e = hipStreamQuery(r->stream);
   ring_refresh(r);
@@ -1561,20 +1770,85 @@ int nbg_ring_stop(nbg_ring* r) {
   h->ring = nullptr;
   float ms = -1.f;
   if (e == hipSuccess && hipEventElapsedTime(&ms, r->ev_start, r->ev_end) == hipSuccess) h->ring_kernel_ms = ms;
+  ring_close_queues(r);
   if (e != hipSuccess) {
+    lk.unlock();  // ring_free deletes the mutex
     ring_free(r);
     return rc;
   }
   // keep the buffers, stream and events for the next start; the grouping streams' work on the
   // scratch is finished first
-  for (auto& g : r->gsets) {
-    if (g.s) (void)hipStreamSynchronize(g.s);
-    g.s = nullptr;
-    g.used = 0;
-  }
-  r->gcalls = 0;
+  ring_release_sets(r);
   h->ring_spare = r;
   return rc;
+}
+
+int nbg_ring_queue_open(nbg_ring* r, nbg_ring_queue** out) {
+  if (!r || !out) return set_error(NBG_EINVAL, "ring_queue_open: null argument");
+  *out = nullptr;
+  std::lock_guard<std::mutex> g(r->mu);
+  if (r->queues.size() >= NBG_RING_MAX_QUEUES)
+    return set_error(NBG_EBUSY, "ring_queue_open: the ring has %u queues open", NBG_RING_MAX_QUEUES);
+  auto* q = new (std::nothrow) nbg_ring_queue;
+  if (!q) return set_error(NBG_ENOMEM, "ring_queue_open: out of memory");
+  q->r = r;
+  r->queues.push_back(q);
+  *out = q;
+  return NBG_OK;
+}
+
+int nbg_ring_queue_close(nbg_ring_queue* q) {
+  if (!q) return set_error(NBG_EINVAL, "ring_queue_close: null queue");
+  nbg_ring* r = q->r;
+  std::lock_guard<std::mutex> g(r->mu);
+  auto it = std::find(r->queues.begin(), r->queues.end(), q);
+  if (it == r->queues.end()) return set_error(NBG_EINVAL, "ring_queue_close: not an open queue of its ring");
+  r->queues.erase(it);
+  delete q;
+  return NBG_OK;
+}
+
+int nbg_ring_queue_post(nbg_ring_queue* q, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_backend, uint64_t* ticket) {
+  if (!q || !ticket) return set_error(NBG_EINVAL, "ring_queue_post: null argument");
+  return ring_post_one(q->r, q, d_pkts, n_pkts, d_backend, ticket);
+}
+
+int nbg_ring_queue_poll(nbg_ring_queue* q, uint64_t* completed) {
+  if (!q || !completed) return set_error(NBG_EINVAL, "ring_queue_poll: null argument");
+  nbg_ring* r = q->r;
+  std::lock_guard<std::mutex> g(r->mu);
+  ring_refresh(r);
+  queue_refresh(q);
+  *completed = q->done;
+  if (q->done < q->posted && ring_gone(r)) return ring_state_error(r);
+  return NBG_OK;
+}
+
+int nbg_ring_queue_wait(nbg_ring_queue* q, uint64_t ticket, uint32_t timeout_ms) {
+  if (!q) return set_error(NBG_EINVAL, "ring_queue_wait: null queue");
+  nbg_ring* r = q->r;
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    if (ticket >= q->posted)
+      return set_error(NBG_EINVAL, "ring_queue_wait: ticket %llu was not posted on this queue",
+                       (unsigned long long)ticket);
+  }
+  return ring_wait_for(r, timeout_ms, "ring_queue_wait", ticket, [&] {
+    queue_refresh(q);
+    return q->done > ticket;
+  });
+}
+
+int nbg_ring_queue_group(nbg_ring_queue* q, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
+  if (!q || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_queue_group: null argument");
+  nbg_ring* r = q->r;
+  std::lock_guard<std::mutex> g(r->mu);
+  if (ticket >= q->posted)
+    return set_error(NBG_EINVAL, "ring_queue_group: ticket %llu was not posted on this queue", (unsigned long long)ticket);
+  if (q->posted - ticket > NBG_RING_SLOTS)
+    return set_error(NBG_EINVAL, "ring_queue_group: ticket %llu is older than the queue's last %u", (unsigned long long)ticket,
+                     NBG_RING_SLOTS);
+  return ring_group_locked(r, q->gidx[ticket % NBG_RING_SLOTS], d_perm, d_counts, static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"
@@ -1670,6 +1944,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   if (!h || !ticket || (!pkt_ptrs && n) || (!lens && n) || (!backend_out && n))
     return set_error(NBG_EINVAL, "host_submit: null argument");
   if (n >= (1ull << 30)) return set_error(NBG_EINVAL, "host_submit: n must be < 2^30");
+  if (h->ring) return set_error(NBG_EBUSY, "host_submit: the handle's persistent ring is running");
   if (h->pending && !h->pending_lag)
     return set_error(NBG_EINVAL, "host_submit: a deferred group is pending (nbg_maglev_finish_group)");
   DeviceGuard g(h->device);

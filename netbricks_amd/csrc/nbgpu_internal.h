@@ -111,7 +111,7 @@ struct LagGroup {
 
 // Persistent RX-ring classify (nbg_ring_*).  One batch per ring slot (64 B, one line), written by
 // nbg_ring_post into pinned host memory.  No classify CU ever touches host memory: a one-wave relay
-// kernel on a CU of its own (ring_relay_kernel) copies each posted descriptor into a device ring in
+// (the ring kernel's last block, on a CU of its own: ring_relay) copies each posted descriptor into a device ring in
 // uncached HBM (`reps` replicas, block b reads replica b % reps), forwards the host's stop, and
 // reports the minimum of the blocks' per-block completion counts (also uncached HBM) to the host.
 // Measured before the relay: with every classify block reading host memory, the per-batch time
@@ -138,6 +138,8 @@ struct RingArgs {
   const RingDesc* hdesc;  // host [slots]: read by the relay only
   RingDesc* desc;         // device, uncached [reps][slots]: the classify blocks' descriptors
   uint32_t* dstop;        // device, uncached: relay -> blocks, every posted batch is relayed and stop was asked
+  uint32_t* dcomp;        // device, uncached: relay, batches complete on every block (the gate kernels poll it)
+  uint32_t* dexit;        // device, uncached: classify blocks that have exited (their stores retired)
   uint32_t* prog;         // device, uncached [grid]: per block, batches all of whose units of it are complete
   uint32_t slots;         // power of two
   uint32_t reps;          // power of two: replicas of the device ring
@@ -183,6 +185,12 @@ struct HistArgs {
   uint32_t part_pkts;
   uint32_t n_parts;
   uint32_t* part_hist;      // [n_parts][nb+1], every entry stored
+};
+
+// hist_kernel over several batches: blocks [j * per, j * per + h[j].n_parts) count batch j.
+struct HistMulti {
+  HistArgs h[kMaxMulti];
+  uint32_t per;
 };
 
 struct ScanArgs {
@@ -237,6 +245,10 @@ size_t stream_lds(uint32_t nb, int mode, bool lag);
 // read only, 1 MAC swap in place.  Returns after the launch; the kernel runs until stop or idle.
 int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int grid, void* stream);
 size_t ring_lds(int mode);
+// One wave on `stream` that returns once the ring has completed `target` batches (dcomp, mod 2^32) or
+// every one of its `grid` classify blocks has exited (dexit): the stream's later launches (a ring
+// batch's grouping) run after the batch is in HBM, with no host round trip.
+int launch_ring_gate(const uint32_t* dcomp, const uint32_t* dexit, uint32_t target, uint32_t grid, void* stream);
 int stream_waves_per_block();
 // Streaming classify for descriptor layouts with owned windows (u8 LUT in LDS, or the u16 LUT
 // gathered from L2); stream_desc_lds: its dynamic LDS bytes (mode 0 read only, 1 in place, 2 records).
@@ -245,6 +257,7 @@ size_t stream_desc_lds(uint32_t nb, int mode, bool wide_lut);
 int launch_scan(const ScanArgs& a, void* stream);
 int launch_zero(uint32_t* p, size_t words, void* stream);  // p[0, words) = 0 (one kernel)
 int launch_hist(const HistArgs& a, void* stream);
+int launch_hist_multi(const HistMulti& hm, uint32_t n, void* stream);  // nb + 1 <= 16384
 bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
                       uint16_t* gate, void* stream);

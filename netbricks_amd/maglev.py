@@ -20,7 +20,7 @@ from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, 
                    NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch, NbgRingBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
-__all__ = ["Maglev", "GroupedBatch", "Ring", "build_lut", "make_trace", "NBG_SENTINEL"]
+__all__ = ["Maglev", "GroupedBatch", "Ring", "RingQueue", "build_lut", "make_trace", "NBG_SENTINEL"]
 
 
 def _ptr(t) -> Optional[int]:
@@ -354,6 +354,8 @@ class Ring:
         self._r = h
         self._held = {}  # ticket -> tensors the kernel reads or writes until the batch is complete
         self._sizes = {}  # ticket -> n_pkts, for the last NBG_RING_SLOTS posts (group() checks perm)
+        self._groups = []  # (event, tensors) of enqueued groupings, until their stream ran them
+        self._queues = []
         mg._ring = self  # Maglev.close() stops the ring first (the handle frees it otherwise)
 
     def post(self, pkts, n_pkts: int, backend) -> int:
@@ -402,8 +404,10 @@ class Ring:
         return k.value, t.value
 
     def group(self, ticket: int, perm, counts, stream=None) -> None:
-        """perm / counts of a completed batch (nbg_ring_group) on `stream` (default: torch's current
-        stream)."""
+        """perm / counts of batch `ticket` (nbg_ring_group) on `stream` (default: torch's current
+        stream).  The batch need not be complete: a gate kernel on the stream waits for it, so the
+        grouping can be enqueued right after the post.  The tensors are held until the stream has run
+        the grouping."""
         import torch
 
         if self._r is None:
@@ -412,8 +416,8 @@ class Ring:
         _check_dev("perm", perm, torch.uint32, self._sizes.get(ticket, 0), dev)
         _check_dev("counts", counts, torch.uint32, self._mg.n_backends + 1, dev)
         st = stream if stream is not None else torch.cuda.current_stream(dev)
-        st = st.cuda_stream if hasattr(st, "cuda_stream") else st
-        check(lib.nbg_ring_group(self._r, ticket, _ptr(perm), _ptr(counts), st), "nbg_ring_group")
+        check(lib.nbg_ring_group(self._r, ticket, _ptr(perm), _ptr(counts), _stream_ptr(st)), "nbg_ring_group")
+        _hold_until_run(self._groups, st, dev, (self._held.get(ticket), perm, counts))
 
     def poll(self) -> int:
         c = C.c_uint64()
@@ -427,12 +431,53 @@ class Ring:
         for k in [k for k in self._held if k <= ticket]:
             del self._held[k]
 
+    def group_burst(self, first: int, perms, counts, stream=None) -> None:
+        """perm / counts of the len(perms) consecutive batches first.. (nbg_ring_group_burst: one gate,
+        one hist and one group launch for all of them)."""
+        import torch
+
+        if self._r is None:
+            raise RuntimeError("ring: stopped")
+        n = len(perms)
+        if n != len(counts) or not 1 <= n <= NBG_MAX_MULTI:
+            raise ValueError(f"perms / counts: 1..{NBG_MAX_MULTI} batches each")
+        dev = torch.device("cuda", self._mg.device)
+        for j in range(n):
+            _check_dev("perm", perms[j], torch.uint32, self._sizes.get(first + j, 0), dev)
+            _check_dev("counts", counts[j], torch.uint32, self._mg.n_backends + 1, dev)
+        pa = (C.c_void_p * n)(*[_ptr(p) for p in perms])
+        ca = (C.c_void_p * n)(*[_ptr(c) for c in counts])
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(lib.nbg_ring_group_burst(self._r, first, n, pa, ca, _stream_ptr(st)), "nbg_ring_group_burst")
+        _hold_until_run(self._groups, st, dev, ([self._held.get(first + j) for j in range(n)], list(perms),
+                                                list(counts)))
+
+    def queue(self) -> "RingQueue":
+        """Open an RX queue on this ring (nbg_ring_queue_open): its own tickets, completion and grouping
+        over the shared ring (one pipeline per RSS queue, scheduler/context.rs:241-255)."""
+        if self._r is None:
+            raise RuntimeError("ring: stopped")
+        q = RingQueue(self)
+        self._queues.append(q)
+        return q
+
     def stop(self) -> None:
+        """nbg_ring_stop: every posted batch completes, the kernel ends, the ring's queues close.  The
+        tensors the kernel reads or writes are released only once it has ended; if the stop times out
+        (the kernel may still run) they are parked for the life of the process."""
         if self._r is not None:
             r, self._r = self._r, None
-            self._held.clear()
             self._mg.__dict__.pop("_ring", None)
-            check(lib.nbg_ring_stop(r), "nbg_ring_stop")
+            rc = lib.nbg_ring_stop(r)
+            keep = (self._held, self._groups, [q._held for q in self._queues])
+            for q in self._queues:
+                q._q = None
+            if rc == _lib.NBG_EBUSY:
+                _LEAKED.append(keep)  # the kernel did not end: never hand its memory back to torch
+            else:
+                self._held = {}
+                self._groups = []
+            check(rc, "nbg_ring_stop")
 
     def __enter__(self):
         return self
@@ -445,6 +490,92 @@ class Ring:
             self.stop()
         except Exception:  # noqa: BLE001 (interpreter teardown)
             pass
+
+
+_LEAKED = []  # tensors of rings whose kernel did not end at stop (never returned to torch's allocator)
+
+
+def _stream_ptr(st):
+    return st.cuda_stream if hasattr(st, "cuda_stream") else st
+
+
+def _hold_until_run(groups: list, st, dev, refs) -> None:
+    """Keep `refs` alive until the work just enqueued on stream `st` has run (an event behind it),
+    pruning entries whose event has passed."""
+    import torch
+
+    while groups and groups[0][0].query():
+        groups.pop(0)
+    ev = torch.cuda.Event()
+    if hasattr(st, "cuda_stream"):
+        ev.record(st)
+    else:
+        ev.record(torch.cuda.ExternalStream(st, device=dev))
+    groups.append((ev, refs))
+
+
+class RingQueue:
+    """One RX queue on a device's ring (nbg_ring_queue_*): its own tickets 0, 1, 2, ..., completion and
+    grouping; the batches of every queue of the ring share its slots in post order.  One thread per
+    queue; queues of one ring may post from different threads."""
+
+    def __init__(self, ring: "Ring"):
+        self._ring = ring
+        h = C.c_void_p()
+        check(lib.nbg_ring_queue_open(ring._r, C.byref(h)), "nbg_ring_queue_open")
+        self._q = h
+        self._held = {}
+        self._sizes = {}
+        self._groups = []
+
+    def post(self, pkts, n_pkts: int, backend) -> int:
+        import torch
+
+        if self._q is None:
+            raise RuntimeError("ring queue: closed")
+        r = self._ring
+        dev = torch.device("cuda", r._mg.device)
+        if pkts.dtype != torch.uint8 or not pkts.is_contiguous() or pkts.device != dev:
+            raise ValueError(f"pkts: expected a contiguous uint8 tensor on {dev}")
+        if n_pkts and pkts.numel() < (n_pkts - 1) * r.stride + _slot_tail(r.stride, r.frame_len):
+            raise ValueError("pkts: too small for n_pkts slots")
+        _check_dev("backend", backend, torch.uint16, n_pkts, dev)
+        t = C.c_uint64()
+        check(lib.nbg_ring_queue_post(self._q, _ptr(pkts), n_pkts, _ptr(backend), C.byref(t)), "nbg_ring_queue_post")
+        self._held[t.value] = (pkts, backend)
+        self._sizes[t.value] = n_pkts
+        self._sizes.pop(t.value - _lib.NBG_RING_SLOTS, None)
+        return t.value
+
+    def poll(self) -> int:
+        c = C.c_uint64()
+        check(lib.nbg_ring_queue_poll(self._q, C.byref(c)), "nbg_ring_queue_poll")
+        for k in [k for k in self._held if k < c.value]:
+            del self._held[k]
+        return c.value
+
+    def wait(self, ticket: int, timeout_ms: int = 10000) -> None:
+        check(lib.nbg_ring_queue_wait(self._q, ticket, timeout_ms), "nbg_ring_queue_wait")
+        for k in [k for k in self._held if k <= ticket]:
+            del self._held[k]
+
+    def group(self, ticket: int, perm, counts, stream=None) -> None:
+        import torch
+
+        if self._q is None:
+            raise RuntimeError("ring queue: closed")
+        dev = torch.device("cuda", self._ring._mg.device)
+        _check_dev("perm", perm, torch.uint32, self._sizes.get(ticket, 0), dev)
+        _check_dev("counts", counts, torch.uint32, self._ring._mg.n_backends + 1, dev)
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(lib.nbg_ring_queue_group(self._q, ticket, _ptr(perm), _ptr(counts), _stream_ptr(st)),
+              "nbg_ring_queue_group")
+        _hold_until_run(self._groups, st, dev, (self._held.get(ticket), perm, counts))
+
+    def close(self) -> None:
+        if self._q is not None:
+            q, self._q = self._q, None
+            check(lib.nbg_ring_queue_close(q), "nbg_ring_queue_close")
 
 
 class HostRegion:

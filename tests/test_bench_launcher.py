@@ -34,6 +34,15 @@ def test_launcher_spawns_ranks(n):
     assert line["lut_digest"].startswith(line["lut_digest_per_rank"][0])
     assert line["config"]["parallelism"] == f"shard{n}"
     assert line["scaling"] == "weak"
+    # config C4: one 1M batch in n contiguous shards, one per rank; with N > 1
+    # the scatter / classify / gather pass ran (gloo here) and rank 0's gathered counts summed to 1M
+    c4 = line["c4"]
+    assert c4["shards"] == n and c4["shard_pkts"] * n == c4["batch_pkts"] == 1 << 20
+    assert len(c4["device_resident"]["per_gpu_mpps"]) == n
+    if n > 1:
+        assert c4["scatter_inclusive"]["checked"] is True and c4["scatter_inclusive"]["steps"] > 0
+    else:
+        assert "scatter_inclusive" not in c4
 
 
 def test_rank_rejects_world_mismatch():

@@ -242,3 +242,295 @@ def test_ring_refuses_unsupported(torch_cuda):
         with pytest.raises(nb.NbgError):
             ring.post(d[8:], 10, out)  # misaligned packet buffer
     mg.close()
+
+
+def _slices(rng, count, lo, hi):
+    """`count` batch sizes in [lo, hi) laid out back to back in one trace, every batch starting on a
+    multiple of 8 packets (16-B aligned backend slices): [(start, n)], total packets."""
+    out, pos = [], 0
+    for n in rng.integers(lo, hi, count):
+        out.append((pos, int(n)))
+        pos += (int(n) + 7) & ~7
+    return out, pos
+
+
+@pytest.mark.parametrize("swap", [False, True])
+def test_ring_1200_batches_wraparound(torch_cuda, swap):
+    """1,200 batches (about 19 wraps of the 64 slots and of the relay's descriptor replicas), posted in
+    RX bursts as slots free up: slices of one 10M-packet trace, each classified once, so one oracle
+    pass over the trace checks every batch's backend[] and (in place) its bytes."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    rng = np.random.default_rng(1200 + swap)
+    batches, total = _slices(rng, 1200, 1, 16000)
+    buf = nb.make_trace(total, 0, seed=4242 + swap)[0]
+    d = torch.from_numpy(buf.copy()).cuda()
+    out = torch.full((total,), 0x7777, dtype=torch.int16, device="cuda").view(torch.uint16)
+    torch.cuda.synchronize()
+    with mg.ring(swap_macs=swap) as ring:
+        nxt = 0
+        while nxt < len(batches):
+            offer = [(d[s * 64:], n, out[s:]) for s, n in batches[nxt:nxt + 40]]
+            k, first = ring.post_burst(offer)
+            assert first == nxt
+            nxt += k
+            if k == 0:
+                ring.wait(nxt - 64)
+        ring.wait(len(batches) - 1)
+        assert ring.poll() == len(batches)
+    got = _got(torch, out)
+    ref = buf.copy()
+    be = orc.classify(ref, total, lut, stride=64, fixed_len=60, swap=swap)
+    covered = np.zeros(total, dtype=bool)
+    for s, n in batches:
+        covered[s:s + n] = True
+    np.testing.assert_array_equal(got[covered], be[covered])
+    assert (got[~covered] == 0x7777).all()  # the alignment gaps are no batch's packets
+    byte_mask = np.repeat(covered, 64)
+    now = d.cpu().numpy()
+    np.testing.assert_array_equal(now[byte_mask], ref[byte_mask])
+    np.testing.assert_array_equal(now[~byte_mask], buf[~byte_mask])
+    mg.close()
+
+
+def test_ring_group_gated_mixed_streams(torch_cuda):
+    """nbg_ring_group enqueued right after each post, before the batch is complete (a gate kernel
+    waits on the stream), alternating torch's default stream (the null stream: ADVICE r3) with side
+    streams so that the scratch sets change owners; perm / counts bit-exact for every batch."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    sizes = [131072, 4097, 1 << 20, 65536, 300001, 777, 131072, 262144, 1, 524288, 9000, 131072]
+    bufs = [nb.make_trace(n, 0, seed=1300 + i)[0] for i, n in enumerate(sizes)]
+    d = [torch.from_numpy(b.copy()).cuda() for b in bufs]
+    outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for n in sizes]
+    perms = [torch.empty(n, dtype=torch.uint32, device="cuda") for n in sizes]
+    counts = [torch.zeros(66, dtype=torch.uint32, device="cuda") for _ in sizes]
+    sides = [torch.cuda.Stream() for _ in range(5)]
+    torch.cuda.synchronize()
+    with mg.ring(swap_macs=True) as ring:
+        for i, n in enumerate(sizes):
+            t = ring.post(d[i], n, outs[i])
+            st = None if i % 3 == 0 else sides[i % 5]  # None: torch's current (default) stream
+            ring.group(t, perms[i], counts[i], stream=st)
+        ring.wait(len(sizes) - 1)
+        for st in sides:
+            st.synchronize()
+        torch.cuda.current_stream().synchronize()  # the null stream's groups (the ring is on its own stream)
+    for i, n in enumerate(sizes):
+        be, _ = _expect(bufs[i], n, lut, True)
+        np.testing.assert_array_equal(_got(torch, outs[i]), be, err_msg=f"batch {i} ({n}) backend")
+        exp_perm, exp_cnt = orc.group(be, 65)
+        np.testing.assert_array_equal(_np32(torch, perms[i]), exp_perm, err_msg=f"batch {i} ({n}) perm")
+        np.testing.assert_array_equal(_np32(torch, counts[i]), exp_cnt, err_msg=f"batch {i} ({n}) counts")
+    mg.close()
+
+
+@pytest.mark.parametrize("n_queues", [2, 4])
+def test_ring_queues_interleaved(torch_cuda, n_queues):
+    """Several RX queues on one ring (nbg_ring_queue_*): each queue's tickets run 0, 1, 2, ...
+    whatever the interleaving, its completion count and grouping are its own, and every batch is
+    bit-exact against the oracle run on that batch alone (120 batches through the 64 shared slots)."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    rng = np.random.default_rng(50 + n_queues)
+    per_q = 120 // n_queues
+    sizes = [[int(x) for x in rng.integers(1, 70000, per_q)] for _ in range(n_queues)]
+    bufs = [[nb.make_trace(n, 0, seed=2000 + 100 * q + i)[0] for i, n in enumerate(sz)] for q, sz in enumerate(sizes)]
+    d = [[torch.from_numpy(b.copy()).cuda() for b in bq] for bq in bufs]
+    outs = [[torch.empty(n, dtype=torch.uint16, device="cuda") for n in sz] for sz in sizes]
+    perms = [[torch.empty(n, dtype=torch.uint32, device="cuda") for n in sz] for sz in sizes]
+    counts = [[torch.zeros(66, dtype=torch.uint32, device="cuda") for _ in sz] for sz in sizes]
+    sides = [torch.cuda.Stream() for _ in range(n_queues)]
+    torch.cuda.synchronize()
+    with mg.ring(swap_macs=True) as ring:
+        qs = [ring.queue() for _ in range(n_queues)]
+        order = rng.permutation(np.repeat(np.arange(n_queues), per_q))  # an arbitrary interleaving
+        nxt = [0] * n_queues
+        for q in order:
+            i = nxt[q]
+            t = qs[q].post(d[q][i], sizes[q][i], outs[q][i])
+            assert t == i  # per-queue tickets
+            qs[q].group(t, perms[q][i], counts[q][i], stream=sides[q])
+            nxt[q] += 1
+        for q in range(n_queues):
+            qs[q].wait(per_q - 1)
+            assert qs[q].poll() == per_q
+        assert ring.poll() == n_queues * per_q
+        for st in sides:
+            st.synchronize()
+        qs[0].close()
+        with pytest.raises(RuntimeError):
+            qs[0].post(d[0][0], sizes[0][0], outs[0][0])
+    for q in range(n_queues):
+        for i, n in enumerate(sizes[q]):
+            be, ref = _expect(bufs[q][i], n, lut, True)
+            np.testing.assert_array_equal(_got(torch, outs[q][i]), be, err_msg=f"queue {q} batch {i} backend")
+            np.testing.assert_array_equal(d[q][i].cpu().numpy(), ref, err_msg=f"queue {q} batch {i} bytes")
+            exp_perm, exp_cnt = orc.group(be, 65)
+            np.testing.assert_array_equal(_np32(torch, perms[q][i]), exp_perm, err_msg=f"queue {q} batch {i} perm")
+            np.testing.assert_array_equal(_np32(torch, counts[q][i]), exp_cnt, err_msg=f"queue {q} batch {i} counts")
+    mg.close()
+
+
+def test_ring_queues_from_threads(torch_cuda):
+    """Four producer threads, one RX queue each, posting and waiting concurrently (the ring's mutex);
+    every batch bit-exact."""
+    import threading
+
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    nq, per_q, n = 4, 40, 50000
+    bufs = [[nb.make_trace(n, 0, seed=3000 + 100 * q + i)[0] for i in range(per_q)] for q in range(nq)]
+    d = [[torch.from_numpy(b).cuda() for b in bq] for bq in bufs]
+    outs = [[torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(per_q)] for _ in range(nq)]
+    torch.cuda.synchronize()
+    errs = []
+    with mg.ring() as ring:
+        qs = [ring.queue() for _ in range(nq)]
+
+        def producer(q):
+            try:
+                for i in range(per_q):
+                    assert qs[q].post(d[q][i], n, outs[q][i]) == i
+                    if i % 7 == 6:
+                        qs[q].wait(i - 3)
+                qs[q].wait(per_q - 1)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        th = [threading.Thread(target=producer, args=(q,)) for q in range(nq)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not errs, errs
+        assert ring.poll() == nq * per_q
+    for q in range(nq):
+        for i in range(per_q):
+            np.testing.assert_array_equal(_got(torch, outs[q][i]), _expect(bufs[q][i], n, lut, False)[0])
+    mg.close()
+
+
+def test_second_ring_on_device_is_busy(torch_cuda):
+    """One ring per GPU: a second nbg_ring_start on the device (another handle) returns NBG_EBUSY at
+    once instead of stalling until the first ring's idle exit; after the first stops, it starts."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    a, b = nb.Maglev(NAMES65, 65537), nb.Maglev(NAMES65, 65537)
+    n = 70000
+    buf = nb.make_trace(n, 0, seed=77)[0]
+    dd = torch.from_numpy(buf).cuda()
+    out = torch.empty(n, dtype=torch.uint16, device="cuda")
+    torch.cuda.synchronize()
+    with a.ring() as ring:
+        t0 = time.perf_counter()
+        with pytest.raises(nb.NbgError) as e:
+            b.ring()
+        assert e.value.code == -16 and time.perf_counter() - t0 < 0.5
+        with pytest.raises(nb.NbgError) as e:  # the ring's own handle refuses direct classify calls
+            a.group_by(dd, n, swap_macs=False)
+        assert e.value.code == -16
+        # another handle's batch co-runs (tile-per-wave kernel while the ring holds the CUs' LDS)
+        r = b.group_by(dd, n, swap_macs=False, stream=torch.cuda.current_stream().cuda_stream)
+        ring.wait(ring.post(dd, n, out))
+        torch.cuda.current_stream().synchronize()
+        be = _expect(buf, n, lut, False)[0]
+        np.testing.assert_array_equal(_got(torch, r.backend), be)
+        np.testing.assert_array_equal(_got(torch, out), be)
+    with b.ring() as ring2:  # the device is free again
+        out.zero_()
+        ring2.wait(ring2.post(dd, n, out))
+    np.testing.assert_array_equal(_got(torch, out), _expect(buf, n, lut, False)[0])
+    a.close()
+    b.close()
+
+
+def test_ring_starts_while_kernels_hold_cus(torch_cuda):
+    """A ring started while another stream's kernel holds CUs: 16 workgroups that each hold 100 KB of
+    a CU's LDS for 60 ms (nbg_debug_hold_cus), so 16 of the ring's blocks (the relay included, the
+    grid's last block) cannot become resident until they leave.  The ring then runs every batch to
+    completion, bit-exact, no earlier than the holders' exit."""
+    import ctypes as C
+
+    torch = torch_cuda
+    import netbricks_amd as nb
+    from netbricks_amd._lib import lib
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    n = 262144
+    bufs = [nb.make_trace(n, 0, seed=90 + i)[0] for i in range(6)]
+    d = [torch.from_numpy(b.copy()).cuda() for b in bufs]
+    outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(6)]
+    busy = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    hold = lib.nbg_debug_hold_cus
+    hold.restype, hold.argtypes = C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]
+    t0 = time.perf_counter()
+    assert hold(16, 100 * 1024, 60000, busy.cuda_stream) == 0
+    time.sleep(0.005)  # the holders are resident before the ring launches
+    with mg.ring(swap_macs=True) as ring:
+        tickets = [ring.post(d[i], n, outs[i]) for i in range(6)]
+        ring.wait(tickets[-1], timeout_ms=20000)
+        t_done = time.perf_counter() - t0
+    busy.synchronize()
+    assert 0.04 < t_done < 10, t_done
+    for i in range(6):
+        be, ref = _expect(bufs[i], n, lut, True)
+        np.testing.assert_array_equal(_got(torch, outs[i]), be)
+        np.testing.assert_array_equal(d[i].cpu().numpy(), ref)
+    mg.close()
+
+
+def test_ring_group_burst(torch_cuda):
+    """nbg_ring_group_burst: bursts of 1..8 consecutive batches grouped by one gate + hist + group
+    launch each, enqueued right after the posts (C4 shard-size batches and mixed sizes, an empty batch
+    in one burst: the per-batch fallback); every batch's perm / counts bit-exact."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    sizes = [131072] * 8 + [1, 5000, 131072, 262144, 65536] + [0, 4096, 300000] + [131072] * 6
+    bursts = [8, 5, 3, 6]
+    bufs = [nb.make_trace(max(n, 1), 0, seed=1700 + i)[0] for i, n in enumerate(sizes)]
+    d = [torch.from_numpy(b.copy()).cuda() for b in bufs]
+    outs = [torch.empty(max(n, 1), dtype=torch.uint16, device="cuda") for n in sizes]
+    perms = [torch.empty(max(n, 1), dtype=torch.uint32, device="cuda") for n in sizes]
+    counts = [torch.full((66,), 7, dtype=torch.uint32, device="cuda") for _ in sizes]
+    sides = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    with mg.ring(swap_macs=True) as ring:
+        i = 0
+        for k, bsz in enumerate(bursts):
+            first = None
+            for j in range(bsz):
+                t = ring.post(d[i + j], sizes[i + j], outs[i + j])
+                first = t if first is None else first
+            ring.group_burst(first, perms[i:i + bsz], counts[i:i + bsz], stream=sides[k % 2])
+            i += bsz
+        ring.wait(len(sizes) - 1)
+        for st in sides:
+            st.synchronize()
+    for i, n in enumerate(sizes):
+        be, _ = _expect(bufs[i], n, lut, True)
+        exp_perm, exp_cnt = orc.group(be[:n], 65)
+        if n:
+            np.testing.assert_array_equal(_got(torch, outs[i])[:n], be[:n], err_msg=f"batch {i} ({n}) backend")
+            np.testing.assert_array_equal(_np32(torch, perms[i])[:n], exp_perm, err_msg=f"batch {i} ({n}) perm")
+        np.testing.assert_array_equal(_np32(torch, counts[i]), exp_cnt, err_msg=f"batch {i} ({n}) counts")
+    mg.close()

@@ -1,6 +1,10 @@
 // Memory-pattern ceilings on MI355X for the Maglev classify kernel's access shapes.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/membench tools/membench.hip
-// Each pattern streams 8 rotating 64 MiB buffers (512 MiB > the 256 MiB Infinity Cache).
+// Usage: membench [rotating buffers, default 8] [iterations, default 100]
+// Each pattern streams N rotating 64 MiB buffers (8: 512 MiB, 2x the 256 MiB Infinity Cache; 32:
+// 2 GiB, 8x), so the ceilings can be taken at the same working set as the timed kernels.  Under
+// rocprofv3 --pmc every dispatch of a pattern moves a known byte count (printed per pattern): the
+// FETCH_SIZE / WRITE_SIZE calibration for these access shapes (tools/runs/r04_membench_pmc.sh).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,7 +33,13 @@ __device__ inline uint4 nt_load(const uint4* p) {
 }
 
 constexpr size_t kBytes = 64ull << 20;
-constexpr int kBufs = 8;
+int kBufs = 8;
+
+// 16 B written through the L2 (sc1): the persistent ring's in-place window stores (stg16_wt)
+__device__ inline void wt_store(uint4* p, uint4 v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(w) : "memory");
+}
 
 // U uint4 per thread, contiguous 1 KiB per wave-instruction; MODE: 0 read, 1 rw full, 2 rw chunk0, 3 copy
 template <int U, int MODE, bool NTL = false>
@@ -49,6 +59,7 @@ __global__ __launch_bounds__(256) void pattern(uint4* __restrict__ buf, uint4* _
     if (MODE == 5) nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
     if (MODE == 6 && (threadIdx.x & 3) == 0)
       nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+    if (MODE == 7) wt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
   }
   if (acc == 0x12345678u) sink[0] = acc;
 }
@@ -119,7 +130,10 @@ float time_it(F f, int iters) {
   return ms * 1000.f / iters;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) kBufs = std::max(1, std::atoi(argv[1]));
+  const int iters = argc > 2 ? std::max(1, std::atoi(argv[2])) : 100;
+  std::printf("rotating buffers: %d x 64 MiB = %d MiB; %d iterations per pattern\n", kBufs, kBufs * 64, iters);
   std::vector<uint4*> bufs(kBufs);
   for (auto& p : bufs) {
     CK(hipMalloc(&p, kBytes));
@@ -132,7 +146,6 @@ int main() {
   const size_t n16 = kBytes / 16;
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  const int iters = 100;
   auto report = [&](const char* name, float us, double rd, double wr) {
     std::printf("%-34s %8.2f us  read %6.0f GB/s  write %6.0f GB/s  total %6.0f GB/s\n", name, us, rd / us / 1e3,
                 wr / us / 1e3, (rd + wr) / us / 1e3);
@@ -170,6 +183,7 @@ int main() {
       const int grid = static_cast<int>(n16 / (256 * 4));
       report("read U4 nt-load", time_it([&](int i) { pattern<4, 0, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, 0);
       report("rw full nt-load nt-store U4", time_it([&](int i) { pattern<4, 5, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
+      report("rw full nt-load sc1-store U4 (ring)", time_it([&](int i) { pattern<4, 7, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
       report("read nt-load + dense 16B/pkt out U4", time_it([&](int i) { pattern<4, 4, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 4);
       // four 64 MiB buffers' worth in one launch (the multi-batch launch's read ceiling)
       uint4* big;
@@ -195,7 +209,7 @@ int main() {
       off[i] = static_cast<uint32_t>(pos);
       pos += (len + 63) & ~63u;
     }
-    std::vector<uint8_t*> ib(kBufs);
+    std::vector<uint8_t*> ib(std::min(kBufs, 32));
     for (auto& p : ib) {
       CK(hipMalloc(&p, pos + 64));
       CK(hipMemset(p, 1, pos + 64));
@@ -208,15 +222,15 @@ int main() {
     const int grid = static_cast<int>(n / 256);
     const double W = 64.0 * n, D = 4.0 * n;
     std::printf("IMIX buffer %.1f MB, 1M windows\n", pos / 1e6);
-    float us = time_it([&](int i) { windows<0><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    float us = time_it([&](int i) { windows<0><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows read", us, W + D, 0);
-    us = time_it([&](int i) { windows<1><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    us = time_it([&](int i) { windows<1><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows rw nt (in place)", us, W + D, W);
-    us = time_it([&](int i) { windows<2><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    us = time_it([&](int i) { windows<2><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows read + 12B/pkt out", us, W + D, 12.0 * n);
-    us = time_it([&](int i) { windows<0, true><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    us = time_it([&](int i) { windows<0, true><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows read nt-load", us, W + D, 0);
-    us = time_it([&](int i) { windows<1, true><<<grid, 256>>>(ib[i % kBufs], d_off, mo, sink, n); }, iters);
+    us = time_it([&](int i) { windows<1, true><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows rw nt-load nt-store", us, W + D, W);
   }
   return 0;
