@@ -1071,10 +1071,9 @@ def run_rank(args) -> None:
             if world > 1:
                 dist.barrier()
             sync_all()
-            t1 = time.perf_counter()
-            _, _, chk = ring_path(n_batches, n=shard_n, gstreams=gstreams, gburst=gburst, check=True)
-            sync_all()
-            el = time.perf_counter() - t1
+            # ring_path's own wall time: ring start, every shard posted and grouped, ring stop (its input
+            # restore for the output check runs before that clock starts)
+            el, _, chk = ring_path(n_batches, n=shard_n, gstreams=gstreams, gburst=gburst, check=True)
             if not chk["ok"]:
                 raise RuntimeError(f"C4 device-resident output check failed on rank {rank}: {chk}")
         else:  # --selftest: no HIP; the timing fields are not a measurement

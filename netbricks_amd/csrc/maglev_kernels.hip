@@ -29,6 +29,9 @@ namespace nbg {
 
 namespace {
 
+#ifndef NBG_CHAIN_ABL  // measurement builds (tools/build_ab.sh): 1 no tbl24 gather, 2 no LUT gather, 4 no gate stores
+#define NBG_CHAIN_ABL 0
+#endif
 constexpr uint32_t kSentinel = NBG_SENTINEL;
 constexpr uint32_t kEth = 14;
 
@@ -355,11 +358,18 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
         uint32_t lo, hi;
         if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
           const uint32_t ip = __builtin_bswap32(src);
+#if NBG_CHAIN_ABL & 1  // measurement builds: no tbl24 gather (gate from the address)
+          gate = (ip >> 8) & 1u;
+#else
           gate = a.tbl24[ip >> 8];
+#endif
           iplo = ip & 0xffu;
           resolve = true;
         }
         fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+#if NBG_CHAIN_ABL & 2  // measurement builds: no LUT gather
+        if constexpr (CHAIN) bin = lo % a.nb; else
+#endif
         bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
       }
     } else {
@@ -401,6 +411,9 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
     if (slow) bin = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, meta.len, p_own, gate);
     if constexpr (CHAIN) {
       if (resolve && (gate & 0x8000u)) gate = a.tbl_long[((gate & 0x7fffu) << 8) + iplo];
+#if NBG_CHAIN_ABL & 4  // measurement builds: no gate stores
+      if (gate == 0xfffeu)
+#endif
       a.gate[p_own] = static_cast<uint16_t>(gate);
       if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
     }
@@ -509,6 +522,25 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
       }
       classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, rm[i % kRing],
                                                            rt[i % kRing]);
+    }
+  } else if (LAYOUT == kDesc && tpw > 1u && tpw <= 4u) {
+    // descriptor layouts, 2..4 tiles per wave (NBG_TPW): the descriptors of all of the wave's tiles are
+    // loaded up front, unconditionally (clamped), so every tile after the first
+    // issues its window loads at once instead of after a descriptor round trip of its own
+    constexpr uint32_t kMetaTiles = 4;
+    TileMeta mq[kMetaTiles];
+#pragma unroll
+    for (uint32_t j = 0; j < kMetaTiles; ++j) mq[j] = load_meta<LAYOUT>(a, (t0 + j) * 64u, lane);
+#pragma unroll
+    for (uint32_t i = 0; i < kMetaTiles; ++i) {
+      const uint32_t wbase = (t0 + i) * 64u;
+      if (i >= tpw || wbase >= a.n_pkts) break;  // wave-uniform
+      __builtin_amdgcn_s_setprio(kLoadPrio);
+      TileRegs cur;
+      load_tile<LAYOUT>(a, wbase, mq[i], part, quad, cur);
+      __builtin_amdgcn_s_setprio(0);
+      transpose(cur);
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i], cur);
     }
   } else {
     for (uint32_t i = 0; i < tpw; ++i) {

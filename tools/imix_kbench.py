@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Classify-kernel time of configs C5 (lpm -> maglev, IMIX) and C3 (1000 backends / 655373, IMIX, in
+place) on one stream (HIP events around each launch, grouping deferred past the stop event), for
+A/B builds loaded with NBG_LIB_OVERRIDE (tools/build_ab.sh).  Prints one JSON line."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=60)
+    ap.add_argument("--which", default="c5,c3")
+    ap.add_argument("--stream-desc", action="store_true")
+    ap.add_argument("--tpw", default="1", help="comma-separated NBG_TPW values (tiles per wave), one handle each")
+    ap.add_argument("--rounds", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+
+    import netbricks_amd as nb
+    from bench import KernelTimer
+
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    bufs, offs, lens = [], [], []
+    for b in range(2):
+        buf, off, ln = nb.make_trace(n, 1, seed=1000 + b)
+        bufs.append(torch.from_numpy(buf).to(dev))
+        offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
+        lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
+    routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
+    out = {"lib": os.environ.get("NBG_LIB_OVERRIDE", "in-tree")}
+    st = torch.cuda.Stream(dev)
+    backend = torch.empty(n, dtype=torch.uint16, device=dev)
+    perm = torch.empty(n, dtype=torch.uint32, device=dev)
+    gate = torch.empty(n, dtype=torch.uint16, device=dev)
+    for which, tpw, rnd in [(w, t, r) for r in range(args.rounds) for w in args.which.split(",")
+                            for t in args.tpw.split(",")]:
+        os.environ["NBG_TPW"] = tpw
+        if which == "c5":
+            mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
+            lpm = nb.Lpm(routes["reference"] + routes["mixed"])
+            counts = torch.empty(66, dtype=torch.uint32, device=dev)
+
+            def call(i):
+                nb.chain_lpm_maglev(mg, lpm, bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True,
+                                    defer_group=True, gate=gate, stream=st.cuda_stream, backend=backend, perm=perm,
+                                    counts=counts, stream_desc=args.stream_desc)
+        else:
+            mg = nb.Maglev([f"be{i}" for i in range(1000)], 655373)
+            counts = torch.empty(1001, dtype=torch.uint32, device=dev)
+
+            def call(i):
+                mg.group_by(bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True, defer_group=True,
+                            stream=st.cuda_stream, backend=backend, perm=perm, counts=counts,
+                            stream_desc=args.stream_desc)
+        for i in range(6):
+            call(i)
+            mg.finish_group(st.cuda_stream)
+        torch.cuda.synchronize()
+        kt = KernelTimer(args.iters)
+        for i in range(args.iters):
+            kt.start(i, st.cuda_stream)
+            call(i)
+            kt.stop(i, st.cuda_stream)
+            mg.finish_group(st.cuda_stream)
+        torch.cuda.synchronize()
+        ms = kt.ms()
+        kt.close()
+        out[f"{which}_tpw{tpw}_r{rnd}"] = {"classify_us_mean": round(float(ms.mean()) * 1e3, 2),
+                                          "classify_us_median": round(float(np.median(ms)) * 1e3, 2)}
+        mg.close()
+        if which == "c5":
+            lpm.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
