@@ -846,16 +846,25 @@ def run_rank(args) -> None:
                 raise RuntimeError(f"nbg_ring_post_burst: {nb._lib.last_error()}")
             return k.value
 
+        # an input is posted again only once its previous batch is complete (at most len(pks) batches
+        # in flight): a batch must not read a buffer an earlier in-flight batch is still rewriting, nor
+        # find its lines freshly written in a cache (round 3's 8-input rotation allowed both)
+        cap = min(slots, len(pks))
         try:
             warm = 0
             while warm < 16:  # warm: the kernel is resident and the first inputs touched
-                warm += post_upto(warm, 16 - warm)
+                if poll(rr, C.byref(cc)):
+                    raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
+                room = min(16 - warm, cap - (warm - cc.value))
+                if room > 0:
+                    warm += post_upto(warm, room)
             ring.wait(15)
             base, stamps, posted, done = 16, [], 0, 0
             t0 = time.perf_counter()
             while done < batches:
-                if posted < batches:
-                    posted += post_upto(16 + posted, min(slots, batches - posted))
+                room = min(batches - posted, cap - (posted - done))
+                if room > 0:
+                    posted += post_upto(16 + posted, room)
                 if poll(rr, C.byref(cc)):
                     raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
                 c = cc.value - base
@@ -880,7 +889,7 @@ def run_rank(args) -> None:
         return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
                 "wall_us_per_batch": round(wall / batches * 1e6, 2), "batches": batches, "bytes_per_pkt": bpp,
                 "pkts_per_batch": n, "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                "working_set_mib": rotate * BATCH * SLOT >> 20, "rotating_inputs": len(pks),
+                "working_set_mib": rotate * BATCH * SLOT >> 20, "rotating_inputs": len(pks), "max_in_flight": cap,
                 "output_check": check,
                 "kernel": f"classify_ring_kernel<true, {1 if swap else 0}>",
                 "what": "persistent RX ring (nbg_ring_*): one resident classify kernel (LUT staged once) takes "
@@ -917,11 +926,12 @@ def run_rank(args) -> None:
         for i in range(per + slots):
             arr[i] = NbgRingBatch(pks[i % len(pks)], n, rd["be"][i % nbe].data_ptr())
         esz, base_addr = C.sizeof(NbgRingBatch), C.addressof(arr)
-        k, tk = C.c_uint32(), C.c_uint64()
+        k, tk, cc = C.c_uint32(), C.c_uint64(), C.c_uint64()
+        cap = min(slots, len(pks))  # an input is reposted only once its previous batch is complete
         sps = [C.c_void_p(x.cuda_stream) for x in sides]
         pps = [(C.c_void_p * gburst)(*[p.data_ptr() for p in ring_res["perm"][q][:gburst]]) for q in range(gstreams)]
         cps = [(C.c_void_p * gburst)(*[c.data_ptr() for c in ring_res["cnt"][q][:gburst]]) for q in range(gstreams)]
-        burst, grp = clib.nbg_ring_post_burst, clib.nbg_ring_group_burst
+        burst, grp, poll = clib.nbg_ring_post_burst, clib.nbg_ring_group_burst, clib.nbg_ring_poll
         evs = {}  # first post of a group burst -> (event after it on its side stream, posts in it)
         last_on = [None] * gstreams  # (first post, count) of the last burst grouped on each side stream
         if check:
@@ -930,9 +940,13 @@ def run_rank(args) -> None:
         ring = mgs[0].ring(swap_macs=True, stream=streams[0])
         rr = ring._r
         try:
-            posted = grouped = safe = 0  # safe: every grouping of posts < safe has run
+            posted = grouped = safe = done = 0  # safe: every grouping of posts < safe has run
             while grouped < batches:
-                want = min(batches - posted, slots, safe + nbe - posted)
+                if cap < slots and posted - done >= cap:  # the next input's previous batch may be in flight
+                    if poll(rr, C.byref(cc)):
+                        raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
+                    done = cc.value
+                want = min(batches - posted, slots, safe + nbe - posted, cap - (posted - done))
                 if want <= 0:  # the backend[] buffers of the next posts still wait for their grouping
                     while safe in evs and evs[safe][0].query():
                         safe += evs.pop(safe)[1]

@@ -201,7 +201,9 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
  * (NBG_SWAP_MACS) its in-place MAC swap are then in HBM, written through the L2, for any later
  * launch or copy.  Per packet the results are those of nbg_maglev_classify_device_ex with the same
  * arguments and no grouping (perm / counts are not produced on the ring).  Everything a post names
- * stays untouched by the caller until the batch is complete.
+ * stays untouched by the caller until the batch is complete — including by a later post: a buffer is
+ * posted again only once its previous batch is complete (the ring runs up to NBG_RING_SLOTS batches
+ * at once, so two posts of one buffer could be classified concurrently).
  * The kernel runs on a private stream of the highest priority (a hardware queue no ordinary stream
  * shares: work queued behind a resident kernel would wait for it) and starts after the work issued
  * on `stream` so far.  It holds the LDS of every CU it occupies until it ends: after

@@ -299,9 +299,11 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
     const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(m.len), src)) : a.fixed_len;
     const uint8_t* base = pkt_addr<LAYOUT>(a, wbase, src, o);
     const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
-    // chunk readable/writable: inside the frame, or the window is owned by this packet
+    // chunk readable/writable: inside the frame, or the window is owned by this packet.  Without the
+    // swap nothing is written back, and the classify reads chunks 0..2 only (bytes 14..37 for IHL 5):
+    // chunk 3 is not loaded (its lanes load the batch base, one line for the whole wave)
     const bool inwin = a.win_owned || (part * 16u + 16u <= l);
-    const bool rd = pv && aligned && inwin;
+    const bool rd = pv && aligned && inwin && (part < 3u || a.swap);
     addr[k] = rd ? base + part * 16u : a.pkts;
     if (rd && l >= 48u) t.cflag |= 1u << k;
   }
