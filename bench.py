@@ -861,7 +861,12 @@ def run_rank(args) -> None:
             ring.wait(15)
             base, stamps, posted, done = 16, [], 0, 0
             t0 = time.perf_counter()
+            last_move, last_state = t0, None
             while done < batches:
+                if (posted, done) != last_state:
+                    last_move, last_state = time.perf_counter(), (posted, done)
+                elif time.perf_counter() - last_move > 10.0:
+                    raise RuntimeError(f"ring_pass stalled: posted {posted} done {done} cap {cap} n {n}")
                 room = min(batches - posted, cap - (posted - done))
                 if room > 0:
                     posted += post_upto(16 + posted, room)
@@ -941,8 +946,17 @@ def run_rank(args) -> None:
         rr = ring._r
         try:
             posted = grouped = safe = done = 0  # safe: every grouping of posts < safe has run
+            last_move, last_state = time.perf_counter(), None
             while grouped < batches:
-                if cap < slots and posted - done >= cap:  # the next input's previous batch may be in flight
+                state = (posted, grouped, safe, done)
+                if state != last_state:
+                    last_move, last_state = time.perf_counter(), state
+                elif time.perf_counter() - last_move > 10.0:  # fail loudly rather than hang the job
+                    poll(rr, C.byref(cc))
+                    raise RuntimeError(f"ring_path stalled: posted {posted} grouped {grouped} safe {safe} done {done} "
+                                       f"ring completed {cc.value} cap {cap} n {n} gburst {gburst} "
+                                       f"pending group bursts {sorted(evs)[:4]}")
+                if posted - done >= cap:  # the next input's previous batch (or the oldest slot) may be in flight
                     if poll(rr, C.byref(cc)):
                         raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
                     done = cc.value
@@ -966,8 +980,15 @@ def run_rank(args) -> None:
                     grouped += cnt
         finally:
             ring.stop()
-        for x in sides:
-            x.synchronize()
+        for q, x in enumerate(sides):  # the last groupings; a gate that never opens fails the job loudly
+            ev = torch.cuda.Event()
+            ev.record(x)
+            tq = time.perf_counter()
+            while not ev.query():
+                if time.perf_counter() - tq > 10.0:
+                    raise RuntimeError(f"ring_path: side stream {q} did not drain in 10 s (posted {posted}, grouped "
+                                       f"{grouped}, last burst {last_on[q]})")
+                time.sleep(1e-4)
         wall = time.perf_counter() - t0
         kms = C.c_float()
         if clib.nbg_ring_kernel_ms(mgs[0]._h, C.byref(kms)):
@@ -1343,7 +1364,9 @@ def run_rank(args) -> None:
     #      classification of the batch.  Any failure fails the job.
     c4 = None
     if not args.no_c4:
+        log(f"[rank {rank}] C4 block")
         c4 = c4_block(args.c4_batches, args.scatter_steps)
+        log(f"[rank {rank}] C4 block done")
 
     # ---- roofline: the headline launch timed alone; labelled variants beside (N = 1)
     roof, mroof, variants = None, None, {}
@@ -1388,6 +1411,7 @@ def run_rank(args) -> None:
                         "classified + grouped as one rank would (MAC swap in place), 64 distinct shards rotating "
                         "on the same streams; below the streaming kernel's 262,144-packet threshold, so the "
                         "tile-per-wave classify kernel + group kernel (pmc.c4_shard.kernel)"}
+            log(f"[rank {rank}] launch-path variants done")
             if not args.no_ring:
                 # the working-set sweep (0.5 / 1 / 2 GiB of rotating 1M batches): the ring read only and
                 # in place, RING_BATCHES batches per pass, slope over the middle three quarters, outputs
@@ -1400,6 +1424,7 @@ def run_rank(args) -> None:
                     log(f"working-set sweep failed: {e}")
                     sweep = {"error": str(e)[:300]}
                 variants["ws_sweep"] = sweep
+                log(f"[rank {rank}] working-set sweep done")
                 top = sweep.get(str(RING_ROTATE), {}) if isinstance(sweep, dict) else {}
                 for name in ("ring_read_only", "ring_in_place"):
                     variants[name] = top.get(name, {"error": "not measured"})

@@ -29,6 +29,9 @@ namespace nbg {
 
 namespace {
 
+#ifndef NBG_DESC_PF2  // measurement builds: descriptor tiles keep the next tile's windows in flight (NBG_TPW >= 2)
+#define NBG_DESC_PF2 0
+#endif
 #ifndef NBG_CHAIN_ABL  // measurement builds (tools/build_ab.sh): 1 no tbl24 gather, 2 no LUT gather, 4 no gate stores
 #define NBG_CHAIN_ABL 0
 #endif
@@ -533,6 +536,20 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     TileMeta mq[kMetaTiles];
 #pragma unroll
     for (uint32_t j = 0; j < kMetaTiles; ++j) mq[j] = load_meta<LAYOUT>(a, (t0 + j) * 64u, lane);
+#if NBG_DESC_PF2  // measurement builds: the next tile's windows in flight beside the current one
+    TileRegs rt[2];
+    load_tile<LAYOUT>(a, t0 * 64u, mq[0], part, quad, rt[0]);
+#pragma unroll
+    for (uint32_t i = 0; i < kMetaTiles; ++i) {
+      const uint32_t wbase = (t0 + i) * 64u;
+      if (i >= tpw || wbase >= a.n_pkts) break;  // wave-uniform
+      if (i + 1 < kMetaTiles)  // unconditional: a tile past the batch loads its base, never used
+        load_tile<LAYOUT>(a, wbase + 64u, mq[i + 1], part, quad, rt[(i + 1) & 1]);
+      transpose(rt[i & 1]);
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i],
+                                                           rt[i & 1]);
+    }
+#else
 #pragma unroll
     for (uint32_t i = 0; i < kMetaTiles; ++i) {
       const uint32_t wbase = (t0 + i) * 64u;
@@ -544,6 +561,7 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
       transpose(cur);
       classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i], cur);
     }
+#endif
   } else {
     for (uint32_t i = 0; i < tpw; ++i) {
       const uint32_t wbase = (t0 + i) * 64u;
