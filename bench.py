@@ -1447,6 +1447,17 @@ def run_rank(args) -> None:
                         "C4's per-GPU shard (131,072 packets: one 1M C2 batch in 8 contiguous shards) through the "
                         "persistent ring, MAC swap in place: no launch, LUT staging or ramp per shard; backend[] + "
                         "swap only")
+                if os.environ.get("NBG_BENCH_RING_GROUP_SWEEP"):  # tuning: burst size x side streams
+                    gs = {}
+                    for n_, name_ in ((BATCH, "1M"), (C4_SHARD, "c4_shard")):
+                        for gb_ in ((1, 2, 4) if n_ == BATCH else (4, 8)):
+                            for st_ in (2, 3, 4):
+                                try:
+                                    r_ = ring_grouped(1024 if n_ == BATCH else 4096, n=n_, gstreams=st_, gburst=gb_)
+                                    gs[f"{name_}_b{gb_}_s{st_}"] = {k_: r_[k_] for k_ in ("us_per_batch", "path_frac")}
+                                except Exception as e:  # noqa: BLE001
+                                    gs[f"{name_}_b{gb_}_s{st_}"] = {"error": str(e)[:200]}
+                    variants["ring_group_sweep"] = gs
                 checks = [v.get("output_check") for k, v in variants.items()
                           if isinstance(v, dict) and isinstance(v.get("output_check"), dict)]
                 checks += [r.get("output_check") for row in (sweep.values() if isinstance(sweep, dict) else [])

@@ -29,9 +29,6 @@ namespace nbg {
 
 namespace {
 
-#ifndef NBG_DESC_PF2  // measurement builds: descriptor tiles keep the next tile's windows in flight (NBG_TPW >= 2)
-#define NBG_DESC_PF2 0
-#endif
 #ifndef NBG_CHAIN_ABL  // measurement builds (tools/build_ab.sh): 1 no tbl24 gather, 2 no LUT gather, 4 no gate stores
 #define NBG_CHAIN_ABL 0
 #endif
@@ -302,11 +299,10 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
     const uint32_t l = a.len ? static_cast<uint32_t>(__shfl(static_cast<int>(m.len), src)) : a.fixed_len;
     const uint8_t* base = pkt_addr<LAYOUT>(a, wbase, src, o);
     const bool aligned = (reinterpret_cast<uintptr_t>(base) & 15u) == 0;
-    // chunk readable/writable: inside the frame, or the window is owned by this packet.  Without the
-    // swap nothing is written back, and the classify reads chunks 0..2 only (bytes 14..37 for IHL 5):
-    // chunk 3 is not loaded (its lanes load the batch base, one line for the whole wave)
+    // chunk readable/writable: inside the frame, or the window is owned by this packet.  (Read only,
+    // chunk 3 is unused, but skipping its load measured 0.7 us slower for C5: profiles/r04_c5_ablation.txt)
     const bool inwin = a.win_owned || (part * 16u + 16u <= l);
-    const bool rd = pv && aligned && inwin && (part < 3u || a.swap);
+    const bool rd = pv && aligned && inwin;
     addr[k] = rd ? base + part * 16u : a.pkts;
     if (rd && l >= 48u) t.cflag |= 1u << k;
   }
@@ -529,27 +525,14 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
                                                            rt[i % kRing]);
     }
   } else if (LAYOUT == kDesc && tpw > 1u && tpw <= 4u) {
-    // descriptor layouts, 2..4 tiles per wave (NBG_TPW): the descriptors of all of the wave's tiles are
-    // loaded up front, unconditionally (clamped), so every tile after the first
+    // descriptor layouts, 2..4 tiles per wave (NBG_TPW, measurement): the descriptors of all of the
+    // wave's tiles are loaded up front (measured no faster than one tile per wave for C3 / C5:
+    // profiles/r04_c5_ablation.txt), unconditionally (clamped), so every tile after the first
     // issues its window loads at once instead of after a descriptor round trip of its own
     constexpr uint32_t kMetaTiles = 4;
     TileMeta mq[kMetaTiles];
 #pragma unroll
     for (uint32_t j = 0; j < kMetaTiles; ++j) mq[j] = load_meta<LAYOUT>(a, (t0 + j) * 64u, lane);
-#if NBG_DESC_PF2  // measurement builds: the next tile's windows in flight beside the current one
-    TileRegs rt[2];
-    load_tile<LAYOUT>(a, t0 * 64u, mq[0], part, quad, rt[0]);
-#pragma unroll
-    for (uint32_t i = 0; i < kMetaTiles; ++i) {
-      const uint32_t wbase = (t0 + i) * 64u;
-      if (i >= tpw || wbase >= a.n_pkts) break;  // wave-uniform
-      if (i + 1 < kMetaTiles)  // unconditional: a tile past the batch loads its base, never used
-        load_tile<LAYOUT>(a, wbase + 64u, mq[i + 1], part, quad, rt[(i + 1) & 1]);
-      transpose(rt[i & 1]);
-      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i],
-                                                           rt[i & 1]);
-    }
-#else
 #pragma unroll
     for (uint32_t i = 0; i < kMetaTiles; ++i) {
       const uint32_t wbase = (t0 + i) * 64u;
@@ -561,7 +544,6 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
       transpose(cur);
       classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i], cur);
     }
-#endif
   } else {
     for (uint32_t i = 0; i < tpw; ++i) {
       const uint32_t wbase = (t0 + i) * 64u;

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--stream-desc", action="store_true")
     ap.add_argument("--tpw", default="1", help="comma-separated NBG_TPW values (tiles per wave), one handle each")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS (NBG_LUT_LDS)")
     args = ap.parse_args()
     import torch
 
@@ -51,7 +52,7 @@ def main():
             def call(i):
                 nb.chain_lpm_maglev(mg, lpm, bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True,
                                     defer_group=True, gate=gate, stream=st.cuda_stream, backend=backend, perm=perm,
-                                    counts=counts, stream_desc=args.stream_desc)
+                                    counts=counts, stream_desc=args.stream_desc, lut_lds=args.lut_lds)
         else:
             mg = nb.Maglev([f"be{i}" for i in range(1000)], 655373)
             counts = torch.empty(1001, dtype=torch.uint32, device=dev)
@@ -59,7 +60,7 @@ def main():
             def call(i):
                 mg.group_by(bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True, defer_group=True,
                             stream=st.cuda_stream, backend=backend, perm=perm, counts=counts,
-                            stream_desc=args.stream_desc)
+                            stream_desc=args.stream_desc, lut_lds=args.lut_lds)
         for i in range(6):
             call(i)
             mg.finish_group(st.cuda_stream)
