@@ -73,7 +73,7 @@ RING_ROTATE = int(os.environ.get("NBG_BENCH_RING_ROTATE", "32"))
 WS_SWEEP = tuple(int(x) for x in os.environ.get("NBG_BENCH_WS_SWEEP", "8,16,32").split(","))  # working-set sweep
 RING_BACKENDS = 128   # backend[] buffers a ring pass rotates over (more than the 64 slots + the grouping lag)
 RING_CHECK = 16       # the last batches of every ring pass, checked against the launch path
-RING_GROUP_BURST = int(os.environ.get("NBG_BENCH_RING_GROUP_BURST", "1"))  # 1M batches per nbg_ring_group_burst
+RING_GROUP_BURST = int(os.environ.get("NBG_BENCH_RING_GROUP_BURST", "2"))  # 1M batches per nbg_ring_group_burst
 C4_GROUP_BURST = int(os.environ.get("NBG_BENCH_C4_GROUP_BURST", "8"))      # C4 shards per nbg_ring_group_burst
 C4_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_C4_GROUP_STREAMS", "2"))
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
@@ -960,7 +960,8 @@ def run_rank(args) -> None:
                     if poll(rr, C.byref(cc)):
                         raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
                     done = cc.value
-                want = min(batches - posted, slots, safe + nbe - posted, cap - (posted - done))
+                # ... and every post stays groupable: a group burst names tickets among the last 64 posted
+                want = min(batches - posted, slots - (posted - grouped), safe + nbe - posted, cap - (posted - done))
                 if want <= 0:  # the backend[] buffers of the next posts still wait for their grouping
                     while safe in evs and evs[safe][0].query():
                         safe += evs.pop(safe)[1]
@@ -1072,6 +1073,64 @@ def run_rank(args) -> None:
         return {"avg_launch_us": round(c_ms.mean() * 1e3, 2), "us_per_batch": round(c_ms.mean() * 1e3 / MULTI_K, 2),
                 "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_pkt": bpp,
                 "working_set_mib": rotate * BATCH * SLOT >> 20, "launches": calls}
+
+    def c4_shard_multi(calls, k=8, n=C4_SHARD, n_streams=2):
+        """C4's per-GPU shard through the multi-batch launch: a rank batches k consecutive shards of its RX
+        queue per nbg_maglev_classify_device_multi call (one streaming-classify launch + one group launch,
+        every shard with its own backend / perm / counts), round-robin on n_streams streams over the ring
+        inputs' 256 distinct shards; then the launch alone (HIP events, grouping deferred)."""
+        from netbricks_amd._lib import NbgBatch
+
+        rd = ring_setup()
+        ring_restore(RING_ROTATE)
+        ins = [rd["bufs"][w].data_ptr() + q * n * SLOT for w, q in ring_inputs(RING_ROTATE, n)]
+        outs_ = [[(torch.empty(n, dtype=torch.uint16, device=dev), torch.empty(n, dtype=torch.uint32, device=dev),
+                   torch.empty(N_BACKENDS + 1, dtype=torch.uint32, device=dev)) for _ in range(k)]
+                 for _ in range(n_streams)]
+        arrs = []
+        for g in range(len(ins) // k):
+            arr = (NbgBatch * k)()
+            for q in range(k):
+                be, pm, ct = outs_[g % n_streams][q]
+                arr[q] = NbgBatch(ins[g * k + q], n, be.data_ptr(), pm.data_ptr(), ct.data_ptr(), None)
+            arrs.append(arr)
+
+        def call(i, st, flags):
+            if clib.nbg_maglev_classify_device_multi(hs[i % n_streams], arrs[i % len(arrs)], k, SLOT, FRAME, flags, st):
+                raise RuntimeError(f"nbg_maglev_classify_device_multi: {nb._lib.last_error()}")
+
+        for i in range(2 * len(arrs)):
+            call(i, sts[i % n_streams], NBG_SWAP_MACS)
+        sync_all()
+        start_ev = torch.cuda.Event()
+        start_ev.record(torch.cuda.current_stream(dev))
+        for st in streams[:n_streams]:
+            st.wait_event(start_ev)
+        t1 = time.perf_counter()
+        for i in range(calls):
+            call(i, sts[i % n_streams], NBG_SWAP_MACS)
+        sync_all()
+        el = time.perf_counter() - t1
+        kt = KernelTimer(calls)
+        for i in range(calls):
+            kt.start(i, sts[0])
+            call(i * n_streams, sts[0], NBG_SWAP_MACS | NBG_DEFER_GROUP)  # stream 0's handle and outputs
+            kt.stop(i, sts[0])
+            finish(hs[0], sts[0])
+        sync_all()
+        c_ms = kt.ms()
+        kt.close()
+        for m in mgs:
+            m.check()
+        us = el / (calls * k) * 1e6
+        ach = k * n * CLASSIFY_BYTES["in_place"] / (c_ms.mean() / 1e3) / 1e9
+        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_shard": round(us, 3), "shards_per_launch": k,
+                "streams": n_streams, "path_frac": round(n * PATH_BYTES["in_place"] / us / 1e3 / HBM_PEAK_GBPS, 4),
+                "avg_launch_us": round(c_ms.mean() * 1e3, 2), "achieved": round(ach, 1),
+                "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "what": "C4's per-GPU shard (131,072 packets) with a rank batching 8 consecutive shards of its RX queue "
+                        "per multi-batch launch (MAC swap in place + grouping, each shard its own outputs), 2 streams; "
+                        "frac from the launch timed alone"}
 
     def ws_sweep(batches):
         """The working-set sweep: the ring (read only, in place) and the multi-batch launch (in place,
@@ -1220,7 +1279,7 @@ def run_rank(args) -> None:
                                 counts=torch.empty(1001, dtype=torch.uint32, device=dev)) for _ in range(S)])
         return imix
 
-    def imix_issue(cfg, g, j, stream=None, defer=False):
+    def imix_issue(cfg, g, j, stream=None, defer=False, lut_lds=False):
         x = imix
         k = g % IMIX_BATCHES
         st = sts[j] if stream is None else stream
@@ -1229,16 +1288,16 @@ def run_rank(args) -> None:
                                 defer_group=defer, stream=st, **x["c3out"][j])
         else:
             nb.chain_lpm_maglev(mgs[j], x["lpm"], x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k],
-                                owned_windows=True, defer_group=defer, gate=x["gates"][j], stream=st,
+                                owned_windows=True, defer_group=defer, gate=x["gates"][j], stream=st, lut_lds=lut_lds,
                                 backend=outs[j][0]["backend"], perm=outs[j][0]["perm"], counts=outs[j][0]["counts"])
 
-    def imix_variant(cfg, steps, warmup):
+    def imix_variant(cfg, steps, warmup, lut_lds=False):
         """Config C3 (1000 backends / 655373, IMIX, MAC swap in place) or C5 (lpm -> maglev, IMIX):
         whole-job rate on S streams (step = BATCHES_PER_STEP batches), then the classify kernel alone."""
         imix_setup()
         cm = imix["c3"] if cfg == "c3" else mgs
         for i in range(max(1, warmup) * BATCHES_PER_STEP):
-            imix_issue(cfg, i, i % S)
+            imix_issue(cfg, i, i % S, lut_lds=lut_lds)
         sync_all()
         start_ev = torch.cuda.Event()
         start_ev.record(torch.cuda.current_stream(dev))
@@ -1247,14 +1306,14 @@ def run_rank(args) -> None:
         n_calls = steps * BATCHES_PER_STEP
         t1 = time.perf_counter()
         for i in range(n_calls):
-            imix_issue(cfg, i, i % S)
+            imix_issue(cfg, i, i % S, lut_lds=lut_lds)
         sync_all()
         el = time.perf_counter() - t1
         kt = KernelTimer(n_calls)
         st = sts[0]
         for i in range(n_calls):
             kt.start(i, st)
-            imix_issue(cfg, i, 0, stream=st, defer=True)
+            imix_issue(cfg, i, 0, stream=st, defer=True, lut_lds=lut_lds)
             kt.stop(i, st)
             cm[0].finish_group(st)
         sync_all()
@@ -1436,6 +1495,7 @@ def run_rank(args) -> None:
                                                                     gburst=C4_GROUP_BURST))]
                 if headline != "ring":
                     ring_runs.append(("ring_in_place_grouped", lambda: ring_grouped(kb)))
+                ring_runs.append(("c4_shard_multi8", lambda: c4_shard_multi(max(args.steps * BATCHES_PER_STEP, 256))))
                 for name, fn in ring_runs:
                     try:  # a ring variant that fails is reported in the line, beside the other figures
                         variants[name] = fn()
@@ -1475,6 +1535,10 @@ def run_rank(args) -> None:
                 log(f"[rank {rank}] IMIX traces ready in {time.time() - t0:.1f}s")
                 variants["c3"] = imix_variant("c3", args.steps, args.warmup)
                 variants["c5"] = imix_variant("c5", args.steps, args.warmup)
+                variants["c5_lut_lds"] = imix_variant("c5", args.steps, args.warmup, lut_lds=True)
+                variants["c5_lut_lds"]["what"] = (
+                    "C5 with the u8 LUT staged in LDS (NBG_LUT_LDS: one 1024-thread block per CU, two tiles' loads "
+                    "in flight per wave): removes the LUT's L2 gather from every wave's critical path")
 
     if rank == 0:
         cpu = None

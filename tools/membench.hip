@@ -185,13 +185,19 @@ int main(int argc, char** argv) {
       report("rw full nt-load nt-store U4", time_it([&](int i) { pattern<4, 5, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
       report("rw full nt-load sc1-store U4 (ring)", time_it([&](int i) { pattern<4, 7, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
       report("read nt-load + dense 16B/pkt out U4", time_it([&](int i) { pattern<4, 4, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 4);
-      // four 64 MiB buffers' worth in one launch (the multi-batch launch's read ceiling)
-      uint4* big;
-      CK(hipMalloc(&big, 4 * kBytes));
-      CK(hipMemset(big, 1, 4 * kBytes));
+      // four 64 MiB buffers' worth in one launch (the multi-batch launch's read ceiling), rotating over
+      // 8 such 256 MiB buffers (2 GiB: a 256 MiB buffer reused back to back would fit the Infinity Cache)
+      std::vector<uint4*> big(8);
+      for (auto& p : big) {
+        CK(hipMalloc(&p, 4 * kBytes));
+        CK(hipMemset(p, 1, 4 * kBytes));
+      }
       const int g4 = static_cast<int>(4 * n16 / (256 * 4));
-      report("read 256 MiB in one launch U4 nt-load", time_it([&](int) { pattern<4, 0, true><<<g4, 256>>>(big, dst, sink); }, iters), 4 * B, 0);
-      CK(hipFree(big));
+      report("read 256 MiB in one launch U4 nt-load", time_it([&](int i) { pattern<4, 0, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 0);
+      // the same rewrite shapes without a launch ramp every 64 MiB (the persistent ring's regime)
+      report("rw full nt-load nt-store, 256 MiB per launch", time_it([&](int i) { pattern<4, 5, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 4 * B);
+      report("rw full nt-load sc1-store, 256 MiB per launch", time_it([&](int i) { pattern<4, 7, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 4 * B);
+      for (auto& p : big) CK(hipFree(p));
     }
     RUN(4, 3, "copy U4", B, B);
     RUN(8, 3, "copy U8", B, B);
