@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--tpw", default="1", help="comma-separated NBG_TPW values (tiles per wave), one handle each")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS (NBG_LUT_LDS)")
+    ap.add_argument("--n", default=str(1 << 20), help="comma-separated batch sizes (packets); times are also per 1M")
     args = ap.parse_args()
     import torch
 
@@ -28,7 +29,8 @@ def main():
     from bench import KernelTimer
 
     dev = torch.device("cuda:0")
-    n = 1 << 20
+    sizes = [int(x) for x in args.n.split(",")]
+    n = max(sizes)
     bufs, offs, lens = [], [], []
     for b in range(2):
         buf, off, ln = nb.make_trace(n, 1, seed=1000 + b)
@@ -41,8 +43,8 @@ def main():
     backend = torch.empty(n, dtype=torch.uint16, device=dev)
     perm = torch.empty(n, dtype=torch.uint32, device=dev)
     gate = torch.empty(n, dtype=torch.uint16, device=dev)
-    for which, tpw, rnd in [(w, t, r) for r in range(args.rounds) for w in args.which.split(",")
-                            for t in args.tpw.split(",")]:
+    for which, tpw, rnd, n in [(w, t, r, z) for r in range(args.rounds) for w in args.which.split(",")
+                               for t in args.tpw.split(",") for z in sizes]:
         os.environ["NBG_TPW"] = tpw
         if which == "c5":
             mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
@@ -74,8 +76,10 @@ def main():
         torch.cuda.synchronize()
         ms = kt.ms()
         kt.close()
-        out[f"{which}_tpw{tpw}_r{rnd}"] = {"classify_us_mean": round(float(ms.mean()) * 1e3, 2),
-                                          "classify_us_median": round(float(np.median(ms)) * 1e3, 2)}
+        key = f"{which}_tpw{tpw}_r{rnd}" + (f"_n{n}" if len(sizes) > 1 else "")
+        out[key] = {"classify_us_mean": round(float(ms.mean()) * 1e3, 2),
+                    "classify_us_median": round(float(np.median(ms)) * 1e3, 2),
+                    "us_per_1m": round(float(ms.mean()) * 1e3 * (1 << 20) / n, 2)}
         mg.close()
         if which == "c5":
             lpm.close()
