@@ -185,6 +185,31 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
                                      uint16_t fixed_len, uint32_t flags, void* stream);
 
 /*
+ * The same for descriptor batches (IMIX: a u32 byte offset and a u16 frame length per packet, the
+ * layout of configs C3 and C5): one tile-per-wave classify launch over all batches, then (grouping)
+ * one hist, one scan and one group launch over all of them.  Each batch's outputs are exactly those
+ * of nbg_maglev_classify_device (or nbg_chain_lpm_maglev_device, with d_gate) on that batch alone
+ * with the same flags.  One launch pays the classify kernel's ramp and tail once: a 1M IMIX batch
+ * takes 26.9 us per launch for C5 and 21.9 us per 1M at 4M packets per launch.
+ * Flags: NBG_SWAP_MACS (ignored by the chain: the two swaps cancel), NBG_OWNED_WINDOWS,
+ * NBG_DEFER_GROUP (nbg_maglev_finish_group launches the grouping of all batches); others are
+ * NBG_EINVAL.  d_off, d_len and d_backend (and d_gate for the chain) are required for a non-empty
+ * batch.  More than 1023 backends with grouping: the batches run one after another.
+ */
+typedef struct nbg_desc_batch {
+  uint8_t* d_pkts;
+  const uint32_t* d_off;
+  const uint16_t* d_len;
+  uint64_t n_pkts;
+  uint16_t* d_backend;
+  uint32_t* d_perm;    /* nullable */
+  uint32_t* d_counts;  /* nullable unless d_perm set (then n_backends + 1 u32) */
+  uint16_t* d_gate;    /* the chain's lpm gate per packet; unused by nbg_maglev_classify_desc_multi */
+} nbg_desc_batch;
+int nbg_maglev_classify_desc_multi(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_batches, uint32_t flags,
+                                   void* stream);
+
+/*
  * Persistent RX ring (the GPUDirect RX model: an RX queue that never stops, ReceiveBatch::execute
  * polling its port, framework/src/operators/receive_batch.rs:26,52-61).  nbg_ring_start launches ONE
  * streaming-classify kernel on `stream` (one block per CU: CUs - 1 classify blocks and a relay
@@ -369,6 +394,12 @@ int nbg_chain_lpm_maglev_device(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_group
                                 const uint32_t* d_off, const uint16_t* d_len, uint32_t stride, uint16_t fixed_len,
                                 uint64_t n_pkts, uint32_t flags, uint16_t* d_gate, uint16_t* d_backend,
                                 uint32_t* d_perm, uint32_t* d_counts, void* stream);
+
+/* The chain over several descriptor batches in one launch of each kernel (nbg_desc_batch, as
+ * nbg_maglev_classify_desc_multi; every batch's d_gate is required).  Each batch's gate / backend /
+ * perm / counts are those of nbg_chain_lpm_maglev_device on that batch alone. */
+int nbg_chain_lpm_maglev_multi(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_groups, const nbg_desc_batch* batches,
+                               uint32_t n_batches, uint32_t flags, void* stream);
 
 const char* nbg_last_error(void);
 

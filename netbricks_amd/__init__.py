@@ -6,7 +6,7 @@ grouping; optionally chained after test/lpm's DIR-24-8 gate) is hand-written HIP
 """
 from ._lib import NBG_HOST_SLOTS, NBG_SENTINEL, NbgError, LIB_PATH  # noqa: F401  (raises ImportError if the .so is missing)
 from .maglev import GroupedBatch, HostRegion, Maglev, Ring, build_lut, make_trace  # noqa: F401
-from .lpm import Lpm, LpmResult, build_lpm, chain_lpm_maglev  # noqa: F401
+from .lpm import Lpm, LpmResult, build_lpm, chain_lpm_maglev, chain_lpm_maglev_multi  # noqa: F401
 
 __all__ = ["Maglev", "GroupedBatch", "HostRegion", "build_lut", "make_trace", "NBG_SENTINEL", "NBG_HOST_SLOTS", "NbgError", "LIB_PATH",
-           "Lpm", "LpmResult", "build_lpm", "chain_lpm_maglev"]
+           "Lpm", "LpmResult", "build_lpm", "chain_lpm_maglev", "chain_lpm_maglev_multi"]

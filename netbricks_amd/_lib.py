@@ -36,6 +36,7 @@ NBG_MAX_MULTI = 8
 NBG_RING_SLOTS = 64
 NBG_RING_MAX_QUEUES = 16
 NBG_EBUSY = -16
+NBG_EINVAL = -22
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 
@@ -47,6 +48,13 @@ class NbgBatch(C.Structure):
     """struct nbg_batch (include/nbgpu.h): one batch of nbg_maglev_classify_device_multi."""
     _fields_ = [("d_pkts", C.c_void_p), ("n_pkts", C.c_uint64), ("d_backend", C.c_void_p),
                 ("d_perm", C.c_void_p), ("d_counts", C.c_void_p), ("d_mac_out", C.c_void_p)]
+
+
+class NbgDescBatch(C.Structure):
+    """struct nbg_desc_batch (include/nbgpu.h): one batch of nbg_maglev_classify_desc_multi /
+    nbg_chain_lpm_maglev_multi."""
+    _fields_ = [("d_pkts", C.c_void_p), ("d_off", C.c_void_p), ("d_len", C.c_void_p), ("n_pkts", C.c_uint64),
+                ("d_backend", C.c_void_p), ("d_perm", C.c_void_p), ("d_counts", C.c_void_p), ("d_gate", C.c_void_p)]
 
 
 class NbgRingBatch(C.Structure):
@@ -68,6 +76,8 @@ SIGNATURES = {
     "nbg_maglev_classify_device_ex": (C.c_int, [_P, _P, _P, _P, C.c_uint32, C.c_uint16, C.c_uint64, C.c_uint32,
                                                 _P, _P, _P, _P, _P]),
     "nbg_maglev_classify_device_multi": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint32, _P]),
+    "nbg_maglev_classify_desc_multi": (C.c_int, [_P, _P, C.c_uint32, C.c_uint32, _P]),
+    "nbg_chain_lpm_maglev_multi": (C.c_int, [_P, _P, C.c_uint32, _P, C.c_uint32, C.c_uint32, _P]),
     "nbg_maglev_finish_group": (C.c_int, [_P, _P]),
     "nbg_ring_start": (C.c_int, [_P, C.c_uint32, C.c_uint16, C.c_uint32, C.c_uint32, _P, C.POINTER(_P)]),
     "nbg_ring_post": (C.c_int, [_P, _P, C.c_uint64, _P, C.POINTER(C.c_uint64)]),

@@ -437,8 +437,10 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
 // row (the block's 64 * waves * tiles_per_wave packets divide part_pkts).
 // ABL (diagnostic builds only, selected by NBG_ABL): 1 = no hash/LUT (bin from header bytes);
 // 3 = FNV without the LUT gather; 4 = LUT gather of a trivial hash.
-template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL = 0, int NT = kBlock>
-__global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(ClassifyArgs a) {
+// The kernel body; `bid` is the block's index within its batch (classify_desc_multi_kernel runs
+// several batches' blocks in one grid).
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL, int NT>
+__device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint32_t bid) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr uint32_t kW = NT / 64u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -450,9 +452,9 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
   uint8_t* xp = smem + lut_bytes + wave * (64u * kXStride);
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + kW * 64u * kXStride);  // per block
   const uint32_t tpw = a.tiles_per_wave;
-  const uint32_t t0 = (blockIdx.x * kW + wave) * tpw;  // first 64-packet tile of this wave
+  const uint32_t t0 = (bid * kW + wave) * tpw;  // first 64-packet tile of this wave
 #ifdef NBG_CPROBE
-  const uint32_t gw = blockIdx.x * kW + wave;
+  const uint32_t gw = bid * kW + wave;
   bool first = true;
 #endif
   CPROBE(0)
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     // one flush per block into its partition row (the block's packets never straddle two):
     // 4096-packet rows take ~16 blocks' adds, so they rarely contend
     lds_sync();
-    const uint32_t p = blockIdx.x * kW * tpw * 64u / a.part_pkts;
+    const uint32_t p = bid * kW * tpw * 64u / a.part_pkts;
     if (a.hist16) {  // two bins per word: half the atomics, and half the rows' bytes for the group kernel
       const uint32_t hw = (nbins + 1) >> 1;
       uint32_t* row = a.part_hist + static_cast<size_t>(p) * hw;
@@ -588,6 +590,32 @@ __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(Cla
     }
   }
   CPROBE(3)
+}
+
+
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL = 0, int NT = kBlock>
+__global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(ClassifyArgs a) {
+  classify_body<LUTM, F4, HIST, CHAIN, LAYOUT, ABL, NT>(a, blockIdx.x);
+}
+
+// Several descriptor batches in one grid (several RX queues' bursts per launch): the launch's ramp
+// and tail are paid once for all of them.  The batch of a block is found by a wave-uniform scan of
+// blk_base (monotone; an empty batch owns no block).
+template <int LUTM, bool F4, bool HIST, bool CHAIN>
+__global__ __launch_bounds__(kBlock, CHAIN ? 1 : 2048 / kBlock) void classify_desc_multi_kernel(ClassifyArgs a,
+                                                                                                 DescBatches db) {
+  uint32_t j = 0;
+#pragma unroll
+  for (uint32_t k = 1; k < kMaxMulti; ++k) j = (k < db.n && blockIdx.x >= db.blk_base[k]) ? k : j;
+  ClassifyArgs b = a;
+  b.pkts = db.pkts[j];
+  b.off = db.off[j];
+  b.len = db.len[j];
+  b.backend = db.backend[j];
+  b.gate = db.gate[j];
+  b.part_hist = db.part_hist[j];
+  b.n_pkts = db.n_pkts[j];
+  classify_body<LUTM, F4, HIST, CHAIN, kDesc, 0, kBlock>(b, blockIdx.x - db.blk_base[j]);
 }
 
 // Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
@@ -2122,8 +2150,9 @@ __global__ __launch_bounds__(kGBlock) void hist_kernel(HistMulti hm) {
 // in registers (each row segment is one coalesced 256-B load, all 32 in flight), and the waves'
 // sums are combined through LDS.
 constexpr uint32_t kScanBins = 64, kScanWaves = kMaxParts / 32;
-__global__ __launch_bounds__(kScanWaves * 64) void scan_kernel(ScanArgs a) {
+__global__ __launch_bounds__(kScanWaves * 64) void scan_kernel(ScanMulti sm) {
   __shared__ uint32_t s_sum[kScanWaves][kScanBins];
+  const ScanArgs a = sm.s[blockIdx.y];  // batch
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
   const uint32_t b = blockIdx.x * kScanBins + lane;
   const uint32_t bc = min(b, a.nbins - 1u), q0 = wave * 32u;
@@ -3042,12 +3071,47 @@ int launch_zero(uint32_t* p, size_t words, void* stream) {
   return NBG_OK;
 }
 
-int launch_scan(const ScanArgs& a, void* stream) {
-  hipLaunchKernelGGL(scan_kernel, dim3((a.nbins + kScanBins - 1) / kScanBins), dim3(kScanWaves * 64), 0,
-                     static_cast<hipStream_t>(stream), a);
+int launch_scan_multi(const ScanMulti& sm, uint32_t n, void* stream) {
+  if (n == 0 || n > kMaxMulti) return set_error(NBG_EINVAL, "scan (multi): %u batches", n);
+  hipLaunchKernelGGL(scan_kernel, dim3((sm.s[0].nbins + kScanBins - 1) / kScanBins, n), dim3(kScanWaves * 64), 0,
+                     static_cast<hipStream_t>(stream), sm);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "scan launch: %s", hipGetErrorString(e));
   return NBG_OK;
+}
+
+int launch_scan(const ScanArgs& a, void* stream) {
+  ScanMulti sm{};
+  sm.s[0] = a;
+  return launch_scan_multi(sm, 1, stream);
+}
+
+uint32_t classify_block_pkts() { return kBlock; }  // one 64-packet tile per wave
+
+template <int LUTM, bool F4, bool HIST>
+int launch_desc_multi_v(const ClassifyArgs& a, const DescBatches& db, size_t lds, hipStream_t s) {
+  auto fn = a.tbl24 ? classify_desc_multi_kernel<LUTM, F4, HIST, true> : classify_desc_multi_kernel<LUTM, F4, HIST, false>;
+  hipLaunchKernelGGL(fn, dim3(db.blk_base[db.n]), dim3(kBlock), lds, s, a, db);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "classify launch (descriptor multi): %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+int launch_classify_desc_multi(const ClassifyArgs& a, const DescBatches& db, bool wide_lut, void* stream) {
+  if (db.n == 0 || db.n > kMaxMulti || a.tiles_per_wave != 1u)
+    return set_error(NBG_EINVAL, "classify (descriptor multi): %u batches, %u tiles per wave", db.n, a.tiles_per_wave);
+  if (db.blk_base[db.n] == 0) return NBG_OK;
+  const bool hist = db.part_hist[0] != nullptr;
+  const size_t lds = classify_lds(a.nb, 0);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (wide_lut) {
+    if (a.m == 65537u)
+      return hist ? launch_desc_multi_v<kGlobalU16, true, true>(a, db, lds, s) : launch_desc_multi_v<kGlobalU16, true, false>(a, db, lds, s);
+    return hist ? launch_desc_multi_v<kGlobalU16, false, true>(a, db, lds, s) : launch_desc_multi_v<kGlobalU16, false, false>(a, db, lds, s);
+  }
+  if (a.m == 65537u)
+    return hist ? launch_desc_multi_v<kGlobalU8, true, true>(a, db, lds, s) : launch_desc_multi_v<kGlobalU8, true, false>(a, db, lds, s);
+  return hist ? launch_desc_multi_v<kGlobalU8, false, true>(a, db, lds, s) : launch_desc_multi_v<kGlobalU8, false, false>(a, db, lds, s);
 }
 
 int launch_classify_idx(const ClassifyArgs& a, int grid, void* stream) {
@@ -3183,10 +3247,12 @@ int launch_group(const GroupArgs& a, int scan, void* stream) {
 
 int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream) {
   const GroupArgs& a = gm.g[0];
-  if (n == 0 || n > kMaxMulti || scan == kScanKernel) return set_error(NBG_EINVAL, "group (multi): %u batches", n);
+  if (n == 0 || n > kMaxMulti) return set_error(NBG_EINVAL, "group (multi): %u batches", n);
   const size_t lds = group_lds(a.nb + 1, gm.per, scan);
-  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7> : group_kernel<kScanLds, 7>)
-                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10> : group_kernel<kScanLds, 10>);
+  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7>
+                                                : (scan == kScanLds ? group_kernel<kScanLds, 7> : group_kernel<kScanKernel, 7>))
+                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10>
+                                               : (scan == kScanLds ? group_kernel<kScanLds, 10> : group_kernel<kScanKernel, 10>));
   if (lds > 64 * 1024) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                             static_cast<int>(lds)) != hipSuccess)

@@ -83,6 +83,10 @@ struct nbg_maglev {
   ScanArgs pending_scan{};
   uint32_t pending_multi = 0;         // > 0: the deferred group is a multi-batch group launch
   GroupMulti pending_gm{};
+  bool pending_hist_multi = false;    // ... preceded by a multi-batch hist launch (many backends)
+  HistMulti pending_hm{};
+  ScanMulti pending_sm{};             // ... and a multi-batch scan launch (pending_scan_mode == kScanKernel)
+  uint32_t* d_prefix_multi = nullptr; // [kMaxMulti][kMaxParts][nb+1] prefixes + [kMaxMulti][nb+1] totals (descriptor multi, scan kernel)
   // lagged grouping (NBG_GROUP_LAG): three rotating partition-histogram sets; a lagged classify
   // accumulates into set lag_idx, groups the pending batch from the previous set and zeroes the third
   bool pending_lag = false;           // the pending group is a lagged one (pending_args / pending_lg)
@@ -256,6 +260,8 @@ void free_scratch(nbg_maglev* h) {
   (void)hipFree(h->d_bin_base);
   (void)hipFree(h->d_sink);
   (void)hipFree(h->d_part_multi);
+  (void)hipFree(h->d_prefix_multi);
+  h->d_prefix_multi = nullptr;
   (void)hipFree(h->d_part_lag);
   (void)hipFree(h->d_counts);
   h->d_part_lag = nullptr;
@@ -896,9 +902,191 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   return NBG_OK;
 }
 
+// Several descriptor batches (IMIX: u32 offset + u16 length per packet; several RX queues' bursts)
+// through one tile-per-wave classify launch, then one hist (many backends), one scan (many
+// partitions x bins) and one group launch over all of them.  The launch's ramp and tail, ~6.7 us of a
+// 1M C5 batch's 26.9 us on one launch (profiles/r04_desc_size_sweep.txt), are paid once per call.
+int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_batches, uint32_t flags,
+                      const nbg_lpm* lpm, uint32_t lpm_groups, void* stream) {
+  const char* what = lpm ? "chain (multi)" : "classify (descriptor multi)";
+  if (!h) return set_error(NBG_EINVAL, "%s: null handle", what);
+  if (!batches || n_batches == 0 || n_batches > NBG_MAX_MULTI)
+    return set_error(NBG_EINVAL, "%s: 1..%u batches", what, NBG_MAX_MULTI);
+  if (flags & ~(NBG_SWAP_MACS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP))
+    return set_error(NBG_EINVAL, "%s: flags other than NBG_SWAP_MACS, NBG_OWNED_WINDOWS and NBG_DEFER_GROUP", what);
+  if (h->ring) return set_error(NBG_EBUSY, "%s: the handle's persistent ring is running", what);
+  if (lpm && lpm->device != h->device) return set_error(NBG_EINVAL, "%s: lpm and maglev handles on different devices", what);
+  if (h->pending_lag) {  // a pending lagged group is launched alone first
+    const int rc = nbg_maglev_finish_group(h, stream);
+    if (rc) return rc;
+  }
+  if (h->pending) return set_error(NBG_EINVAL, "%s: a deferred group is pending (nbg_maglev_finish_group)", what);
+  const bool group = batches[0].d_perm || batches[0].d_counts;
+  uint64_t max_n = 0;
+  for (uint32_t j = 0; j < n_batches; ++j) {
+    const nbg_desc_batch& x = batches[j];
+    if ((x.d_perm || x.d_counts) != group)
+      return set_error(NBG_EINVAL, "%s: batch %u: every batch or none has perm/counts", what, j);
+    if (x.n_pkts >= (1ull << 30)) return set_error(NBG_EINVAL, "%s: batch %u: n_pkts must be < 2^30", what, j);
+    if (x.n_pkts && (!x.d_pkts || !x.d_off || !x.d_len || !x.d_backend || (lpm && !x.d_gate)))
+      return set_error(NBG_EINVAL, "%s: batch %u: null packet, offset, length, backend%s buffer", what, j,
+                       lpm ? " or gate" : "");
+    max_n = std::max<uint64_t>(max_n, x.n_pkts);
+  }
+  const uint32_t nbins = h->nb + 1;
+  if (group && nbins > kMaxGroupBins) {
+    // the wide grouping path has no multi-batch form: one batch after another (same results)
+    if (flags & NBG_DEFER_GROUP)
+      return set_error(NBG_EINVAL, "%s: NBG_DEFER_GROUP needs at most %u backends", what, kMaxGroupBins - 1);
+    for (uint32_t j = 0; j < n_batches; ++j) {
+      const nbg_desc_batch& x = batches[j];
+      const int rc = classify_common(h, x.d_pkts, x.d_off, x.d_len, 0, 0, x.n_pkts, flags, x.d_backend, x.d_perm,
+                                     x.d_counts, nullptr, lpm, lpm_groups, x.d_gate, stream);
+      if (rc) return rc;
+    }
+    return NBG_OK;
+  }
+  DeviceGuard g(h->device);
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  NBG_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cap));
+  if (cap != hipStreamCaptureStatusNone) return set_error(NBG_EINVAL, "%s: cannot be captured in a graph", what);
+  // one partition size for every batch (as the fixed-slot multi path): the group grid is
+  // n_batches x the largest batch's partitions
+  const uint64_t per = (max_n + kChunk * kMaxParts - 1) / (kChunk * kMaxParts);
+  const uint32_t part_pkts = static_cast<uint32_t>(std::max<uint64_t>(per, 1) * kChunk);
+  const uint32_t n_parts_max = static_cast<uint32_t>(std::max<uint64_t>((max_n + part_pkts - 1) / part_pkts, 1));
+  const bool hist_k = group && !hist_in_classify(nbins);
+  const int scan = group ? pick_group_scan(nbins, n_parts_max) : kScanDirect;
+  const size_t set_words = static_cast<size_t>(kMaxMulti) * kMaxParts * nbins;
+  if (group && !h->d_part_multi) {
+    NBG_HIP(hipMalloc(&h->d_part_multi, 2 * set_words * sizeof(uint32_t)));
+    SetupStream st;
+    (void)st.zero(h->d_part_multi, 2 * set_words * sizeof(uint32_t));
+    NBG_HIP(st.finish());
+  }
+  if (group && scan == kScanKernel && !h->d_prefix_multi)
+    NBG_HIP(hipMalloc(&h->d_prefix_multi, (set_words + static_cast<size_t>(kMaxMulti) * nbins) * sizeof(uint32_t)));
+  int rc = order_after_last(h, static_cast<hipStream_t>(stream));
+  if (rc) return rc;
+  uint32_t* set_cur = group ? h->d_part_multi + static_cast<size_t>(h->mparity) * set_words : nullptr;
+  uint32_t* set_next = group ? h->d_part_multi + static_cast<size_t>(h->mparity ^ 1u) * set_words : nullptr;
+  ClassifyArgs a{};
+  a.tiles_per_wave = 1;
+  a.lut = h->d_lut;
+  a.m = static_cast<uint32_t>(h->m);
+  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
+  a.nb = h->nb;
+  a.swap = (flags & NBG_SWAP_MACS) && !lpm ? 1u : 0u;  // chain: lpm's and maglev's swaps cancel
+  a.win_owned = (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
+  a.wb_full = 1u;
+  a.part_pkts = part_pkts;
+  // partition rows from the classify kernel's flush (few backends, rows accumulated: zeroed by the
+  // previous call's group launch) or from hist_kernel (many, rows stored whole)
+  a.hist16 = group && !hist_k && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
+  if (lpm) {
+    a.tbl24 = lpm->d_tbl24;
+    a.tbl_long = lpm->d_tbl_long;
+    a.lpm_groups = lpm_groups;
+  }
+  const uint32_t bp = classify_block_pkts();
+  DescBatches db{};
+  GroupMulti gm{};
+  HistMulti hm{};
+  ScanMulti sm{};
+  uint32_t bits = 0;
+  while ((1u << bits) < nbins) ++bits;
+  uint32_t blocks = 0;
+  for (uint32_t j = 0; j < n_batches; ++j) {
+    const nbg_desc_batch& x = batches[j];
+    const uint32_t n = static_cast<uint32_t>(x.n_pkts);
+    const uint32_t n_parts = n ? (n + part_pkts - 1) / part_pkts : 0u;
+    uint32_t* rows = group ? set_cur + static_cast<size_t>(j) * kMaxParts * nbins : nullptr;
+    db.pkts[j] = x.d_pkts;
+    db.off[j] = x.d_off;
+    db.len[j] = x.d_len;
+    db.backend[j] = x.d_backend;
+    db.gate[j] = x.d_gate;
+    db.part_hist[j] = group && !hist_k ? rows : nullptr;
+    db.n_pkts[j] = n;
+    db.blk_base[j] = blocks;
+    blocks += (n + bp - 1) / bp;
+    if (!group) continue;
+    HistArgs& ha = hm.h[j];
+    ha.backend = x.d_backend;
+    ha.n_pkts = n;
+    ha.nb = h->nb;
+    ha.part_pkts = part_pkts;
+    ha.n_parts = n_parts;
+    ha.part_hist = rows;
+    uint32_t* pre = h->d_prefix_multi ? h->d_prefix_multi + static_cast<size_t>(j) * kMaxParts * nbins : nullptr;
+    uint32_t* tot = h->d_prefix_multi ? h->d_prefix_multi + set_words + static_cast<size_t>(j) * nbins : nullptr;
+    ScanArgs& sa = sm.s[j];
+    sa.part_hist = rows;
+    sa.part_prefix = pre;
+    sa.totals = tot;
+    sa.n_parts = std::max(n_parts, 1u);  // an empty batch scans row 0 (in bounds, unused: no group block)
+    sa.nbins = nbins;
+    GroupArgs& ga = gm.g[j];
+    ga.backend = x.d_backend;
+    ga.n_pkts = n;
+    ga.nb = h->nb;
+    ga.bits = bits;
+    ga.n_parts = n_parts;
+    ga.part_pkts = part_pkts;
+    ga.part_hist = rows;
+    ga.part_prefix = pre;
+    ga.totals = tot;
+    ga.hist16 = a.hist16;
+    ga.part_hist_next = hist_k ? nullptr : set_next;  // hist_kernel stores whole rows: nothing to zero
+    ga.next_words = hist_k ? 0u : static_cast<uint32_t>(set_words);
+    ga.counts = x.d_counts ? x.d_counts : h->d_counts;
+    ga.perm = x.d_perm;
+  }
+  db.blk_base[n_batches] = blocks;
+  db.n = n_batches;
+  hm.per = n_parts_max;
+  gm.per = n_parts_max;
+  // what the batches share; per-batch pointers come from db (a's copies only select the layout)
+  a.pkts = db.pkts[0];
+  a.off = db.off[0];
+  a.len = db.len[0];
+  h->last_stream = static_cast<hipStream_t>(stream);
+  h->issued = true;
+  for (uint32_t j = 0; j < n_batches; ++j)  // an empty batch's counts (no group block writes them)
+    if (batches[j].n_pkts == 0 && batches[j].d_counts && (rc = zero_captured(batches[j].d_counts, nbins, stream)))
+      return rc;
+  if ((rc = launch_classify_desc_multi(a, db, h->wide, stream))) return rc;
+  if (!group) return NBG_OK;
+  h->mparity ^= 1u;
+  if (flags & NBG_DEFER_GROUP) {
+    h->pending = true;
+    h->pending_multi = n_batches;
+    h->pending_gm = gm;
+    h->pending_hist_multi = hist_k;
+    h->pending_hm = hm;
+    h->pending_sm = sm;
+    h->pending_scan_mode = scan;
+    return NBG_OK;
+  }
+  if (hist_k && (rc = launch_hist_multi(hm, n_batches, stream))) return rc;
+  if (scan == kScanKernel && (rc = launch_scan_multi(sm, n_batches, stream))) return rc;
+  return launch_group_multi(gm, n_batches, scan, stream);
+}
+
 }  // namespace
 
 extern "C" {
+
+int nbg_maglev_classify_desc_multi(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_batches, uint32_t flags,
+                                   void* stream) {
+  return desc_multi_common(h, batches, n_batches, flags, nullptr, 0, stream);
+}
+
+int nbg_chain_lpm_maglev_multi(nbg_maglev* mg, nbg_lpm* lpm, uint32_t lpm_groups, const nbg_desc_batch* batches,
+                               uint32_t n_batches, uint32_t flags, void* stream) {
+  if (!lpm) return set_error(NBG_EINVAL, "chain (multi): null lpm handle");
+  return desc_multi_common(mg, batches, n_batches, flags & ~NBG_SWAP_MACS, lpm, lpm_groups, stream);
+}
 
 int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
                                   uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
@@ -1033,6 +1221,7 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
       h->pending = true;
       h->pending_multi = n_batches;
       h->pending_gm = gm;
+      h->pending_hist_multi = false;
       h->pending_scan_mode = scan;
       return NBG_OK;
     }
@@ -1110,11 +1299,13 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
   if (h->pending_lag) return flush_lag(h, static_cast<hipStream_t>(stream));
   h->pending = false;
   if (h->pending_multi) {
-    // the fused multi path is taken only with the partition rows in the classify kernel and the
-    // direct (or LDS) scan in the group prologue (nbg_maglev_classify_device_multi), so there is no
-    // hist or scan kernel to launch here, unlike the single-batch branch below
+    // fixed slots (nbg_maglev_classify_device_multi): partition rows from the classify kernel and the
+    // direct scan, one group launch; descriptor batches with many backends
+    // (nbg_maglev_classify_desc_multi) also a hist and a scan launch, each over all batches
     const uint32_t n = h->pending_multi;
     h->pending_multi = 0;
+    if (h->pending_hist_multi && (rc = launch_hist_multi(h->pending_hm, n, stream))) return rc;
+    if (h->pending_scan_mode == kScanKernel && (rc = launch_scan_multi(h->pending_sm, n, stream))) return rc;
     return launch_group_multi(h->pending_gm, n, h->pending_scan_mode, stream);
   }
   if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;

@@ -201,6 +201,26 @@ struct ScanArgs {
   uint32_t nbins;
 };
 
+// scan_kernel over several batches: blockIdx.y = batch
+struct ScanMulti {
+  ScanArgs s[kMaxMulti];
+};
+
+// Several descriptor-layout batches (IMIX: u32 offset + u16 length per packet) in one launch of the
+// tile-per-wave classify kernel (nbg_maglev_classify_desc_multi / nbg_chain_lpm_maglev_multi): what
+// differs per batch.  Blocks [blk_base[j], blk_base[j + 1]) classify batch j (tiles never straddle).
+struct DescBatches {
+  uint8_t* pkts[kMaxMulti];
+  const uint32_t* off[kMaxMulti];
+  const uint16_t* len[kMaxMulti];
+  uint16_t* backend[kMaxMulti];
+  uint16_t* gate[kMaxMulti];        // chain only
+  uint32_t* part_hist[kMaxMulti];   // nullable: partition rows written by the classify kernel
+  uint32_t n_pkts[kMaxMulti];
+  uint32_t blk_base[kMaxMulti + 1];
+  uint32_t n;
+};
+
 struct GroupArgs {
   const uint16_t* backend;
   uint32_t n_pkts;
@@ -255,6 +275,11 @@ int stream_waves_per_block();
 int launch_classify_stream_desc(const ClassifyArgs& a, bool wide_lut, int grid, void* stream);
 size_t stream_desc_lds(uint32_t nb, int mode, bool wide_lut);
 int launch_scan(const ScanArgs& a, void* stream);
+int launch_scan_multi(const ScanMulti& sm, uint32_t n, void* stream);
+// the tile-per-wave classify kernel (256 threads, one 64-packet tile per wave) over db.n descriptor
+// batches; a carries what they share (LUT, flags, lpm tables), db what differs
+int launch_classify_desc_multi(const ClassifyArgs& a, const DescBatches& db, bool wide_lut, void* stream);
+uint32_t classify_block_pkts();  // packets per block of launch_classify_desc_multi
 int launch_zero(uint32_t* p, size_t words, void* stream);  // p[0, words) = 0 (one kernel)
 int launch_hist(const HistArgs& a, void* stream);
 int launch_hist_multi(const HistMulti& hm, uint32_t n, void* stream);  // nb + 1 <= 16384

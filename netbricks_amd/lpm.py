@@ -18,7 +18,7 @@ from . import _lib
 from ._lib import NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_STREAM_DESC, check, lib
 from .maglev import GroupedBatch, Maglev, _ptr
 
-__all__ = ["Lpm", "build_lpm", "chain_lpm_maglev", "LpmResult"]
+__all__ = ["Lpm", "build_lpm", "chain_lpm_maglev", "chain_lpm_maglev_multi", "LpmResult"]
 
 Route = Tuple[Union[str, int], int, int]
 
@@ -113,3 +113,20 @@ def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int
                                          _ptr(perm) if group else None, _ptr(counts) if group else None, stream)
     check(rc, "nbg_chain_lpm_maglev_device")
     return LpmResult(gate, backend, perm if group else None, counts if group else None)
+
+
+def chain_lpm_maglev_multi(mg: Maglev, lpm: Lpm, batches, *, lpm_groups: int = 3, owned_windows: bool = True,
+                           group: bool = True, defer_group: bool = False, stream=None) -> list:
+    """lpm(...) -> maglev(...) over several descriptor batches ((pkts, offsets, lens, n_pkts) each) in
+    one launch of each kernel (nbg_chain_lpm_maglev_multi).  Returns one LpmResult per batch, as
+    chain_lpm_maglev would give it for that batch alone."""
+    import torch
+
+    arr, out = mg._desc_batches(batches, group, True, True)
+    if stream is None:
+        stream = torch.cuda.current_stream(torch.device("cuda", mg.device)).cuda_stream
+    flags = (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_DEFER_GROUP if defer_group else 0)
+    check(lib.nbg_chain_lpm_maglev_multi(mg._h, lpm._h, lpm_groups, arr, len(batches), flags, stream),
+          "nbg_chain_lpm_maglev_multi")
+    mg._multi_keep = arr
+    return [LpmResult(g, b, p, c) for b, p, c, g in out]

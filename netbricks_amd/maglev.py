@@ -17,7 +17,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, NBG_LUT_TILED, NBG_MAX_MULTI, NBG_OWNED_WINDOWS,
-                   NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch, NbgRingBatch,
+                   NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch, NbgDescBatch, NbgRingBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
 __all__ = ["Maglev", "GroupedBatch", "Ring", "RingQueue", "build_lut", "make_trace", "NBG_SENTINEL"]
@@ -263,6 +263,53 @@ class Maglev:
               "nbg_maglev_classify_device_multi")
         self._multi_keep = arr
         return [g for g, _ in out] if not records else out
+
+    def _desc_batches(self, batches, group: bool, scatter: bool, gates: bool):
+        """ctypes array of nbg_desc_batch for group_by_desc_multi / chain_lpm_maglev_multi: `batches`
+        is a list of (pkts, offsets, lens, n_pkts) device tensors (u8, u32, u16) on this device."""
+        import torch
+
+        if not 1 <= len(batches) <= NBG_MAX_MULTI:
+            raise ValueError(f"batches: 1..{NBG_MAX_MULTI}")
+        arr = (NbgDescBatch * len(batches))()
+        out = []
+        for j, (pkts, offsets, lens, n_pkts) in enumerate(batches):
+            dev = pkts.device
+            if pkts.dtype != torch.uint8 or not pkts.is_contiguous():
+                raise ValueError(f"batch {j}: expected a contiguous uint8 tensor")
+            if dev.type != "cuda" or dev.index != self.device:
+                raise ValueError(f"batch {j}: on {dev}, expected cuda:{self.device}")
+            _check_dev(f"batch {j} offsets", offsets, torch.uint32, n_pkts, dev)
+            _check_dev(f"batch {j} lens", lens, torch.uint16, n_pkts, dev)
+            if n_pkts and (offsets is None or lens is None):
+                raise ValueError(f"batch {j}: offsets and lens are required")
+            backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
+            perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev) if group and scatter else None
+            counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev) if group else None
+            gate = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev) if gates else None
+            arr[j] = NbgDescBatch(_ptr(pkts), _ptr(offsets), _ptr(lens), n_pkts, _ptr(backend), _ptr(perm),
+                                  _ptr(counts), _ptr(gate))
+            out.append((backend, perm, counts, gate))
+        return arr, out
+
+    def group_by_desc_multi(self, batches, *, swap_macs: bool = True, owned_windows: bool = True,
+                            group: bool = True, scatter: bool = True, defer_group: bool = False,
+                            stream=None) -> list:
+        """Classify several device-resident descriptor batches (IMIX: (pkts, offsets, lens, n_pkts)
+        per batch) in one launch of each kernel (nbg_maglev_classify_desc_multi).  Every batch gets
+        its own backend / perm / counts, as group_by(..., offsets=, lens=) would give it alone.
+        Returns one GroupedBatch per batch."""
+        import torch
+
+        arr, out = self._desc_batches(batches, group, scatter, False)
+        if stream is None:
+            stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
+        flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_OWNED_WINDOWS if owned_windows else 0)
+                 | (NBG_DEFER_GROUP if defer_group else 0))
+        check(lib.nbg_maglev_classify_desc_multi(self._h, arr, len(batches), flags, stream),
+              "nbg_maglev_classify_desc_multi")
+        self._multi_keep = arr
+        return [GroupedBatch(b, p, c) for b, p, c, _ in out]
 
     def finish_group(self, stream=None) -> None:
         """Launch the grouping deferred by group_by(..., defer_group=True) or left pending by

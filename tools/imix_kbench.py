@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS (NBG_LUT_LDS)")
     ap.add_argument("--n", default=str(1 << 20), help="comma-separated batch sizes (packets); times are also per 1M")
+    ap.add_argument("--multi", default="", help="comma-separated batches per launch (descriptor multi path, 1M "
+                                               "IMIX batches); also times the grouping launches")
     args = ap.parse_args()
     import torch
 
@@ -39,6 +41,10 @@ def main():
         lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
     routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
     out = {"lib": os.environ.get("NBG_LIB_OVERRIDE", "in-tree")}
+    if args.multi:
+        multi(args, torch, nb, KernelTimer, routes, out)
+        print(json.dumps(out), flush=True)
+        return
     st = torch.cuda.Stream(dev)
     backend = torch.empty(n, dtype=torch.uint16, device=dev)
     perm = torch.empty(n, dtype=torch.uint32, device=dev)
@@ -84,6 +90,56 @@ def main():
         if which == "c5":
             lpm.close()
     print(json.dumps(out), flush=True)
+
+
+def multi(args, torch, nb, KernelTimer, routes, out):
+    """nbg_maglev_classify_desc_multi / nbg_chain_lpm_maglev_multi over K distinct 1M IMIX batches:
+    the classify launch and the deferred grouping launches (finish_group) timed separately, one stream."""
+    dev = torch.device("cuda:0")
+    n = 1 << 20
+    ks = [int(k) for k in args.multi.split(",")]
+    dbs = []
+    for b in range(max(ks)):
+        buf, off, ln = nb.make_trace(n, 1, seed=1000 + b)
+        dbs.append((torch.from_numpy(buf).to(dev), torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32),
+                    torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16), n))
+    st = torch.cuda.Stream(dev)
+    for rnd in range(args.rounds):
+        for which in args.which.split(","):
+            for k in ks:
+                if which == "c5":
+                    mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
+                    lpm = nb.Lpm(routes["reference"] + routes["mixed"])
+
+                    def call():
+                        nb.chain_lpm_maglev_multi(mg, lpm, dbs[:k], defer_group=True, stream=st.cuda_stream)
+                else:
+                    mg = nb.Maglev([f"be{i}" for i in range(1000)], 655373)
+
+                    def call():
+                        mg.group_by_desc_multi(dbs[:k], defer_group=True, stream=st.cuda_stream)
+                for _ in range(4):
+                    call()
+                    mg.finish_group(st.cuda_stream)
+                torch.cuda.synchronize()
+                kt, gt = KernelTimer(args.iters), KernelTimer(args.iters)
+                for i in range(args.iters):
+                    kt.start(i, st.cuda_stream)
+                    call()
+                    kt.stop(i, st.cuda_stream)
+                    gt.start(i, st.cuda_stream)
+                    mg.finish_group(st.cuda_stream)
+                    gt.stop(i, st.cuda_stream)
+                torch.cuda.synchronize()
+                mg.check()
+                c, g = float(kt.ms().mean()) * 1e3, float(gt.ms().mean()) * 1e3
+                kt.close()
+                gt.close()
+                out[f"{which}_multi{k}_r{rnd}"] = {"classify_us": round(c, 2), "classify_us_per_batch": round(c / k, 2),
+                                                   "group_us": round(g, 2), "group_us_per_batch": round(g / k, 2)}
+                mg.close()
+                if which == "c5":
+                    lpm.close()
 
 
 if __name__ == "__main__":
