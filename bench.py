@@ -77,6 +77,9 @@ RING_GROUP_BURST = int(os.environ.get("NBG_BENCH_RING_GROUP_BURST", "2"))  # 1M 
 C4_GROUP_BURST = int(os.environ.get("NBG_BENCH_C4_GROUP_BURST", "8"))      # C4 shards per nbg_ring_group_burst
 C4_GROUP_STREAMS = int(os.environ.get("NBG_BENCH_C4_GROUP_STREAMS", "2"))
 MULTI_STREAMS = int(os.environ.get("NBG_BENCH_MULTI_STREAMS", "2"))
+# C3 / C5 (IMIX descriptors): batches per multi-batch launch and streams (each stream its own inputs)
+IMIX_MULTI_K = int(os.environ.get("NBG_BENCH_IMIX_MULTI_K", "8"))
+IMIX_MULTI_STREAMS = int(os.environ.get("NBG_BENCH_IMIX_MULTI_STREAMS", "2"))
 SEED = 0x4E42474D41474C56
 # algorithmic bytes per packet of the classify kernel per variant:
 #   in place: 64 B packet read + 12 B MAC write + 2 B backend write
@@ -1340,56 +1343,55 @@ def run_rank(args) -> None:
     # ---- C3 / C5 with several RX queues' IMIX batches per launch (nbg_maglev_classify_desc_multi,
     #      nbg_chain_lpm_maglev_multi): MULTI_K distinct 1M IMIX batches per call, each stream its own
     #      MULTI_K inputs (no buffer is in two calls in flight), per-batch outputs
-    def imix_multi_setup():
+    def imix_multi_setup(k, ms):
+        """k distinct 1M IMIX inputs per stream for ms streams (no buffer is in two calls in flight),
+        per-batch outputs, one nbg_desc_batch array per (config, k, stream)."""
         x = imix_setup()
-        if "marr" in x:
+        x.setdefault("marr", {})
+        x.setdefault("mkeep", [])
+        if ("c3", k, ms - 1) in x["marr"]:
             return x
         from netbricks_amd._lib import NbgDescBatch
-        ms = min(MULTI_STREAMS, S)
-        need = ms * MULTI_K
-        for b in range(len(x["bufs"]), need):
+        for b in range(len(x["bufs"]), k * ms):
             buf, off, ln = nb.make_trace(BATCH, 1, seed=1000 + b)
             x["bufs"].append(torch.from_numpy(buf).to(dev))
             x["offs"].append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
             x["lens"].append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
-        marr = {}
-        keep = []
         for cfg, nbins in (("c3", 1001), ("c5", N_BACKENDS + 1)):
             for j in range(ms):
-                arr = (NbgDescBatch * MULTI_K)()
-                for q in range(MULTI_K):
-                    k = j * MULTI_K + q
+                arr = (NbgDescBatch * k)()
+                for q in range(k):
+                    i = j * k + q
                     o = [torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
                          torch.empty(nbins, dtype=torch.uint32, device=dev), torch.empty(BATCH, dtype=torch.uint16, device=dev)]
-                    keep.append(o)
-                    arr[q] = NbgDescBatch(x["bufs"][k].data_ptr(), x["offs"][k].data_ptr(), x["lens"][k].data_ptr(), BATCH,
+                    x["mkeep"].append(o)
+                    arr[q] = NbgDescBatch(x["bufs"][i].data_ptr(), x["offs"][i].data_ptr(), x["lens"][i].data_ptr(), BATCH,
                                           o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
                                           o[3].data_ptr() if cfg == "c5" else None)
-                marr[(cfg, j)] = arr
-        x.update(marr=marr, mkeep=keep, mstreams=ms)
+                x["marr"][(cfg, k, j)] = arr
         return x
 
-    def imix_mcall(cfg, j, stream, defer=False):
+    def imix_mcall(cfg, k, j, stream, defer=False):
         x = imix
         flags = NBG_OWNED_WINDOWS | (NBG_DEFER_GROUP if defer else 0)
         if cfg == "c3":
-            rc = clib.nbg_maglev_classify_desc_multi(x["c3"][j]._h, x["marr"][("c3", j)], MULTI_K, flags | NBG_SWAP_MACS,
+            rc = clib.nbg_maglev_classify_desc_multi(x["c3"][j]._h, x["marr"][("c3", k, j)], k, flags | NBG_SWAP_MACS,
                                                      stream)
         else:
-            rc = clib.nbg_chain_lpm_maglev_multi(mgs[j]._h, x["lpm"]._h, 3, x["marr"][("c5", j)], MULTI_K, flags, stream)
+            rc = clib.nbg_chain_lpm_maglev_multi(mgs[j]._h, x["lpm"]._h, 3, x["marr"][("c5", k, j)], k, flags, stream)
         if rc:
             from netbricks_amd._lib import last_error
             raise RuntimeError(f"{cfg} multi call: {rc} {last_error()}")
 
-    def imix_multi_variant(cfg, steps, warmup):
-        """C3 / C5 with MULTI_K IMIX batches of 1M per call on MULTI_STREAMS streams (whole-job rate),
-        then the multi-batch classify launch alone (events, grouping deferred)."""
-        x = imix_multi_setup()
-        ms = x["mstreams"]
+    def imix_multi_variant(cfg, steps, warmup, k=IMIX_MULTI_K, ms=IMIX_MULTI_STREAMS):
+        """C3 / C5 with k IMIX batches of 1M per call on ms streams (whole-job rate), then the
+        multi-batch classify launch alone (events, grouping deferred)."""
+        ms = min(ms, S)
+        x = imix_multi_setup(k, ms)
         cm = x["c3"] if cfg == "c3" else mgs
-        calls = max(steps * BATCHES_PER_STEP // MULTI_K, 10)
+        calls = max(steps * BATCHES_PER_STEP // k, 10)
         for i in range(max(warmup, 2) * ms):
-            imix_mcall(cfg, i % ms, sts[i % ms])
+            imix_mcall(cfg, k, i % ms, sts[i % ms])
         sync_all()
         start_ev = torch.cuda.Event()
         start_ev.record(torch.cuda.current_stream(dev))
@@ -1397,14 +1399,14 @@ def run_rank(args) -> None:
             st.wait_event(start_ev)
         t1 = time.perf_counter()
         for i in range(calls):
-            imix_mcall(cfg, i % ms, sts[i % ms])
+            imix_mcall(cfg, k, i % ms, sts[i % ms])
         sync_all()
         el = time.perf_counter() - t1
         st = sts[0]
         kt = KernelTimer(calls)
         for i in range(calls):
             kt.start(i, st)
-            imix_mcall(cfg, 0, st, defer=True)
+            imix_mcall(cfg, k, 0, st, defer=True)
             kt.stop(i, st)
             cm[0].finish_group(st)
         sync_all()
@@ -1413,13 +1415,13 @@ def run_rank(args) -> None:
         kus = float(kt.ms().mean()) * 1e3
         kt.close()
         cb = C3_BYTES if cfg == "c3" else C5_BYTES
-        ach = MULTI_K * BATCH * cb["classify"] / kus / 1e3
-        return {"value": round(MULTI_K * BATCH * calls / el / 1e6, 1), "unit": "Mpps",
-                "ms_per_batch": round(el / (calls * MULTI_K) * 1e3, 5), "batches_per_launch": MULTI_K, "streams": ms,
-                "avg_launch_us": round(kus, 2), "classify_us_per_batch": round(kus / MULTI_K, 2),
+        ach = k * BATCH * cb["classify"] / kus / 1e3
+        return {"value": round(k * BATCH * calls / el / 1e6, 1), "unit": "Mpps",
+                "ms_per_batch": round(el / (calls * k) * 1e3, 5), "batches_per_launch": k, "streams": ms,
+                "avg_launch_us": round(kus, 2), "classify_us_per_batch": round(kus / k, 2),
                 "classify_bytes_per_pkt": cb["classify"], "path_bytes_per_pkt": cb["path"],
                 "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4),
-                "what": (f"{cfg.upper()} with {MULTI_K} RX queues' 1M IMIX batches per launch "
+                "what": (f"{cfg.upper()} with {k} RX queues' 1M IMIX batches per launch "
                          f"({'nbg_maglev_classify_desc_multi' if cfg == 'c3' else 'nbg_chain_lpm_maglev_multi'}: one "
                          "classify launch, then one hist / scan / group launch over all batches, per-batch outputs), "
                          f"{ms} streams with distinct inputs; classify_us_per_batch from the multi launch timed alone")}
@@ -1626,8 +1628,17 @@ def run_rank(args) -> None:
                 variants["c5_lut_lds"]["what"] = (
                     "C5 with the u8 LUT staged in LDS (NBG_LUT_LDS: one 1024-thread block per CU, two tiles' loads "
                     "in flight per wave): removes the LUT's L2 gather from every wave's critical path")
-                variants[f"c3_multi{MULTI_K}"] = imix_multi_variant("c3", args.steps, args.warmup)
-                variants[f"c5_multi{MULTI_K}"] = imix_multi_variant("c5", args.steps, args.warmup)
+                variants[f"c3_multi{IMIX_MULTI_K}"] = imix_multi_variant("c3", args.steps, args.warmup)
+                variants[f"c5_multi{IMIX_MULTI_K}"] = imix_multi_variant("c5", args.steps, args.warmup)
+                sweep_spec = os.environ.get("NBG_BENCH_IMIX_SWEEP", "")  # measurement: "KxS,..."
+                if sweep_spec:
+                    isw = {}
+                    for spec in sweep_spec.split(","):
+                        k, m = (int(v) for v in spec.split("x"))
+                        for cfg in ("c3", "c5"):
+                            r = imix_multi_variant(cfg, args.steps, args.warmup, k=k, ms=m)
+                            isw[f"{cfg}_{spec}"] = {q: r[q] for q in ("ms_per_batch", "classify_us_per_batch", "value")}
+                    variants["imix_multi_sweep"] = isw
 
     if rank == 0:
         cpu = None

@@ -2497,11 +2497,14 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
   const uint32_t nbp = (nbins + 3) & ~3u;
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbp;          // [nbins]
-  const uint32_t cst = (nbins + 4) & ~3u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
-  uint32_t* cnt = tot + nbp;           // [kW][cst]
-  uint32_t* sidx = cnt + kW * cst;     // [kChunk]
-  uint16_t* sbin = reinterpret_cast<uint16_t*>(sidx + kChunk);  // [kChunk]
-  uint32_t* ph = reinterpret_cast<uint32_t*>(sbin + kChunk);    // [n_parts][nbins] (kScanLds)
+  // 16-bit per-wave counters (a wave counts <= 512 packets of a chunk; chunk slots < kChunk) and one
+  // word per sorted slot (bin << 12 | packet within the chunk): 40 KB of LDS at 1001 bins instead of
+  // 64 KB, so that a resident group block leaves other streams' classify blocks their LDS
+  static_assert(kChunk <= 4096, "sorted slots hold a 12-bit packet index");
+  const uint32_t cst = (nbins + 8) & ~7u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(tot + nbp);  // [kW][cst]
+  uint32_t* sslot = reinterpret_cast<uint32_t*>(cnt + kW * cst);  // [kChunk]
+  uint32_t* ph = sslot + kChunk;       // [n_parts][nbins] (kScanLds)
 
   // ---- the first chunk's backends are loaded up front: their latency overlaps the prologue
   const uint32_t pbeg = c * a.part_pkts;
@@ -2669,13 +2672,13 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
-  uint32_t* mycnt = cnt + wave * cst;
+  uint16_t* mycnt = cnt + wave * cst;
   for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
     // each wave zeroes its own counter row: every reader of the previous chunk's counters has
     // passed a barrier since, and one wave's LDS operations execute in order
 #pragma unroll
-    for (uint32_t k = 0; k < (kMaxBins + 4 + 255) / 256; ++k)
-      if ((lane + k * 64) * 4 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
+    for (uint32_t k = 0; k < (kMaxBins + 8 + 511) / 512; ++k)
+      if ((lane + k * 64) * 8 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
     GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
@@ -2704,7 +2707,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       // scratch slot
       const uint32_t slot = valid ? bin : nbins;
       const uint32_t prior = mycnt[slot];
-      mycnt[slot] = prior + __popc(elo) + __popc(ehi);
+      mycnt[slot] = static_cast<uint16_t>(prior + __popc(elo) + __popc(ehi));
       const uint32_t rank = prior + __popc(elo & lt_lo) + __popc(ehi & lt_hi);
       br[r] = valid ? (rank << 16) | bin : 0xffffffffu;
     }
@@ -2735,7 +2738,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t e = tid * kPer + k;
-      if (e < ne) cnt[(e % kW) * cst + e / kW] = x;
+      if (e < ne) cnt[(e % kW) * cst + e / kW] = static_cast<uint16_t>(x);
       x += ev[k];
     }
     lds_sync();
@@ -2753,8 +2756,7 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       if (br[r] != 0xffffffffu) {
         const uint32_t bin = br[r] & 0xffffu;
         const uint32_t j = mycnt[bin] + (br[r] >> 16);
-        sidx[j] = wbase + r * 64u + lane;
-        sbin[j] = static_cast<uint16_t>(bin);
+        sslot[j] = (bin << 12) | (wbase - cbase + r * 64u + lane);
       }
     }
     lds_sync();
@@ -2763,12 +2765,13 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
     // next chunk's first writes to sidx/sbin/tot come after the barriers of its scan.
     for (uint32_t j = tid; j < ctotal; j += kGBlock) {
 #ifdef NBG_GUARD  // diagnostic build: a store whose slot comes from inconsistent histograms is dropped
-      if (tot[sbin[j]] + j >= a.n_pkts) continue;
+      if (tot[sslot[j] >> 12] + j >= a.n_pkts) continue;
 #endif
 #if !(NBG_GABL & 4)
-      a.perm[tot[sbin[j]] + j] = sidx[j];
+      const uint32_t sv = sslot[j];
+      a.perm[tot[sv >> 12] + j] = cbase + (sv & 0xfffu);
 #else
-      if (sidx[j] == 0xffffffffu) a.perm[0] = tot[sbin[j]];
+      if (sslot[j] == 0xffffffffu) a.perm[0] = tot[sslot[j] >> 12];
 #endif
     }
   }
@@ -2888,9 +2891,11 @@ int launch_desc_lut(const ClassifyArgs& a, int mode, int grid, size_t lds, hipSt
               : launch_desc_mode<LUTM, false, false>(a, mode, grid, lds, s);
 }
 
-size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes) {
+// The block histogram is allocated only when the kernel keeps one (HIST): C3's 1001 bins would
+// otherwise cost every 256-thread block 4 KB of the LDS a co-resident group block needs.
+size_t classify_lds(uint32_t nb, uint32_t lut_lds_bytes, bool hist = true) {
   const uint32_t waves = (lut_lds_bytes ? kLdsBlock : kBlock) / 64;
-  return static_cast<size_t>(lut_lds_bytes) + waves * 64u * kXStride + static_cast<size_t>(nb + 1) * 4;
+  return static_cast<size_t>(lut_lds_bytes) + waves * 64u * kXStride + (hist ? static_cast<size_t>(nb + 1) * 4 : 0u);
 }
 
 }  // namespace
@@ -3002,7 +3007,7 @@ int launch_classify_stream(const ClassifyArgs& a, int grid, void* stream) {
 
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream) {
   const bool hist = a.part_hist != nullptr;
-  const size_t lds = classify_lds(a.nb, lds_lut ? a.lut_lds_bytes : 0);
+  const size_t lds = classify_lds(a.nb, lds_lut ? a.lut_lds_bytes : 0, hist);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (lds_lut)
     return wide_lut ? launch_mode<kLdsU16>(a, hist, grid, lds, s) : launch_mode<kLdsU8>(a, hist, grid, lds, s);
@@ -3102,7 +3107,7 @@ int launch_classify_desc_multi(const ClassifyArgs& a, const DescBatches& db, boo
     return set_error(NBG_EINVAL, "classify (descriptor multi): %u batches, %u tiles per wave", db.n, a.tiles_per_wave);
   if (db.blk_base[db.n] == 0) return NBG_OK;
   const bool hist = db.part_hist[0] != nullptr;
-  const size_t lds = classify_lds(a.nb, 0);
+  const size_t lds = classify_lds(a.nb, 0, hist);
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (wide_lut) {
     if (a.m == 65537u)
@@ -3190,8 +3195,8 @@ int launch_group_wide(const GroupArgs& a, void* stream) {
 }
 
 size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
-  const size_t nbp = (nbins + 3) & ~3u, cst = (nbins + 4) & ~3u;
-  size_t w = nbp * 2 + cst * (kGBlock / 64) + kChunk + kChunk / 2;
+  const size_t nbp = (nbins + 3) & ~3u, cst = (nbins + 8) & ~7u;
+  size_t w = nbp * 2 + cst * (kGBlock / 64) / 2 + kChunk;
   if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
   return w * 4;
 }
