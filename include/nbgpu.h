@@ -57,9 +57,11 @@ extern "C" {
  *   C2  1M fixed 64-B slots, 65 backends several RX queues resident: nbg_maglev_classify_device_multi;
  *                                         a stream of batches: the persistent ring (nbg_ring_*) with
  *                                         nbg_ring_group_burst; one batch: nbg_maglev_classify_device
- *   C3  IMIX descriptors, 1000 backends  nbg_maglev_classify_device with NBG_OWNED_WINDOWS
+ *   C3  IMIX descriptors, 1000 backends  several RX queues: nbg_maglev_classify_desc_multi (up to 8 batches
+ *                                         per launch); one batch: nbg_maglev_classify_device; NBG_OWNED_WINDOWS
  *   C4  C2 in 8 shards, one per GPU      per rank: the persistent ring + nbg_ring_group_burst
- *   C5  lpm -> maglev, IMIX              nbg_chain_lpm_maglev_device with NBG_OWNED_WINDOWS
+ *   C5  lpm -> maglev, IMIX              several RX queues: nbg_chain_lpm_maglev_multi; one batch:
+ *                                         nbg_chain_lpm_maglev_device; NBG_OWNED_WINDOWS
  */
 
 /* classify flags */

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS (NBG_LUT_LDS)")
     ap.add_argument("--n", default=str(1 << 20), help="comma-separated batch sizes (packets); times are also per 1M")
+    ap.add_argument("--max-plen", type=int, default=32,
+                    help="C5: drop routes longer than this (24: no tbl_long lookups; measures their cost)")
     ap.add_argument("--multi", default="", help="comma-separated batches per launch (descriptor multi path, 1M "
                                                "IMIX batches); also times the grouping launches")
     args = ap.parse_args()
@@ -40,6 +42,8 @@ def main():
         offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
         lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
     routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
+    for k in ("reference", "mixed"):
+        routes[k] = [r for r in routes[k] if int(r[1]) <= args.max_plen]
     out = {"lib": os.environ.get("NBG_LIB_OVERRIDE", "in-tree")}
     if args.multi:
         multi(args, torch, nb, KernelTimer, routes, out)
