@@ -96,6 +96,7 @@ PMC_WARMUP, PMC_STEPS = 10, 40
 # the child's launch sequence, one classify dispatch per call, in this order
 PMC_ORDER = ("in_place", "in_place_lag", "records", "read_only", "c4_shard", "c3", "c5")
 PMC_MULTI = ("read_only", "in_place")  # then these as multi-batch launches (variants.<name>_multi<K>)
+PMC_DESC_MULTI = ("c3", "c5")  # and these with IMIX_MULTI_K descriptor batches per launch (after the ring)
 PMC_RING_BATCHES = RING_BATCHES  # then the ring runs (one dispatch each, read only then in place), as timed
 NBG_SWAP_MACS, NBG_OWNED_WINDOWS, NBG_DEFER_GROUP, NBG_GROUP_LAG = 0x1, 0x4, 0x10, 0x80
 
@@ -278,9 +279,9 @@ class KernelTimer:
 # PMC traffic (launcher, N = 1): two rocprofv3 --pmc passes of a short child run
 # ---------------------------------------------------------------------------------------------
 
-def _pmc_rows(d, counter, ring=False):
+def _pmc_rows(d, counter, ring=False, desc=False):
     """Classify-kernel counter values (bytes) in dispatch order from one --pmc pass (ring: the
-    persistent ring kernel's dispatches instead)."""
+    persistent ring kernel's dispatches instead; desc: the multi-batch descriptor kernel's)."""
     path = None
     for dp, _, files in os.walk(d):
         for f in files:
@@ -291,7 +292,8 @@ def _pmc_rows(d, counter, ring=False):
     rows = []
     for row in csv.DictReader(open(path)):
         name = row.get("Kernel_Name", "")
-        want = ("classify_ring_kernel" in name) if ring else ("classify_stream_kernel" in name or "classify_kernel" in name)
+        want = (("classify_ring_kernel" in name) if ring else ("classify_desc_multi_kernel" in name) if desc
+                else ("classify_stream_kernel" in name or "classify_kernel" in name))
         if row.get("Counter_Name") == counter and want:
             rows.append((int(row.get("Dispatch_Id", len(rows))), float(row["Counter_Value"]) * 1024.0,
                          name))
@@ -322,7 +324,7 @@ def pmc_traffic(timeout_s: int = 180):
     if shutil.which("rocprofv3") is None:
         return {"error": "rocprofv3 not found"}
     env = dict(os.environ, TMPDIR="/tmp")
-    vals, names, rvals = {}, [], {}
+    vals, names, rvals, dvals = {}, [], {}, {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"nbg_pmc_{counter}_", dir="/tmp")
         cmd = ["timeout", "-k", "5", "-s", "KILL", str(timeout_s), "rocprofv3", "--pmc", counter, "--kernel-trace",
@@ -335,6 +337,7 @@ def pmc_traffic(timeout_s: int = 180):
         try:
             vals[counter], names = _pmc_rows(d, counter)
             rvals[counter], _ = _pmc_rows(d, counter, ring=True)
+            dvals[counter], _ = _pmc_rows(d, counter, desc=True)
         finally:
             shutil.rmtree(d, ignore_errors=True)
     seg = PMC_WARMUP + PMC_STEPS
@@ -367,6 +370,17 @@ def pmc_traffic(timeout_s: int = 180):
                          "hbm_bytes_per_batch": round((rd + wr) / PMC_RING_BATCHES),
                          "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
                          "kernel": f"classify_ring_kernel<true, {k}>"}
+    df, dw = dvals.get("FETCH_SIZE", []), dvals.get("WRITE_SIZE", [])
+    if len(df) == len(dw) == seg * len(PMC_DESC_MULTI):
+        for k, cfg in enumerate(PMC_DESC_MULTI):
+            rd = 2.0 * float(np.mean(df[k * seg + PMC_WARMUP:(k + 1) * seg]))
+            wr = float(np.mean(dw[k * seg + PMC_WARMUP:(k + 1) * seg]))
+            alg = IMIX_MULTI_K * BATCH * (C3_BYTES if cfg == "c3" else C5_BYTES)["classify"]
+            out[f"{cfg}_multi{IMIX_MULTI_K}"] = {
+                "read_bytes": round(rd), "write_bytes": round(wr), "hbm_bytes": round(rd + wr),
+                "algorithmic_bytes": alg, "ratio": round((rd + wr) / alg, 3),
+                "read_bytes_per_pkt": round(rd / (IMIX_MULTI_K * BATCH), 1),  # membench IMIX windows: 94.7 B
+                "kernel": "classify_desc_multi_kernel"}
     return out
 
 
@@ -1457,6 +1471,14 @@ def run_rank(args) -> None:
         if not args.no_ring:
             for v in ("read_only", "in_place"):
                 ring_pass(v, PMC_RING_BATCHES)
+        # then C3 and C5 with IMIX_MULTI_K batches per launch (classify_desc_multi_kernel dispatches)
+        if not args.no_imix:
+            imix_multi_setup(IMIX_MULTI_K, 1)
+            for cfg in PMC_DESC_MULTI:
+                for i in range(PMC_WARMUP + PMC_STEPS):
+                    imix_mcall(cfg, IMIX_MULTI_K, 0, st, defer=True)
+                    (imix["c3"][0] if cfg == "c3" else mgs[0]).finish_group(st)
+                sync_all()
         return
 
     if args.multi_only:  # profiling run: only the multi-batch passes
