@@ -377,8 +377,10 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
       slow = true;
     }
   }
-  // MAC swap in the loader lanes + window write-back (fast-path packets only)
-  if (a.swap) {
+  // MAC swap in the loader lanes + window write-back (fast-path packets only).  Never in the chain
+  // (lpm's and maglev's swaps cancel; the host clears a.swap): compiled out there, so the tile's
+  // registers are dead after the transpose
+  if (!CHAIN && a.swap) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       // the quad's chunk-0 lane holds bytes 12..15 (IHL) of this packet
