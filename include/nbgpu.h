@@ -191,8 +191,8 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
  * layout of configs C3 and C5): one tile-per-wave classify launch over all batches, then (grouping)
  * one hist, one scan and one group launch over all of them.  Each batch's outputs are exactly those
  * of nbg_maglev_classify_device (or nbg_chain_lpm_maglev_device, with d_gate) on that batch alone
- * with the same flags.  One launch pays the classify kernel's ramp and tail once: a 1M IMIX batch
- * takes 26.9 us per launch for C5 and 21.9 us per 1M at 4M packets per launch.
+ * with the same flags.  One launch pays the classify kernel's ramp and tail (~6.7 us, a quarter of
+ * a 1M IMIX batch) once for all batches (DESIGN.md sections 4 and 6).
  * Flags: NBG_SWAP_MACS (ignored by the chain: the two swaps cancel), NBG_OWNED_WINDOWS,
  * NBG_DEFER_GROUP (nbg_maglev_finish_group launches the grouping of all batches); others are
  * NBG_EINVAL.  d_off, d_len and d_backend (and d_gate for the chain) are required for a non-empty

@@ -191,3 +191,51 @@ def test_desc_multi_refusals(torch_cuda):
     torch.cuda.synchronize()
     mg.check()
     mg.close()
+
+
+def test_desc_multi_beside_running_ring(torch_cuda):
+    """Several RX queues' IMIX batches (C3 and the C5 chain, multi-batch launches on other handles)
+    while the device's persistent ring runs and takes fixed-slot batches: the tile-per-wave blocks
+    co-run in the LDS the ring leaves, every output bit-exact, and the ring's batches too."""
+    import netbricks_amd as nb
+    from netbricks_amd import Lpm, Maglev, chain_lpm_maglev_multi
+
+    torch = torch_cuda
+    ring_mg = Maglev(NAMES65, 65537)
+    c3 = Maglev(NAMES1000, 655373)
+    c5 = Maglev(NAMES65, 65537)
+    lpm = Lpm(ROUTES["mixed"])
+    lut65, lut1000 = orc.lut_build(NAMES65, 65537), orc.lut_build(NAMES1000, 655373)
+    rc, t24, tl = orc.lpm_build(ROUTES["mixed"])
+    assert rc == 0
+    n = 100000
+    rbuf = nb.make_trace(n, 0, seed=8100)[0]
+    rd = torch.from_numpy(rbuf.copy()).cuda()
+    rout = torch.empty(n, dtype=torch.uint16, device="cuda")
+    tr3 = _traces([120000, 7, 65537], seed=8200)
+    tr5 = _traces([90000, 1, 30000], seed=8300)
+    db3 = [_dev_batch(torch, *t) for t in tr3]
+    db5 = [_dev_batch(torch, *t) for t in tr5]
+    torch.cuda.synchronize()
+    s3, s5 = torch.cuda.Stream(), torch.cuda.Stream()
+    with ring_mg.ring(swap_macs=False) as ring:
+        t = ring.post(rd, n, rout)
+        r3 = c3.group_by_desc_multi(db3, stream=s3.cuda_stream)
+        r5 = chain_lpm_maglev_multi(c5, lpm, db5, stream=s5.cuda_stream)
+        ring.wait(t)
+        s3.synchronize()
+        s5.synchronize()
+    c3.check()
+    c5.check()
+    np.testing.assert_array_equal(_np16(rout, n), orc.classify(rbuf.copy(), n, lut65, swap=False))
+    _check_maglev(torch, c3, tr3, r3, db3, lut1000, 1000)
+    for (buf, off, ln, m), r in zip(tr5, r5):
+        eg, eb = orc.chain_classify(buf, m, t24, tl, lut65, offs=off, lens=ln)
+        perm, counts = orc.group(eb, 65)
+        np.testing.assert_array_equal(_np16(r.gate, m), eg)
+        np.testing.assert_array_equal(_np16(r.backend, m), eb)
+        np.testing.assert_array_equal(_np32(r.counts), counts)
+        np.testing.assert_array_equal(_np32(r.perm, m), perm)
+    for h in (ring_mg, c3, c5):
+        h.close()
+    lpm.close()
