@@ -3093,7 +3093,7 @@ int launch_scan(const ScanArgs& a, void* stream) {
   return launch_scan_multi(sm, 1, stream);
 }
 
-uint32_t classify_block_pkts() { return kBlock; }  // one 64-packet tile per wave
+uint32_t classify_block_pkts() { return kBlock; }  // per tile per wave (64 packets x 4 waves)
 
 template <int LUTM, bool F4, bool HIST>
 int launch_desc_multi_v(const ClassifyArgs& a, const DescBatches& db, size_t lds, hipStream_t s) {
@@ -3105,7 +3105,7 @@ int launch_desc_multi_v(const ClassifyArgs& a, const DescBatches& db, size_t lds
 }
 
 int launch_classify_desc_multi(const ClassifyArgs& a, const DescBatches& db, bool wide_lut, void* stream) {
-  if (db.n == 0 || db.n > kMaxMulti || a.tiles_per_wave != 1u)
+  if (db.n == 0 || db.n > kMaxMulti || (a.tiles_per_wave != 1u && a.tiles_per_wave != 2u && a.tiles_per_wave != 4u))
     return set_error(NBG_EINVAL, "classify (descriptor multi): %u batches, %u tiles per wave", db.n, a.tiles_per_wave);
   if (db.blk_base[db.n] == 0) return NBG_OK;
   const bool hist = db.part_hist[0] != nullptr;

@@ -971,7 +971,7 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
   uint32_t* set_cur = group ? h->d_part_multi + static_cast<size_t>(h->mparity) * set_words : nullptr;
   uint32_t* set_next = group ? h->d_part_multi + static_cast<size_t>(h->mparity ^ 1u) * set_words : nullptr;
   ClassifyArgs a{};
-  a.tiles_per_wave = 1;
+  a.tiles_per_wave = std::min<uint32_t>(h->tiles_per_wave, 4u);  // NBG_TPW (measurement): 1, 2 or 4
   a.lut = h->d_lut;
   a.m = static_cast<uint32_t>(h->m);
   a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
@@ -988,7 +988,7 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
     a.tbl_long = lpm->d_tbl_long;
     a.lpm_groups = lpm_groups;
   }
-  const uint32_t bp = classify_block_pkts();
+  const uint32_t bp = classify_block_pkts() * a.tiles_per_wave;
   DescBatches db{};
   GroupMulti gm{};
   HistMulti hm{};

@@ -279,7 +279,7 @@ int launch_scan_multi(const ScanMulti& sm, uint32_t n, void* stream);
 // the tile-per-wave classify kernel (256 threads, one 64-packet tile per wave) over db.n descriptor
 // batches; a carries what they share (LUT, flags, lpm tables), db what differs
 int launch_classify_desc_multi(const ClassifyArgs& a, const DescBatches& db, bool wide_lut, void* stream);
-uint32_t classify_block_pkts();  // packets per block of launch_classify_desc_multi
+uint32_t classify_block_pkts();  // packets per block and tile per wave of launch_classify_desc_multi
 int launch_zero(uint32_t* p, size_t words, void* stream);  // p[0, words) = 0 (one kernel)
 int launch_hist(const HistArgs& a, void* stream);
 int launch_hist_multi(const HistMulti& hm, uint32_t n, void* stream);  // nb + 1 <= 16384

@@ -33,6 +33,32 @@ def test_pmc_rows_filters_and_orders(tmp_path):
     assert bench._pmc_rows(str(tmp_path / "pass"), "WRITE_SIZE")[0] == [9.0 * 1024]
 
 
+def test_pmc_rows_desc_multi_kept_apart(tmp_path):
+    """The descriptor multi-batch kernel (C3 / C5, several IMIX batches per launch) is its own row set:
+    never mixed into the single-launch classify order, and read by desc=True alone."""
+    d = tmp_path / "pass" / "host" / "1"
+    d.mkdir(parents=True)
+    rows = [
+        (1, "void nbg::(anonymous namespace)::classify_kernel<3, false, false, false, 2, 0, 256>(nbg::ClassifyArgs)",
+         "FETCH_SIZE", 1.0),
+        (2, "void nbg::(anonymous namespace)::classify_desc_multi_kernel<3, false, false, false>(nbg::ClassifyArgs, "
+            "nbg::DescBatches)", "FETCH_SIZE", 8.0),
+        (3, "void nbg::(anonymous namespace)::classify_ring_kernel<true, 1>(nbg::ClassifyArgs, nbg::RingArgs)",
+         "FETCH_SIZE", 5.0),
+        (4, "void nbg::(anonymous namespace)::classify_desc_multi_kernel<2, true, true, true>(nbg::ClassifyArgs, "
+            "nbg::DescBatches)", "FETCH_SIZE", 7.0),
+    ]
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        for r in rows:
+            w.writerow(r)
+    top = str(tmp_path / "pass")
+    assert bench._pmc_rows(top, "FETCH_SIZE")[0] == [1.0 * 1024]
+    assert bench._pmc_rows(top, "FETCH_SIZE", ring=True)[0] == [5.0 * 1024]
+    assert bench._pmc_rows(top, "FETCH_SIZE", desc=True)[0] == [8.0 * 1024, 7.0 * 1024]
+
+
 def test_pmc_algorithmic_bytes():
     """Per-launch algorithmic bytes of every PMC entry: a lagged launch carries the
     whole path (82 B: classify + the previous batch's perm), the others their classify bytes."""
