@@ -1037,8 +1037,10 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
     ga.part_prefix = pre;
     ga.totals = tot;
     ga.hist16 = a.hist16;
-    ga.part_hist_next = hist_k ? nullptr : set_next;  // hist_kernel stores whole rows: nothing to zero
-    ga.next_words = hist_k ? 0u : static_cast<uint32_t>(set_words);
+    // the next call's set is zeroed whenever a call on this handle may accumulate rows into it (the
+    // classify kernel's flush: few backends), even if this call's rows come from hist_kernel
+    ga.part_hist_next = hist_in_classify(nbins) ? set_next : nullptr;
+    ga.next_words = hist_in_classify(nbins) ? static_cast<uint32_t>(set_words) : 0u;
     ga.counts = x.d_counts ? x.d_counts : h->d_counts;
     ga.perm = x.d_perm;
   }
@@ -1130,8 +1132,16 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
   const uint32_t part_pkts = static_cast<uint32_t>(std::max<uint64_t>(per, 1) * kChunk);
   const uint32_t n_parts_max = static_cast<uint32_t>((max_n + part_pkts - 1) / part_pkts);
   const int scan = group ? pick_group_scan(nbins, n_parts_max) : kScanDirect;
+  // NBG_MULTI_HIST_KERNEL=1 (measurement): partition rows from one hist_kernel launch beside the group
+  // launch instead of the classify kernel's per-unit flush (whose block barriers the ring kernel,
+  // the faster in-place path, does not have)
+  static const bool multi_hist_k = [] {
+    const char* e = std::getenv("NBG_MULTI_HIST_KERNEL");
+    return e && std::atoi(e) == 1;
+  }();
+  const bool hist_k = group && multi_hist_k;
   const bool fused = lean && !h->wide && h->m <= 65537 && total >= 262144 && nbins <= 256 && use_stream(h, total) &&
-                     (!group || (hist_in_classify(nbins) && scan != kScanKernel));
+                     (!group || ((hist_k || hist_in_classify(nbins)) && scan != kScanKernel));
   if (!fused && (flags & NBG_DEFER_GROUP))
     return set_error(NBG_EINVAL, "classify (multi): NBG_DEFER_GROUP needs the fused path (fixed 64-B slots, >= 262144 "
                      "packets in all, <= 255 backends)");
@@ -1175,16 +1185,18 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
   a.lut_lds_bytes = std::min<uint32_t>(h->lut_alloc, 65536u);
   a.lut_tail = h->m > 65536 ? h->lut_host[65536] : 0u;
   a.part_pkts = part_pkts;
-  a.hist16 = group && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
+  a.hist16 = group && !hist_k && scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;
   StreamBatches sb{};
   GroupMulti gm{};
+  HistMulti hm{};
   uint32_t units = 0;
   for (uint32_t j = 0; j < n_batches; ++j) {
     const nbg_batch& x = batches[j];
     sb.pkts[j] = x.d_pkts;
     sb.backend[j] = x.d_backend;
     sb.mac_out[j] = x.d_mac_out;
-    sb.part_hist[j] = group ? set_cur + static_cast<size_t>(j) * kMaxParts * nbins : nullptr;
+    uint32_t* rows = group ? set_cur + static_cast<size_t>(j) * kMaxParts * nbins : nullptr;
+    sb.part_hist[j] = hist_k ? nullptr : rows;
     sb.n_pkts[j] = static_cast<uint32_t>(x.n_pkts);
     sb.unit_base[j] = units;
     units += static_cast<uint32_t>((((x.n_pkts + 63) >> 6) + stream_waves_per_block() - 1) / stream_waves_per_block());
@@ -1197,13 +1209,23 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
     ga.bits = bits;
     ga.n_parts = static_cast<uint32_t>((x.n_pkts + part_pkts - 1) / part_pkts);
     ga.part_pkts = part_pkts;
-    ga.part_hist = sb.part_hist[j];
+    ga.part_hist = rows;
     ga.hist16 = a.hist16;
-    ga.part_hist_next = set_next;
-    ga.next_words = static_cast<uint32_t>(set_words);
+    // zeroed for the next call even when this call's rows come from hist_kernel (stored whole): the
+    // next call may accumulate into them (the classify kernel's flush)
+    ga.part_hist_next = hist_in_classify(nbins) ? set_next : nullptr;
+    ga.next_words = hist_in_classify(nbins) ? static_cast<uint32_t>(set_words) : 0u;
     ga.counts = x.d_counts ? x.d_counts : h->d_counts;
     ga.perm = x.d_perm;
+    HistArgs& ha = hm.h[j];
+    ha.backend = x.d_backend;
+    ha.n_pkts = ga.n_pkts;
+    ha.nb = h->nb;
+    ha.part_pkts = part_pkts;
+    ha.n_parts = ga.n_parts;
+    ha.part_hist = rows;
   }
+  hm.per = n_parts_max;
   sb.unit_base[n_batches] = units;
   sb.n = n_batches;
   a.mac_out = sb.mac_out[0];  // selects the records mode; per-batch pointers come from sb
@@ -1221,10 +1243,12 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
       h->pending = true;
       h->pending_multi = n_batches;
       h->pending_gm = gm;
-      h->pending_hist_multi = false;
+      h->pending_hist_multi = hist_k;
+      h->pending_hm = hm;
       h->pending_scan_mode = scan;
       return NBG_OK;
     }
+    if (hist_k && (rc = launch_hist_multi(hm, n_batches, stream))) return rc;
     if ((rc = launch_group_multi(gm, n_batches, scan, stream))) return rc;
   }
   return NBG_OK;
