@@ -57,7 +57,7 @@ extern "C" {
  *   C2  1M fixed 64-B slots, 65 backends several RX queues resident: nbg_maglev_classify_device_multi;
  *                                         a stream of batches: the persistent ring (nbg_ring_*) with
  *                                         nbg_ring_group_burst; one batch: nbg_maglev_classify_device
- *   C3  IMIX descriptors, 1000 backends  several RX queues: nbg_maglev_classify_desc_multi (up to 8 batches
+ *   C3  IMIX descriptors, 1000 backends  several RX queues: nbg_maglev_classify_desc_multi (up to 16 batches
  *                                         per launch); one batch: nbg_maglev_classify_device; NBG_OWNED_WINDOWS
  *   C4  C2 in 8 shards, one per GPU      per rank: the persistent ring + nbg_ring_group_burst
  *   C5  lpm -> maglev, IMIX              several RX queues: nbg_chain_lpm_maglev_multi; one batch:
@@ -174,7 +174,7 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
  * then launches the one group kernel of all batches); others are NBG_EINVAL.
  * Either every batch has d_perm (or d_counts) or none has.
  */
-#define NBG_MAX_MULTI 8u
+#define NBG_MAX_MULTI 16u
 typedef struct nbg_batch {
   uint8_t* d_pkts;
   uint64_t n_pkts;

@@ -32,7 +32,7 @@ NBG_LUT_TILED = 0x20
 NBG_STREAM_DESC = 0x40
 NBG_GROUP_LAG = 0x80
 NBG_HOST_SLOTS = 3
-NBG_MAX_MULTI = 8
+NBG_MAX_MULTI = 16
 NBG_RING_SLOTS = 64
 NBG_RING_MAX_QUEUES = 16
 NBG_EBUSY = -16

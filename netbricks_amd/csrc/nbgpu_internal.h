@@ -82,7 +82,7 @@ struct ClassifyArgs {
 
 // Several batches in one streaming-classify launch (nbg_maglev_classify_device_multi): what differs
 // per batch.  A single-batch launch passes n = 1.  Units (512 packets) never straddle batches.
-constexpr uint32_t kMaxMulti = 8;
+constexpr uint32_t kMaxMulti = 16;
 struct StreamBatches {
   uint8_t* pkts[kMaxMulti];
   uint16_t* backend[kMaxMulti];

@@ -130,7 +130,8 @@ def test_desc_multi_defer_group_other_stream(torch_cuda):
     mg.close()
 
 
-@pytest.mark.parametrize("sizes", [[1 << 20, 1000, 262144], [1, 2, 3, 4, 5, 6, 7, 70000]])
+@pytest.mark.parametrize("sizes", [[1 << 20, 1000, 262144], [1, 2, 3, 4, 5, 6, 7, 70000],
+                                   [65536 + 7 * i for i in range(16)]])
 def test_chain_multi_vs_oracle(torch_cuda, sizes):
     """Config C5's chain over several IMIX batches in one launch: gate, backend, perm, counts of every
     batch as the oracle gives them for that batch alone; packet bytes unchanged."""
@@ -170,9 +171,10 @@ def test_chain_multi_vs_oracle(torch_cuda, sizes):
 
 
 def test_desc_multi_refusals(torch_cuda):
-    """0 or 9 batches, a batch without offsets, unknown flags: NBG_EINVAL, nothing launched."""
+    """0 or NBG_MAX_MULTI + 1 batches, a batch without offsets, unknown flags: NBG_EINVAL, nothing
+    launched."""
     from netbricks_amd import Maglev
-    from netbricks_amd._lib import NBG_EINVAL, NBG_LUT_LDS, NbgDescBatch, lib
+    from netbricks_amd._lib import NBG_EINVAL, NBG_LUT_LDS, NBG_MAX_MULTI, NbgDescBatch, lib
 
     torch = torch_cuda
     mg = Maglev(NAMES65, 65537)
@@ -180,9 +182,10 @@ def test_desc_multi_refusals(torch_cuda):
     d, o, lt, _ = _dev_batch(torch, buf, off, ln, n)
     be = torch.empty(n, dtype=torch.uint16, device="cuda")
     good = NbgDescBatch(d.data_ptr(), o.data_ptr(), lt.data_ptr(), n, be.data_ptr(), None, None, None)
-    arr = (NbgDescBatch * 9)(*([good] * 9))
+    over = NBG_MAX_MULTI + 1
+    arr = (NbgDescBatch * over)(*([good] * over))
     assert lib.nbg_maglev_classify_desc_multi(mg._h, arr, 0, 0, None) == NBG_EINVAL
-    assert lib.nbg_maglev_classify_desc_multi(mg._h, arr, 9, 0, None) == NBG_EINVAL
+    assert lib.nbg_maglev_classify_desc_multi(mg._h, arr, over, 0, None) == NBG_EINVAL
     assert lib.nbg_maglev_classify_desc_multi(mg._h, arr, 1, NBG_LUT_LDS, None) == NBG_EINVAL
     bad = (NbgDescBatch * 1)(NbgDescBatch(d.data_ptr(), None, lt.data_ptr(), n, be.data_ptr(), None, None, None))
     assert lib.nbg_maglev_classify_desc_multi(mg._h, bad, 1, 0, None) == NBG_EINVAL

@@ -90,10 +90,11 @@ def test_multi_fallback_small_batches(torch_cuda, mg65, lut65):
 
 
 def test_multi_alternating_batch_counts(torch_cuda, mg65, lut65):
-    """Ping-pong partition histograms across calls with 4, 2, 8, 1 and 3 batches, single calls between."""
+    """Ping-pong partition histograms across calls with 4, 2, 8, 1, 3 and 16 batches, single calls between."""
     from netbricks_amd import make_trace
 
-    for i, sizes in enumerate([[1 << 20] * 4, [400_000, 300_000], [131_072] * 8, [1 << 20], [262_144, 1, 262_144]]):
+    for i, sizes in enumerate([[1 << 20] * 4, [400_000, 300_000], [131_072] * 8, [1 << 20], [262_144, 1, 262_144],
+                               [65_536 + 64 * k for k in range(16)]]):
         _check(torch_cuda, mg65, lut65, sizes, seed=200 + 10 * i)
         buf, _, _ = make_trace(300_000, 0, seed=300 + i)
         d = torch_cuda.from_numpy(buf.copy()).to(torch_cuda.device("cuda:0"))
@@ -110,8 +111,10 @@ def test_multi_rejects_bad_counts(torch_cuda, mg65):
     with pytest.raises(ValueError):
         mg65.group_by_multi([])
     d = torch_cuda.zeros(64 * 10, dtype=torch_cuda.uint8, device="cuda:0")
+    from netbricks_amd._lib import NBG_MAX_MULTI
+
     with pytest.raises(ValueError):
-        mg65.group_by_multi([(d, 10)] * 9)
+        mg65.group_by_multi([(d, 10)] * (NBG_MAX_MULTI + 1))
 
 
 def test_multi_deferred_group_on_second_stream(torch_cuda, mg65, lut65):
