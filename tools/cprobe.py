@@ -20,7 +20,7 @@ def pct(x, qs=(0, 10, 50, 90, 100)):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variant", default="noswap", choices=["noswap", "inplace", "macout", "hist"])
+    ap.add_argument("--variant", default="noswap", choices=["noswap", "inplace", "macout", "hist", "c5"])
     ap.add_argument("--lut-lds", action="store_true")
     ap.add_argument("--n", type=int, default=1 << 20)
     args = ap.parse_args()
@@ -35,7 +35,16 @@ def main():
     dev = torch.device("cuda:0")
     mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
     n = args.n
-    bufs = [torch.from_numpy(nb.make_trace(n, 0, seed=b + 5)[0]).to(dev) for b in range(8)]
+    mode = 1 if args.variant == "c5" else 0  # C5: IMIX descriptors through the lpm -> maglev chain
+    traces = [nb.make_trace(n, mode, seed=b + 5) for b in range(8)]
+    bufs = [torch.from_numpy(t[0]).to(dev) for t in traces]
+    offs = [torch.from_numpy(t[1].view(np.int32)).to(dev).view(torch.uint32) for t in traces] if mode else None
+    lens = [torch.from_numpy(t[2].view(np.int16)).to(dev).view(torch.uint16) for t in traces] if mode else None
+    if mode:
+        import json
+        routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
+        lpm = nb.Lpm(routes["reference"] + routes["mixed"])
+        gate = torch.empty(n, dtype=torch.uint16, device=dev)
     be = torch.empty(n, dtype=torch.uint16, device=dev)
     perm = torch.empty(n, dtype=torch.uint32, device=dev)
     cnt = torch.empty(66, dtype=torch.uint32, device=dev)
@@ -47,6 +56,10 @@ def main():
             mg.group_by(bufs[i % 8], n, group=False, swap_macs=False, **kw)
         elif args.variant == "inplace":
             mg.group_by(bufs[i % 8], n, group=False, **kw)
+        elif args.variant == "c5":
+            nb.chain_lpm_maglev(mg, lpm, bufs[i % 8], n, offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True,
+                                defer_group=True, gate=gate, perm=perm, counts=cnt, **kw)
+            mg.finish_group()
         elif args.variant == "macout":
             mg.group_by(bufs[i % 8], n, group=False, mac_out=mac, **kw)
         else:
