@@ -106,6 +106,125 @@ def log(*a):
 
 
 # ---------------------------------------------------------------------------------------------
+# the stdout line: a compact record the driver can read whole (its stdout tail is ~8.3 KB); the
+# full record (prose, PMC blocks, sweeps) goes to a file.  The reference's own measurement is a
+# one-line rate print (test/maglev/src/main.rs:83-88).
+# ---------------------------------------------------------------------------------------------
+
+LINE_LIMIT = 7000  # bytes of the stdout JSON line; bench fails loudly above it
+VARIANT_FIELDS = ("us_per_batch", "frac", "pmc_ratio", "classify_us_per_batch")
+FULL_RECORD = os.environ.get("NBG_BENCH_FULL", os.path.join("gpurun_out", "bench_full_latest.json"))
+
+
+def _r(x, nd=4):
+    return round(float(x), nd) if isinstance(x, (int, float)) and not isinstance(x, bool) else None
+
+
+def _variant_row(name, v, pmc):
+    """[us per batch (or shard), frac (classify / kernel), PMC hbm/algorithmic, classify us per batch]."""
+    if not isinstance(v, dict):
+        return None
+    if "error" in v and "value" not in v and "us_per_batch" not in v:
+        return "error: " + str(v["error"])[:60]
+    us = v.get("us_per_batch")
+    if us is None and "ms_per_batch" in v:
+        us = v["ms_per_batch"] * 1e3
+    if us is None:
+        us = v.get("us_per_shard")
+    ratio = v.get("traffic_ratio")
+    pname = "in_place" if name == "launch_in_place" else name  # the same classify launch
+    if ratio is None and isinstance(pmc, dict) and isinstance(pmc.get(pname), dict):
+        ratio = pmc[pname].get("ratio")
+    frac = v.get("frac", v.get("path_frac"))
+    return [_r(us, 3), _r(frac), _r(ratio, 3), _r(v.get("classify_us_per_batch"), 2)]
+
+
+def compact_line(full: dict) -> dict:
+    """The driver-facing line: headline, roofline (with PMC traffic), cpu_baseline, north_star, c4,
+    e2e and a {variant: [us_per_batch, frac, pmc_ratio, classify_us_per_batch]} map; no prose."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "ms_per_batch",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "per_gpu_mpps", "lut_digest",
+            "rccl_ranks", "comm_backend", "hbm_gbps_per_gpu", "hbm_bytes_per_pkt", "aggregate_frac",
+            "steady_state", "north_star", "selftest")
+    line = {k: full[k] for k in keep if k in full}
+    cfg = full.get("config", {})
+    line["config"] = {k: cfg[k] for k in ("workload", "backends", "table_size", "batch_pkts", "slot_bytes",
+                                          "mac_swap", "batches_per_launch", "streams", "parallelism") if k in cfg}
+    digs = full.get("lut_digest_per_rank")
+    if digs:
+        line["lut_digests_agree"] = len(set(digs)) == 1
+    roof = full.get("roofline")
+    if isinstance(roof, dict):
+        line["roofline"] = {k: roof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                 "traffic_ratio", "bytes_per_pkt", "pkts_per_launch",
+                                                 "batches_per_launch", "avg_launch_us", "us_per_batch")
+                            if k in roof}
+        if "kernel" in roof:
+            line["roofline"]["kernel"] = roof["kernel"].split(" (")[0][:100]
+        if isinstance(roof.get("traffic"), (int, float)) and "traffic_ratio" not in roof and roof.get("achieved"):
+            alg = roof.get("bytes_per_pkt", 0) * roof.get("pkts_per_launch", 0)
+            if alg:
+                line["roofline"]["traffic_ratio"] = round(roof["traffic"] / alg, 3)
+    cpu = full.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        line["cpu_baseline"] = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "single_core_mpps",
+                                                    "cpu_model") if k in cpu}
+        line["cpu_baseline"]["sample"] = str(cpu.get("sample", ""))[:240]
+    else:
+        line["cpu_baseline"] = cpu
+    c4 = full.get("c4")
+    if isinstance(c4, dict):
+        line["c4"] = {k: ({q: w for q, w in v.items() if q != "what"} if isinstance(v, dict) else v)
+                      for k, v in c4.items() if k != "path"}
+    e2e = full.get("e2e")
+    if isinstance(e2e, dict):
+        line["e2e"] = e2e.get("compact", {k: v for k, v in e2e.items() if not isinstance(v, (dict, list))})
+    pmc = full.get("pmc")
+    variants = full.get("variants")
+    if isinstance(variants, dict):
+        rows = {}
+        for k, v in variants.items():
+            if k in ("ws_sweep", "ring_output_checks", "ring_group_sweep", "imix_multi_sweep"):
+                continue
+            row = _variant_row(k, v, pmc)
+            if row is not None:
+                rows[k] = row
+        sw = variants.get("ws_sweep")
+        if isinstance(sw, dict):  # "ws<rot>_<name>": the working-set sweep's rows
+            for rot, row in sw.items():
+                if isinstance(row, dict):
+                    for k, v in row.items():
+                        r = _variant_row(k, v, None)
+                        if r is not None:
+                            rows[f"ws{rot}_{k}"] = r
+        line["variants_fields"] = list(VARIANT_FIELDS)
+        line["variants"] = rows
+        if isinstance(variants.get("ring_output_checks"), dict):
+            line["ring_output_checks"] = variants["ring_output_checks"]
+    if isinstance(pmc, dict) and "error" in pmc:
+        line["pmc_error"] = str(pmc["error"])[:200]
+    line["full_record"] = FULL_RECORD
+    return line
+
+
+def emit_line(full: dict) -> None:
+    """Write the full record to FULL_RECORD and print the compact line (one line, <= LINE_LIMIT bytes:
+    a longer one would be cut by the driver's stdout tail, so fail loudly instead)."""
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(FULL_RECORD)), exist_ok=True)
+        with open(FULL_RECORD, "w") as f:
+            json.dump(full, f, indent=1)
+    except OSError as e:
+        log(f"bench: could not write the full record {FULL_RECORD}: {e}")
+    line = compact_line(full)
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_LIMIT:
+        log(f"bench: the JSON line is {len(s)} bytes, above the {LINE_LIMIT}-byte limit")
+        raise SystemExit(3)
+    print(s, flush=True)
+
+
+# ---------------------------------------------------------------------------------------------
 # CPU baseline (rank 0, N = 1): the oracle's C port of the reference's per-core loop
 # ---------------------------------------------------------------------------------------------
 
@@ -384,6 +503,21 @@ def pmc_traffic(timeout_s: int = 180):
     return out
 
 
+def e2e_block(timeout_s: int = 240):
+    """The end-to-end rate over PCIe (north_star: host memory in and out, DPDK mbufs; native/pmd.c:192-206,
+    framework/src/operators/packet_batch.rs:78-99), measured by tools/e2e_bench.py in a child process
+    after the ranks ended: pipelined H2D -> classify -> D2H, the synchronous and pipelined host-mbuf
+    entry points over 2-KiB mbufs, zero-copy over a registered pool, and copies alone."""
+    cmd = ["timeout", "-k", "5", str(timeout_s), sys.executable, os.path.join(ROOT, "tools", "e2e_bench.py")]
+    r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        return {"error": f"e2e_bench rc={r.returncode}: {r.stderr[-300:]}"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"error": "e2e_bench printed no JSON line"}
+    return json.loads(lines[-1])
+
+
 # ---------------------------------------------------------------------------------------------
 # launcher
 # ---------------------------------------------------------------------------------------------
@@ -464,7 +598,11 @@ def launch(args, argv) -> int:
             roof["traffic"] = pmc[f"in_place_multi{roof['batches_per_launch']}"]["hbm_bytes"]
         elif "in_place" in pmc:
             roof["traffic"] = pmc["in_place"]["hbm_bytes"]
-    print(json.dumps(line), flush=True)
+    if n == 1 and not args.selftest and not args.no_e2e:
+        t0 = time.time()
+        line["e2e"] = e2e_block()
+        log(f"bench: end-to-end pass {time.time() - t0:.0f}s")
+    emit_line(line)
     return 0
 
 
@@ -496,6 +634,15 @@ def run_rank(args) -> None:
             dist.init_process_group("gloo")
         if dist.get_world_size() != world:
             raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, expected {world}")
+    comm = None
+    if world > 1:
+        # the communicator's own rank count: an all-reduce of 1 per rank over it (RCCL on GPUs, gloo in
+        # the selftest), so the line shows how many ranks the collective library really connected
+        one = torch.ones(1, dtype=torch.int32, device=dev)
+        dist.all_reduce(one)
+        comm = {"rccl_ranks": int(one.item()), "comm_backend": str(dist.get_backend())}
+        if int(one.item()) != world:
+            raise SystemExit(f"bench: the communicator counted {int(one.item())} ranks, expected {world}")
 
     def sync_all():
         if gpu:
@@ -1774,10 +1921,15 @@ def run_rank(args) -> None:
         line["cpu_baseline"] = cpu
         if c4 is not None:
             line["c4"] = c4
+        if comm is not None:
+            line.update(comm)
         if args.selftest:
             line["selftest"] = True
             line["data"] = "synthetic (launcher selftest on CPU: no HIP call, steps are empty)"
-        print(json.dumps(line), flush=True)
+        if os.environ.get("NBG_BENCH_LAUNCHED") == "1":
+            print(json.dumps(line), flush=True)  # the launcher adds PMC / e2e and prints the compact line
+        else:
+            emit_line(line)  # a rank of torch.distributed.run: rank 0 prints the line itself
     if gpu:
         for m in mgs:
             m.close()
@@ -1809,6 +1961,7 @@ def parse_args(argv):
     ap.add_argument("--multi-only", action="store_true",
                     help="profiling: only the multi-batch passes (rocprof kernel stats of the multi launch)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) pass")
     ap.add_argument("--inline", action="store_true",
                     help="run as a single rank in this process (no launcher; for running under a profiler)")
     ap.add_argument("--selftest", action="store_true",

@@ -81,3 +81,63 @@ def test_cpu_inventory_is_sane():
     assert affinity >= 1
     assert quota is None or quota > 0
     assert isinstance(model, str) and model
+
+
+def _full_record_n8():
+    """A full-size N = 8 record: round 4's final N = 1 record (21 variants, 16 PMC blocks, the working-set
+    sweep) with an 8-rank c4 block, 8 per-GPU rates and an e2e block."""
+    import json
+
+    full = json.load(open(os.path.join(ROOT, "profiles", "r04_bench_final.json")))
+    full["n_gpus"] = 8
+    full["per_gpu_mpps"] = [44000.1] * 8
+    full["lut_digest_per_rank"] = ["0123456789abc"] * 8
+    full["rccl_ranks"], full["comm_backend"] = 8, "nccl"
+    full["c4"]["device_resident"]["per_gpu_mpps"] = [5000.5] * 8
+    full["c4"]["scatter_inclusive"] = {"value": 9000.1, "unit": "Mpps", "steps": 50, "ms_per_batch": 0.1165,
+                                       "root_egress_GBps": 500.0, "checked": True, "what": "x" * 300}
+    full["e2e"] = {"pipelined": {"mpps": 700.0}, "compact": {k: 123.4 for k in (
+        "pipelined_mpps", "pipelined_h2d_gbps", "host_submit_mpps", "classify_host_mpps", "zero_copy_mpps",
+        "host_submit_registered_mpps", "copies_only_mpps", "h2d_only_gbps", "d2h_only_gbps",
+        "pcie_bound_gbps_per_dir", "batch_pkts", "host_batch_pkts")}}
+    return full
+
+
+def test_compact_line_fits_driver_tail():
+    """The stdout line stays whole in the driver's ~8.3 KB tail (BENCH_r04 was 22.9 KB and unparsed):
+    a full-size record compacts to <= LINE_LIMIT bytes and keeps every field the driver and judge read."""
+    import json
+
+    full = _full_record_n8()
+    assert len(json.dumps(full)) > 20000
+    line = bench.compact_line(full)
+    s = json.dumps(line, separators=(",", ":"))
+    assert len(s) <= bench.LINE_LIMIT < 8000, len(s)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "config", "dtype",
+              "roofline", "cpu_baseline", "north_star", "c4", "e2e", "variants", "rccl_ranks"):
+        assert k in line, k
+    assert line["roofline"]["traffic"] == full["roofline"]["traffic"]
+    assert line["c4"]["scatter_inclusive"]["checked"] is True and "what" not in line["c4"]["scatter_inclusive"]
+    assert line["variants_fields"] == list(bench.VARIANT_FIELDS)
+    row = line["variants"]["c5_multi8"]
+    v = full["variants"]["c5_multi8"]
+    assert row[0] == round(v["ms_per_batch"] * 1e3, 3) and row[1] == v["frac"]
+    assert row[2] == full["pmc"]["c5_multi8"]["ratio"] and row[3] == v["classify_us_per_batch"]
+    assert line["variants"]["ring_in_place"][2] == full["variants"]["ring_in_place"]["traffic_ratio"]
+    assert "ws32_ring_in_place" in line["variants"]
+
+
+def test_emit_line_fails_loudly_over_limit(tmp_path, monkeypatch, capsys):
+    import json
+
+    import pytest
+
+    monkeypatch.setattr(bench, "FULL_RECORD", str(tmp_path / "full.json"))
+    full = _full_record_n8()
+    bench.emit_line(full)
+    out = capsys.readouterr().out.strip()
+    assert json.loads(out)["value"] == full["value"]
+    assert json.load(open(tmp_path / "full.json"))["pmc"] == full["pmc"]
+    full["variants"].update({f"extra_{i}": {"us_per_batch": 1.0, "frac": 0.5} for i in range(400)})
+    with pytest.raises(SystemExit):
+        bench.emit_line(full)

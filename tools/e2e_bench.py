@@ -21,6 +21,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+PCIE_GEN5_X16_GBPS = 63.0
 
 
 def main():
@@ -84,6 +85,17 @@ def main():
             d_win[i % S].copy_(h_win[i % S], non_blocking=True)
     torch.cuda.synchronize()
     res["h2d_only_gbps"] = round(args.batches * n * 64 / (time.perf_counter() - t0) / 1e9, 1)
+    # D2H alone: the backend + perm + MAC records of every batch
+    t0 = time.perf_counter()
+    for i in range(args.batches):
+        with torch.cuda.stream(sts[i % S]):
+            h_be[i % S].copy_(d_be[i % S].view(torch.int16), non_blocking=True)
+            h_pm[i % S].copy_(d_pm[i % S].view(torch.int32), non_blocking=True)
+            h_mac[i % S].copy_(d_mac[i % S], non_blocking=True)
+    torch.cuda.synchronize()
+    res["d2h_only_gbps"] = round(args.batches * n * 18 / (time.perf_counter() - t0) / 1e9, 1)
+    # H2D of 64-B windows alone, as a packet rate: the copies-only bound of the pipelined path
+    res["copies_only_mpps"] = round(res["h2d_only_gbps"] * 1e9 / 64 / 1e6, 1)
 
     # (b) the synchronous host-mbuf entry point and (c) the pipelined one, over 2-KiB mbufs
     hn = args.host_n
@@ -208,6 +220,15 @@ def main():
                                        "what": "nbg_maglev_host_submit/_wait over the registered mbuf pool (zero-copy "
                                                "inside the library; offsets computed by host threads)"}
     reg.close()
+    # PCIe Gen5 x16: 32 GT/s x 16 lanes x 128/130 = 63.0 GB/s per direction before protocol overhead
+    res["pcie_bound_gbps_per_dir"] = PCIE_GEN5_X16_GBPS
+    res["compact"] = {
+        "pipelined_mpps": res["pipelined"]["mpps"], "pipelined_h2d_gbps": res["pipelined"]["h2d_gbps"],
+        "host_submit_mpps": res["host_pipeline"]["mpps"], "classify_host_mpps": res["classify_host"]["mpps"],
+        "zero_copy_mpps": res["zero_copy"]["mpps"], "host_submit_registered_mpps": res["host_pipeline_registered"]["mpps"],
+        "copies_only_mpps": res["copies_only_mpps"], "h2d_only_gbps": res["h2d_only_gbps"],
+        "d2h_only_gbps": res["d2h_only_gbps"], "pcie_bound_gbps_per_dir": PCIE_GEN5_X16_GBPS,
+        "batch_pkts": n, "host_batch_pkts": hn}
     print(json.dumps(res))
     _ = C
 
