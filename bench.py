@@ -1449,10 +1449,10 @@ def run_rank(args) -> None:
         st = sts[j] if stream is None else stream
         if cfg == "c3":
             x["c3"][j].group_by(x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k], owned_windows=True,
-                                defer_group=defer, stream=st, **x["c3out"][j])
+                                bounds_check=False, defer_group=defer, stream=st, **x["c3out"][j])
         else:
             nb.chain_lpm_maglev(mgs[j], x["lpm"], x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k],
-                                owned_windows=True, defer_group=defer, gate=x["gates"][j], stream=st, lut_lds=lut_lds,
+                                owned_windows=True, bounds_check=False, defer_group=defer, gate=x["gates"][j], stream=st, lut_lds=lut_lds,
                                 backend=outs[j][0]["backend"], perm=outs[j][0]["perm"], counts=outs[j][0]["counts"])
 
     def imix_variant(cfg, steps, warmup, lut_lds=False):

@@ -171,7 +171,9 @@ int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t
  * most 255 backends, M <= 65537 and at least 262144 packets in all; otherwise the batches are run
  * one after another through nbg_maglev_classify_device_ex on `stream`.  1 <= n_batches <=
  * NBG_MAX_MULTI.  Flags: NBG_SWAP_MACS, and NBG_DEFER_GROUP on the fused path (nbg_maglev_finish_group
- * then launches the one group kernel of all batches); others are NBG_EINVAL.
+ * then launches the one group kernel of all batches); others are NBG_EINVAL.  While a persistent ring
+ * runs on the device the fused path (a streaming kernel) is not taken, so NBG_DEFER_GROUP is then
+ * NBG_EINVAL too; a ring stops holding the device once its kernel has ended (stop or idle exit).
  * Either every batch has d_perm (or d_counts) or none has.
  */
 #define NBG_MAX_MULTI 16u
@@ -236,15 +238,21 @@ int nbg_maglev_classify_desc_multi(nbg_maglev* h, const nbg_desc_batch* batches,
  * on `stream` so far.  It holds the LDS of every CU it occupies until it ends: after
  * nbg_ring_stop, or by itself after idle_ms without a post (its exit condition when the producer
  * goes away; 0 = 2000 ms; the next ring call then returns NBG_ETIMEDOUT).  nbg_ring_stop completes
- * every posted batch, waits for the kernel to end, and frees the ring (NBG_EBUSY if the kernel did
- * not end within idle_ms + 5 s: then nothing it may touch is freed, and the device stays busy).
+ * every posted batch, waits for the kernel to end and for calls still blocked on the ring (other
+ * producer threads' posts and waits, which then return) to leave, and keeps the ring's buffers for
+ * the handle's next start: the ring pointer stays valid until nbg_maglev_destroy, and calls on a
+ * stopped ring report its end.  NBG_EBUSY if the kernel did not end within idle_ms + 5 s: then
+ * nothing it may touch is freed, the device stays busy, and every later call on the ring returns
+ * NBG_EBUSY.
  * ONE ring per GPU: a second nbg_ring_start on a device whose ring runs (from any handle) returns
  * NBG_EBUSY at once.  Several RX queues share the device's ring through nbg_ring_queue_* below.
  * While a handle's ring runs, that handle's classify calls (device, multi, host, chain) return
  * NBG_EBUSY: their kernels would queue behind the resident one.  Other handles' batches on the same
- * device co-run in the LDS the ring leaves free (about 30 KB per CU in place): while a ring runs they
- * take the tile-per-wave classify kernel (never the streaming ones or NBG_LUT_LDS, which need a whole
- * CU's LDS), with identical results.
+ * device co-run in the LDS the ring leaves free (about 30 KB per CU in place): while a
+ * ring runs they take the tile-per-wave classify kernel (never the streaming ones or NBG_LUT_LDS,
+ * which need a whole CU's LDS), with identical results.  A grouping launch whose block needs more
+ * LDS than that (many backends: the 1001-bin group block of C3 takes about 40 KB) waits until the
+ * ring's kernel ends.
  * Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
  * flags: 0 (read only) or NBG_SWAP_MACS (in place).
  * The nbg_ring_* calls of one ring are thread-safe (one mutex per ring).
@@ -290,7 +298,10 @@ int nbg_ring_stop(nbg_ring* r);
  * its own completion count and its own grouping; the batches of all queues share the ring's
  * NBG_RING_SLOTS slots in the order they were posted.  Up to NBG_RING_MAX_QUEUES per ring; a queue
  * is used by one thread at a time (different queues from different threads).  nbg_ring_stop closes
- * every queue of the ring (their handles become invalid); nbg_ring_queue_close closes one earlier.
+ * every queue of the ring: later calls on a closed queue return NBG_EINVAL (a wait already blocked
+ * when the ring stopped returns its batch's completion), and nbg_ring_queue_close frees it; queues
+ * never closed are freed by nbg_maglev_destroy.  nbg_ring_queue_close before the stop closes and
+ * frees one at once.
  */
 #define NBG_RING_MAX_QUEUES 16u
 typedef struct nbg_ring_queue nbg_ring_queue;

@@ -96,6 +96,7 @@ struct nbg_maglev {
   uint32_t lag_dirty = 0;             // bit k: set k may hold counts (zeroed before it is accumulated into)
   nbg_ring* ring = nullptr;           // the running persistent ring (nbg_ring_start), if any
   nbg_ring* ring_spare = nullptr;     // a stopped ring's buffers and stream, kept for the next start
+  std::vector<nbg_ring*> ring_dead;   // rings whose stream failed: kept (callers may hold them) until destroy
   bool ring_leaked = false;           // a ring's kernel did not end at stop: never free what it may touch
   float ring_kernel_ms = -1.f;        // the last ring kernel's duration (HIP events), after its stop
   hipStream_t last_stream = nullptr;  // the stream of the handle's last launch
@@ -533,6 +534,11 @@ void nbg_maglev_destroy(nbg_maglev* h) {
     ring_free(h->ring_spare);
     h->ring_spare = nullptr;
   }
+  for (nbg_ring* r : h->ring_dead) {
+    DeviceGuard g(h->device);
+    ring_free(r);
+  }
+  h->ring_dead.clear();
   {
     DeviceGuard g(h->device);
     free_scratch(h);
@@ -912,8 +918,9 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
   if (!h) return set_error(NBG_EINVAL, "%s: null handle", what);
   if (!batches || n_batches == 0 || n_batches > NBG_MAX_MULTI)
     return set_error(NBG_EINVAL, "%s: 1..%u batches", what, NBG_MAX_MULTI);
-  if (flags & ~(NBG_SWAP_MACS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP))
-    return set_error(NBG_EINVAL, "%s: flags other than NBG_SWAP_MACS, NBG_OWNED_WINDOWS and NBG_DEFER_GROUP", what);
+  if (flags & ~(NBG_SWAP_MACS | NBG_OWNED_WINDOWS | NBG_DEFER_GROUP | NBG_WB_PARTIAL))
+    return set_error(NBG_EINVAL, "%s: flags other than NBG_SWAP_MACS, NBG_OWNED_WINDOWS, NBG_WB_PARTIAL and NBG_DEFER_GROUP",
+                     what);
   if (h->ring) return set_error(NBG_EBUSY, "%s: the handle's persistent ring is running", what);
   if (lpm && lpm->device != h->device) return set_error(NBG_EINVAL, "%s: lpm and maglev handles on different devices", what);
   if (h->pending_lag) {  // a pending lagged group is launched alone first
@@ -978,7 +985,7 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
   a.nb = h->nb;
   a.swap = (flags & NBG_SWAP_MACS) && !lpm ? 1u : 0u;  // chain: lpm's and maglev's swaps cancel
   a.win_owned = (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
-  a.wb_full = 1u;
+  a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
   a.part_pkts = part_pkts;
   // partition rows from the classify kernel's flush (few backends, rows accumulated: zeroed by the
   // previous call's group launch) or from hist_kernel (many, rows stored whole)
@@ -1142,9 +1149,13 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
   const bool hist_k = group && multi_hist_k;
   const bool fused = lean && !h->wide && h->m <= 65537 && total >= 262144 && nbins <= 256 && use_stream(h, total) &&
                      (!group || ((hist_k || hist_in_classify(nbins)) && scan != kScanKernel));
-  if (!fused && (flags & NBG_DEFER_GROUP))
+  if (!fused && (flags & NBG_DEFER_GROUP)) {
+    if (device_ring_running(h->device))
+      return set_error(NBG_EINVAL, "classify (multi): NBG_DEFER_GROUP needs the streaming kernel, which cannot run while "
+                       "a persistent ring runs on device %d (stop it, or call without NBG_DEFER_GROUP)", h->device);
     return set_error(NBG_EINVAL, "classify (multi): NBG_DEFER_GROUP needs the fused path (fixed 64-B slots, >= 262144 "
                      "packets in all, <= 255 backends)");
+  }
   if (!fused) {
     // one batch after another on the same stream (same results, one launch sequence each)
     for (uint32_t j = 0; j < n_batches; ++j) {
@@ -1357,11 +1368,18 @@ struct nbg_ring_queue {
   nbg_ring* r = nullptr;
   uint64_t posted = 0, done = 0;        // this queue's batches posted / complete
   uint64_t gidx[NBG_RING_SLOTS] = {};   // the ring ticket of this queue's ticket t, at t % NBG_RING_SLOTS
+  bool closed = false;                  // closed by nbg_ring_stop: calls fail, nbg_ring_queue_close frees it
 };
 
 struct nbg_ring {
-  nbg_maglev* h = nullptr;
+  nbg_maglev* h = nullptr;             // the owning handle (never touched once `leaked`)
+  int device = 0;                      // copies of the handle's device and backend count
+  uint32_t nb = 0;
   std::mutex mu;                       // posts, completion, queues, grouping: several producer threads
+  // calls that release and retake `mu` while they wait (post, wait): nbg_ring_stop lets them leave
+  // (the ended kernel makes each return) before it closes the queues or frees anything
+  uint32_t calls = 0;
+  bool leaked = false;                 // the kernel did not end at stop: every call returns NBG_EBUSY
   hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
   hipEvent_t ev_start = nullptr, ev_end = nullptr;  // around the kernel on `stream` (its duration)
   size_t hbytes = 0, dbytes = 0;       // the pinned host ring and the uncached device ring
@@ -1391,6 +1409,7 @@ struct nbg_ring {
   GroupSet gsets[kGroupSets];
   uint64_t gcalls = 0;
   std::vector<nbg_ring_queue*> queues;  // open RX queues (closed by nbg_ring_stop)
+  std::vector<nbg_ring_queue*> closed;  // queues nbg_ring_stop closed: freed by nbg_ring_queue_close or with the ring
   bool ended = false;  // the kernel has ended (stop, idle timeout, or a fault)
   // hipStreamQuery is not cheap on a stream with a resident kernel, so the kernel's end is only
   // checked after the completed count has not moved for kStallCheck
@@ -1422,9 +1441,15 @@ void queue_refresh(nbg_ring_queue* q) {
 
 constexpr auto kStallCheck = std::chrono::milliseconds(2);
 
-// The kernel has ended?  (hipStreamQuery: the ring kernel is the last work on its stream.)
+// The kernel has ended?  (hipStreamQuery: the ring kernel is the last work on its stream.)  An ended
+// ring no longer holds the device: other handles' calls take the LDS-hungry kernels again and a new
+// ring may start, before this one's nbg_ring_stop.  Under r->mu.
 bool ring_ended(nbg_ring* r) {
-  if (!r->ended && hipStreamQuery(r->stream) != hipErrorNotReady) r->ended = true;
+  if (!r->ended && hipStreamQuery(r->stream) != hipErrorNotReady) {
+    r->ended = true;
+    std::lock_guard<std::mutex> dg(g_dev_ring_mu);
+    if (static_cast<size_t>(r->device) < g_dev_ring.size() && g_dev_ring[r->device] == r) g_dev_ring[r->device] = nullptr;
+  }
   return r->ended;
 }
 
@@ -1446,9 +1471,30 @@ void ring_pause(Clock::time_point t0) {
   if (Clock::now() - t0 > std::chrono::microseconds(200)) std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
+// Stop: the open queues become closed ones (their producers may still hold them).  Under r->mu.
 void ring_close_queues(nbg_ring* r) {
-  for (auto* q : r->queues) delete q;
+  for (auto* q : r->queues) {
+    q->closed = true;
+    r->closed.push_back(q);
+  }
   r->queues.clear();
+}
+
+// A call that waits on the ring, counted in r->calls for its whole duration.  Under r->mu.
+struct RingCall {
+  nbg_ring* r;
+  explicit RingCall(nbg_ring* r_) : r(r_) {
+    std::lock_guard<std::mutex> g(r->mu);
+    ++r->calls;
+  }
+  ~RingCall() {
+    std::lock_guard<std::mutex> g(r->mu);
+    --r->calls;
+  }
+};
+
+int ring_leaked_error() {
+  return set_error(NBG_EBUSY, "ring: its kernel did not end at nbg_ring_stop (leaked; the device stays busy)");
 }
 
 // Wait for the grouping streams' work on the scratch sets and release them.
@@ -1469,7 +1515,10 @@ void ring_free(nbg_ring* r) {
     (void)hipFree(g.prefix);
     (void)hipFree(g.totals);
   }
-  ring_close_queues(r);
+  for (auto* q : r->queues) delete q;
+  for (auto* q : r->closed) delete q;
+  r->queues.clear();
+  r->closed.clear();
   if (r->host) (void)hipHostFree(r->host);
   if (r->dev) (void)hipFree(r->dev);
   if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -1483,6 +1532,8 @@ int ring_alloc(nbg_maglev* h, nbg_ring** out) {
   auto* r = new (std::nothrow) nbg_ring;
   if (!r) return set_error(NBG_ENOMEM, "ring_start: out of memory");
   r->h = h;
+  r->device = h->device;
+  r->nb = h->nb;
   r->grid = h->cus - 1;  // classify blocks; one more block, on a CU of its own, is the relay
   if (const char* e = std::getenv("NBG_RING_REPS")) {  // measurement: replicas, a power of two <= 256
     const uint32_t v = static_cast<uint32_t>(std::atoi(e));
@@ -1569,9 +1620,12 @@ int ring_post_one(nbg_ring* r, nbg_ring_queue* q, uint8_t* d_pkts, uint64_t n_pk
   int rc = ring_check_batch(d_pkts, n_pkts, d_backend);
   if (rc) return rc;
   const auto t0 = Clock::now();
+  RingCall call(r);
   for (;;) {
     {
       std::lock_guard<std::mutex> g(r->mu);
+      if (r->leaked) return ring_leaked_error();
+      if (q && q->closed) return set_error(NBG_EINVAL, "ring_queue_post: the queue was closed by nbg_ring_stop");
       ring_refresh(r);
       if (ring_gone(r)) return ring_state_error(r);
       if (r->posted - r->completed < r->slots) {
@@ -1631,9 +1685,9 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
     return set_error(NBG_EINVAL, "ring_group: ticket %llu is older than the ring's %u slots", (unsigned long long)ticket,
                      r->slots);
   ring_refresh(r);
-  DeviceGuard g(r->h->device);
+  DeviceGuard g(r->device);
   const auto [backend, n_pkts] = r->rec[ticket & (r->slots - 1)];
-  const uint32_t nbins = r->h->nb + 1;
+  const uint32_t nbins = r->nb + 1;
   nbg_ring::GroupSet* gs = nullptr;
   int rc = ring_gset(r, s, &gs);
   if (rc) return rc;
@@ -1653,7 +1707,7 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
   HistArgs ha{};
   ha.backend = backend;
   ha.n_pkts = static_cast<uint32_t>(n_pkts);
-  ha.nb = r->h->nb;
+  ha.nb = r->nb;
   ha.part_pkts = part_pkts;
   ha.n_parts = n_parts;
   ha.part_hist = gs->rows;
@@ -1671,7 +1725,7 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
   GroupArgs ga{};
   ga.backend = backend;
   ga.n_pkts = static_cast<uint32_t>(n_pkts);
-  ga.nb = r->h->nb;
+  ga.nb = r->nb;
   uint32_t bits = 0;
   while ((1u << bits) < nbins) ++bits;
   ga.bits = bits;
@@ -1701,7 +1755,7 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
                      (unsigned long long)first, r->slots);
   for (uint32_t j = 0; j < n; ++j)
     if (!d_perm[j] || !d_counts[j]) return set_error(NBG_EINVAL, "ring_group_burst: null output of batch %u", j);
-  const uint32_t nbins = r->h->nb + 1;
+  const uint32_t nbins = r->nb + 1;
   uint64_t max_n = 0;
   bool empty = false;
   for (uint32_t j = 0; j < n; ++j) {
@@ -1721,7 +1775,7 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
     return NBG_OK;
   }
   ring_refresh(r);
-  DeviceGuard g(r->h->device);
+  DeviceGuard g(r->device);
   nbg_ring::GroupSet* gs = nullptr;
   int rc = ring_gset(r, s, &gs);
   if (rc) return rc;
@@ -1741,14 +1795,14 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
     HistArgs& ha = hm.h[j];
     ha.backend = backend;
     ha.n_pkts = static_cast<uint32_t>(n_pkts);
-    ha.nb = r->h->nb;
+    ha.nb = r->nb;
     ha.part_pkts = part_pkts;
     ha.n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
     ha.part_hist = rows;
     GroupArgs& ga = gm.g[j];
     ga.backend = backend;
     ga.n_pkts = static_cast<uint32_t>(n_pkts);
-    ga.nb = r->h->nb;
+    ga.nb = r->nb;
     ga.bits = bits;
     ga.n_parts = ha.n_parts;
     ga.part_pkts = part_pkts;
@@ -1768,9 +1822,11 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
 template <typename F>
 int ring_wait_for(nbg_ring* r, uint32_t timeout_ms, const char* what, uint64_t ticket, F done) {
   const auto t0 = Clock::now();
+  RingCall call(r);
   for (;;) {
     {
       std::lock_guard<std::mutex> g(r->mu);
+      if (r->leaked) return ring_leaked_error();
       ring_refresh(r);
       if (done()) return NBG_OK;
       if (ring_gone(r)) {
@@ -1893,6 +1949,7 @@ int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_b
     if (rc) return rc;
   }
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
   *first_ticket = r->posted;
   ring_refresh(r);
   if (ring_gone(r)) return ring_state_error(r);
@@ -1911,6 +1968,7 @@ int nbg_ring_post(nbg_ring* r, uint8_t* d_pkts, uint64_t n_pkts, uint16_t* d_bac
 int nbg_ring_group(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* d_counts, void* stream) {
   if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group: null argument");
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
   return ring_group_locked(r, ticket, d_perm, d_counts, static_cast<hipStream_t>(stream));
 }
 
@@ -1918,6 +1976,7 @@ int nbg_ring_group_burst(nbg_ring* r, uint64_t first_ticket, uint32_t n_batches,
                          uint32_t* const* d_counts, void* stream) {
   if (!r || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_group_burst: null argument");
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
   return ring_group_burst_locked(r, first_ticket, n_batches, d_perm, d_counts, static_cast<hipStream_t>(stream));
 }
 
@@ -1939,6 +1998,7 @@ int nbg_ring_kernel_ms(nbg_maglev* h, float* ms) {
 int nbg_ring_poll(nbg_ring* r, uint64_t* completed) {
   if (!r || !completed) return set_error(NBG_EINVAL, "ring_poll: null argument");
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
   ring_refresh(r);
   *completed = r->completed;
   if (r->completed < r->posted && ring_gone(r)) return ring_state_error(r);
@@ -1949,6 +2009,7 @@ int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms) {
   if (!r) return set_error(NBG_EINVAL, "ring_wait: null ring");
   {
     std::lock_guard<std::mutex> g(r->mu);
+    if (r->leaked) return ring_leaked_error();
     if (ticket >= r->posted)
       return set_error(NBG_EINVAL, "ring_wait: ticket %llu was not posted", (unsigned long long)ticket);
   }
@@ -1957,25 +2018,36 @@ int nbg_ring_wait(nbg_ring* r, uint64_t ticket, uint32_t timeout_ms) {
 
 int nbg_ring_stop(nbg_ring* r) {
   if (!r) return set_error(NBG_EINVAL, "ring_stop: null ring");
-  DeviceGuard g(r->h->device);
+  std::unique_lock<std::mutex> lk(r->mu);
+  if (r->leaked) return ring_leaked_error();
+  DeviceGuard g(r->device);
   __atomic_store_n(&const_cast<RingCtl*>(const_cast<volatile RingCtl*>(r->ctl))->stop, 1u, __ATOMIC_RELEASE);
   const auto t0 = Clock::now();
   int rc = NBG_OK;
-  std::unique_lock<std::mutex> lk(r->mu);
   while (!ring_ended(r)) {
     if (Clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 5000u)) {
       // never free memory a running kernel may still read: leak the ring (and the handle's device
-      // memory, nbg_maglev_destroy) instead; the device stays marked busy
+      // memory, nbg_maglev_destroy) instead; the device stays marked busy, and every later call on
+      // the ring returns NBG_EBUSY without touching the handle
       r->h->ring = nullptr;
       r->h->ring_leaked = true;
+      r->leaked = true;
       return set_error(NBG_EBUSY, "ring_stop: the kernel did not end (its memory is leaked, the device stays busy)");
     }
+    lk.unlock();  // producers blocked in post / wait take the lock to see the kernel end
     ring_pause(t0);
+    lk.lock();
+  }
+  // the kernel has ended, so every call still waiting on the ring returns at its next look: let them
+  // leave before the queues close and the scratch is released (or the ring freed)
+  while (r->calls) {
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    lk.lock();
   }
   {
     std::lock_guard<std::mutex> dg(g_dev_ring_mu);
-    if (static_cast<size_t>(r->h->device) < g_dev_ring.size() && g_dev_ring[r->h->device] == r)
-      g_dev_ring[r->h->device] = nullptr;
+    if (static_cast<size_t>(r->device) < g_dev_ring.size() && g_dev_ring[r->device] == r) g_dev_ring[r->device] = nullptr;
   }
   const hipError_t e = hipStreamQuery(r->stream);
   ring_refresh(r);
@@ -1987,8 +2059,9 @@ int nbg_ring_stop(nbg_ring* r) {
   if (e == hipSuccess && hipEventElapsedTime(&ms, r->ev_start, r->ev_end) == hipSuccess) h->ring_kernel_ms = ms;
   ring_close_queues(r);
   if (e != hipSuccess) {
-    lk.unlock();  // ring_free deletes the mutex
-    ring_free(r);
+    // the stream failed: the ring is not reused, but callers may still hold it and its queues, so it
+    // is kept (every call reports the failure) and freed with the handle
+    h->ring_dead.push_back(r);
     return rc;
   }
   // keep the buffers, stream and events for the next start; the grouping streams' work on the
@@ -2002,6 +2075,7 @@ int nbg_ring_queue_open(nbg_ring* r, nbg_ring_queue** out) {
   if (!r || !out) return set_error(NBG_EINVAL, "ring_queue_open: null argument");
   *out = nullptr;
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
   if (r->queues.size() >= NBG_RING_MAX_QUEUES)
     return set_error(NBG_EBUSY, "ring_queue_open: the ring has %u queues open", NBG_RING_MAX_QUEUES);
   auto* q = new (std::nothrow) nbg_ring_queue;
@@ -2016,6 +2090,13 @@ int nbg_ring_queue_close(nbg_ring_queue* q) {
   if (!q) return set_error(NBG_EINVAL, "ring_queue_close: null queue");
   nbg_ring* r = q->r;
   std::lock_guard<std::mutex> g(r->mu);
+  if (q->closed) {  // closed by nbg_ring_stop: free it now
+    auto it = std::find(r->closed.begin(), r->closed.end(), q);
+    if (it == r->closed.end()) return set_error(NBG_EINVAL, "ring_queue_close: not a queue of its ring");
+    r->closed.erase(it);
+    delete q;
+    return NBG_OK;
+  }
   auto it = std::find(r->queues.begin(), r->queues.end(), q);
   if (it == r->queues.end()) return set_error(NBG_EINVAL, "ring_queue_close: not an open queue of its ring");
   r->queues.erase(it);
@@ -2032,6 +2113,8 @@ int nbg_ring_queue_poll(nbg_ring_queue* q, uint64_t* completed) {
   if (!q || !completed) return set_error(NBG_EINVAL, "ring_queue_poll: null argument");
   nbg_ring* r = q->r;
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
+  if (q->closed) return set_error(NBG_EINVAL, "ring_queue_poll: the queue was closed by nbg_ring_stop");
   ring_refresh(r);
   queue_refresh(q);
   *completed = q->done;
@@ -2044,10 +2127,14 @@ int nbg_ring_queue_wait(nbg_ring_queue* q, uint64_t ticket, uint32_t timeout_ms)
   nbg_ring* r = q->r;
   {
     std::lock_guard<std::mutex> g(r->mu);
+    if (r->leaked) return ring_leaked_error();
+    if (q->closed) return set_error(NBG_EINVAL, "ring_queue_wait: the queue was closed by nbg_ring_stop");
     if (ticket >= q->posted)
       return set_error(NBG_EINVAL, "ring_queue_wait: ticket %llu was not posted on this queue",
                        (unsigned long long)ticket);
   }
+  // a queue stop closes while this waits still has its tickets' completion (the ring completes every
+  // posted batch before it ends), so the wait reports that rather than the close
   return ring_wait_for(r, timeout_ms, "ring_queue_wait", ticket, [&] {
     queue_refresh(q);
     return q->done > ticket;
@@ -2058,6 +2145,8 @@ int nbg_ring_queue_group(nbg_ring_queue* q, uint64_t ticket, uint32_t* d_perm, u
   if (!q || !d_perm || !d_counts) return set_error(NBG_EINVAL, "ring_queue_group: null argument");
   nbg_ring* r = q->r;
   std::lock_guard<std::mutex> g(r->mu);
+  if (r->leaked) return ring_leaked_error();
+  if (q->closed) return set_error(NBG_EINVAL, "ring_queue_group: the queue was closed by nbg_ring_stop");
   if (ticket >= q->posted)
     return set_error(NBG_EINVAL, "ring_queue_group: ticket %llu was not posted on this queue", (unsigned long long)ticket);
   if (q->posted - ticket > NBG_RING_SLOTS)

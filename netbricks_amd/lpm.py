@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import NBG_DEFER_GROUP, NBG_LUT_LDS, NBG_OWNED_WINDOWS, NBG_STREAM_DESC, check, lib
-from .maglev import GroupedBatch, Maglev, _ptr
+from .maglev import GroupedBatch, Maglev, _check_owned, _ptr
 
 __all__ = ["Lpm", "build_lpm", "chain_lpm_maglev", "chain_lpm_maglev_multi", "LpmResult"]
 
@@ -89,13 +89,15 @@ class Lpm:
 def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int = 3, stride: int = 64,
                      frame_len: int = 60, offsets=None, lens=None, owned_windows: bool = False,
                      defer_group: bool = False, group: bool = True, lut_lds: bool = False,
-                     stream_desc: bool = False, gate=None,
+                     stream_desc: bool = False, gate=None, bounds_check: bool = True,
                      backend=None, perm=None,
                      counts=None, stream=None) -> LpmResult:
     """lpm(...) -> maglev(...) over a device-resident batch (packet layout as Maglev.group_by)."""
     import torch
 
     dev = pkts.device
+    if owned_windows and bounds_check:
+        _check_owned("offsets", pkts, offsets, n_pkts)
     if gate is None:
         gate = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
     if backend is None:
@@ -115,14 +117,15 @@ def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int
     return LpmResult(gate, backend, perm if group else None, counts if group else None)
 
 
-def chain_lpm_maglev_multi(mg: Maglev, lpm: Lpm, batches, *, lpm_groups: int = 3, owned_windows: bool = True,
-                           group: bool = True, defer_group: bool = False, stream=None) -> list:
+def chain_lpm_maglev_multi(mg: Maglev, lpm: Lpm, batches, *, lpm_groups: int = 3, owned_windows: bool = False,
+                           group: bool = True, defer_group: bool = False, bounds_check: bool = True,
+                           stream=None) -> list:
     """lpm(...) -> maglev(...) over several descriptor batches ((pkts, offsets, lens, n_pkts) each) in
     one launch of each kernel (nbg_chain_lpm_maglev_multi).  Returns one LpmResult per batch, as
     chain_lpm_maglev would give it for that batch alone."""
     import torch
 
-    arr, out = mg._desc_batches(batches, group, True, True)
+    arr, out = mg._desc_batches(batches, group, True, True, owned_windows and bounds_check)
     if stream is None:
         stream = torch.cuda.current_stream(torch.device("cuda", mg.device)).cuda_stream
     flags = (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_DEFER_GROUP if defer_group else 0)

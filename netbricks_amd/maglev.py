@@ -62,6 +62,19 @@ def _slot_tail(stride: int, frame_len: int) -> int:
     return max(64, frame_len) if stride >= 64 else frame_len
 
 
+def _check_owned(name: str, pkts, offsets, n_pkts: int) -> None:
+    """NBG_OWNED_WINDOWS: the kernels read, and in place rewrite, the whole 64-B window at every offset,
+    so each window must lie inside pkts (one device reduction; bounds_check=False skips it for callers
+    that checked their descriptors once)."""
+    import torch
+
+    if n_pkts and offsets is not None:
+        top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
+        if top + 64 > pkts.numel():
+            raise ValueError(f"{name}: the 64-B owned window at offset {top} runs past the end of pkts "
+                             f"({pkts.numel()} B); pass owned_windows=False for frames without a 64-B data room")
+
+
 def build_lut(backends: Sequence[str], lut_size: int = 65537) -> np.ndarray:
     """The product's host LUT builder (Maglev::new, nf.rs:70-76) -> u16 entries."""
     arr, lens, _keep = _lib.names_args(backends)
@@ -186,7 +199,7 @@ class Maglev:
                  swap_macs: bool = True, group: bool = True, scatter: bool = True, lut_lds: bool = False,
                  owned_windows: bool = False, wb_partial: bool = False,
                  defer_group: bool = False, lut_tiled: bool = False, stream_desc: bool = False,
-                 group_lag: bool = False,
+                 group_lag: bool = False, bounds_check: bool = True,
                  backend=None, perm=None, counts=None, mac_out=None, stream=None) -> GroupedBatch:
         """Classify a device-resident batch (torch uint8 tensor on this device).
 
@@ -205,6 +218,8 @@ class Maglev:
             raise ValueError("pkts: smaller than n_pkts fixed slots")
         _check_dev("offsets", offsets, torch.uint32, n_pkts, dev)
         _check_dev("lens", lens, torch.uint16, n_pkts, dev)
+        if owned_windows and bounds_check:
+            _check_owned("offsets", pkts, offsets, n_pkts)
         _check_dev("backend", backend, torch.uint16, n_pkts, dev)
         _check_dev("perm", perm, torch.uint32, n_pkts, dev)
         _check_dev("counts", counts, torch.uint32, self.n_backends + 1, dev)
@@ -264,7 +279,7 @@ class Maglev:
         self._multi_keep = arr
         return [g for g, _ in out] if not records else out
 
-    def _desc_batches(self, batches, group: bool, scatter: bool, gates: bool):
+    def _desc_batches(self, batches, group: bool, scatter: bool, gates: bool, owned: bool = False):
         """ctypes array of nbg_desc_batch for group_by_desc_multi / chain_lpm_maglev_multi: `batches`
         is a list of (pkts, offsets, lens, n_pkts) device tensors (u8, u32, u16) on this device."""
         import torch
@@ -283,6 +298,8 @@ class Maglev:
             _check_dev(f"batch {j} lens", lens, torch.uint16, n_pkts, dev)
             if n_pkts and (offsets is None or lens is None):
                 raise ValueError(f"batch {j}: offsets and lens are required")
+            if owned:
+                _check_owned(f"batch {j} offsets", pkts, offsets, n_pkts)
             backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
             perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev) if group and scatter else None
             counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev) if group else None
@@ -292,20 +309,22 @@ class Maglev:
             out.append((backend, perm, counts, gate))
         return arr, out
 
-    def group_by_desc_multi(self, batches, *, swap_macs: bool = True, owned_windows: bool = True,
+    def group_by_desc_multi(self, batches, *, swap_macs: bool = True, owned_windows: bool = False,
                             group: bool = True, scatter: bool = True, defer_group: bool = False,
-                            stream=None) -> list:
+                            wb_partial: bool = False, bounds_check: bool = True, stream=None) -> list:
         """Classify several device-resident descriptor batches (IMIX: (pkts, offsets, lens, n_pkts)
         per batch) in one launch of each kernel (nbg_maglev_classify_desc_multi).  Every batch gets
         its own backend / perm / counts, as group_by(..., offsets=, lens=) would give it alone.
+        owned_windows=True (mbuf data rooms: the 64 B at every offset belong to that frame) lets the
+        MAC swap write whole windows back; every window is then checked to lie inside its pkts.
         Returns one GroupedBatch per batch."""
         import torch
 
-        arr, out = self._desc_batches(batches, group, scatter, False)
+        arr, out = self._desc_batches(batches, group, scatter, False, owned_windows and bounds_check)
         if stream is None:
             stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
         flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_OWNED_WINDOWS if owned_windows else 0)
-                 | (NBG_DEFER_GROUP if defer_group else 0))
+                 | (NBG_DEFER_GROUP if defer_group else 0) | (NBG_WB_PARTIAL if wb_partial else 0))
         check(lib.nbg_maglev_classify_desc_multi(self._h, arr, len(batches), flags, stream),
               "nbg_maglev_classify_desc_multi")
         self._multi_keep = arr

@@ -562,3 +562,70 @@ def test_ring_repeated_inputs_in_place(torch_cuda):
         np.testing.assert_array_equal(d[i].cpu().numpy(), swapped if times % 2 else bufs[i], err_msg=f"buffer {i}")
         np.testing.assert_array_equal(_got(torch, outs[posts - k + ((i - posts) % k)]), be)
     mg.close()
+
+
+@pytest.mark.parametrize("swap", [False, True])
+def test_ring_stop_while_producers_blocked(torch_cuda, swap):
+    """nbg_ring_stop while other producer threads are blocked inside nbg_ring_queue_post (more batches
+    outstanding than the ring's 64 slots) or nbg_ring_queue_wait: stop waits for them to leave, their
+    calls return (a completion or the ring's end, never a crash or a hang), and every later call on a
+    closed queue fails cleanly.  Every batch a producer saw complete is bit-exact; the handle starts a
+    new ring afterwards."""
+    import threading
+
+    torch = torch_cuda
+    import netbricks_amd as nb
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    nq, per_q, n = 4, 20, 262144  # 80 buffers in flight at most: more than the 64 slots, so posts block
+    bufs = [[nb.make_trace(n, 0, seed=5000 + 100 * q + i)[0] for i in range(per_q)] for q in range(nq)]
+    d = [[torch.from_numpy(b.copy()).cuda() for b in bq] for bq in bufs]
+    outs = [[torch.empty(n, dtype=torch.uint16, device="cuda") for _ in range(per_q)] for _ in range(nq)]
+    torch.cuda.synchronize()
+    done = [[] for _ in range(nq)]  # (ticket, buffer) a producer saw complete
+    errs, started = [], threading.Barrier(nq + 1)
+    ring = mg.ring(swap_macs=swap)
+    qs = [ring.queue() for _ in range(nq)]
+
+    def producer(q):
+        started.wait()
+        i = 0
+        try:
+            while True:
+                if i >= per_q:  # the buffer's previous batch must be complete before it is reposted
+                    qs[q].wait(i - per_q)
+                    done[q].append(i - per_q)
+                qs[q].post(d[q][i % per_q], n, outs[q][i % per_q])
+                i += 1
+        except (nb.NbgError, RuntimeError) as e:  # the ring stopped under the call
+            errs.append(type(e).__name__)
+
+    th = [threading.Thread(target=producer, args=(q,), daemon=True) for q in range(nq)]
+    for t in th:
+        t.start()
+    started.wait()
+    time.sleep(0.05)
+    t0 = time.perf_counter()
+    ring.stop()
+    assert time.perf_counter() - t0 < 10
+    for t in th:
+        t.join(10)
+    assert not any(t.is_alive() for t in th)
+    assert len(errs) == nq, errs
+    with pytest.raises(RuntimeError):
+        qs[0].post(d[0][0], n, outs[0][0])
+    with pytest.raises(nb.NbgError):
+        qs[1].wait(0)
+    if not swap:  # read only: every buffer is pristine, so each completed batch checks against it
+        for q in range(nq):
+            for i in done[q][-3:]:
+                np.testing.assert_array_equal(_got(torch, outs[q][i % per_q]), _expect(bufs[q][i % per_q], n, lut,
+                                                                                       False)[0])
+    buf = nb.make_trace(n, 0, seed=99)[0]
+    dd = torch.from_numpy(buf.copy()).cuda()
+    out = torch.empty(n, dtype=torch.uint16, device="cuda")
+    with mg.ring(swap_macs=False) as ring2:  # the handle runs a new ring
+        ring2.wait(ring2.post(dd, n, out))
+    np.testing.assert_array_equal(_got(torch, out), _expect(buf, n, lut, False)[0])
+    mg.close()

@@ -117,11 +117,11 @@ def main():
             j = i % S if j is None else j
             k = i % N_BATCHES
             if cfg == "c5":
-                nb.chain_lpm_maglev(mgs[j], lpm, bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
+                nb.chain_lpm_maglev(mgs[j], lpm, bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, bounds_check=False,
                                     defer_group=defer, gate=gates[j], stream=sts[j].cuda_stream,
                                     stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])
             else:
-                mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True,
+                mgs[j].group_by(bufs[k], BATCH, offsets=offs[k], lens=lens[k], owned_windows=True, bounds_check=False,
                                 swap_macs=c3v != "read_only", mac_out=recs[j] if c3v == "records" else None,
                                 defer_group=defer, lut_tiled=cfg == "c3t", stream=sts[j].cuda_stream,
                                 stream_desc=args.stream_desc, lut_lds=args.lut_lds, **outs[j])

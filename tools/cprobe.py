@@ -57,7 +57,7 @@ def main():
         elif args.variant == "inplace":
             mg.group_by(bufs[i % 8], n, group=False, **kw)
         elif args.variant == "c5":
-            nb.chain_lpm_maglev(mg, lpm, bufs[i % 8], n, offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True,
+            nb.chain_lpm_maglev(mg, lpm, bufs[i % 8], n, offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True, bounds_check=False,
                                 defer_group=True, gate=gate, perm=perm, counts=cnt, **kw)
             mg.finish_group()
         elif args.variant == "macout":

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--tpw", default="1", help="comma-separated NBG_TPW values (tiles per wave), one handle each")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--lut-lds", action="store_true", help="stage the LUT in LDS (NBG_LUT_LDS)")
+    ap.add_argument("--wb-partial", default="0", help="C3: comma-separated 0/1: NBG_WB_PARTIAL (rewrite only the "
+                                                    "16 B holding the MACs of each owned window)")
     ap.add_argument("--n", default=str(1 << 20), help="comma-separated batch sizes (packets); times are also per 1M")
     ap.add_argument("--max-plen", type=int, default=32,
                     help="C5: drop routes longer than this (24: no tbl_long lookups; measures their cost)")
@@ -62,7 +64,7 @@ def main():
             counts = torch.empty(66, dtype=torch.uint32, device=dev)
 
             def call(i):
-                nb.chain_lpm_maglev(mg, lpm, bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True,
+                nb.chain_lpm_maglev(mg, lpm, bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True, bounds_check=False,
                                     defer_group=True, gate=gate, stream=st.cuda_stream, backend=backend, perm=perm,
                                     counts=counts, stream_desc=args.stream_desc, lut_lds=args.lut_lds)
         else:
@@ -70,7 +72,7 @@ def main():
             counts = torch.empty(1001, dtype=torch.uint32, device=dev)
 
             def call(i):
-                mg.group_by(bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True, defer_group=True,
+                mg.group_by(bufs[i % 2], n, offsets=offs[i % 2], lens=lens[i % 2], owned_windows=True, bounds_check=False, defer_group=True,
                             stream=st.cuda_stream, backend=backend, perm=perm, counts=counts,
                             stream_desc=args.stream_desc, lut_lds=args.lut_lds)
         for i in range(6):
@@ -110,18 +112,20 @@ def multi(args, torch, nb, KernelTimer, routes, out):
     st = torch.cuda.Stream(dev)
     for rnd in range(args.rounds):
         for which in args.which.split(","):
-            for k in ks:
+            for k, wbp in [(k, int(w)) for k in ks for w in args.wb_partial.split(",")]:
                 if which == "c5":
                     mg = nb.Maglev([f"backend-{i}" for i in range(65)], 65537)
                     lpm = nb.Lpm(routes["reference"] + routes["mixed"])
 
                     def call():
-                        nb.chain_lpm_maglev_multi(mg, lpm, dbs[:k], defer_group=True, stream=st.cuda_stream)
+                        nb.chain_lpm_maglev_multi(mg, lpm, dbs[:k], owned_windows=True, bounds_check=False,
+                                                  defer_group=True, stream=st.cuda_stream)
                 else:
                     mg = nb.Maglev([f"be{i}" for i in range(1000)], 655373)
 
                     def call():
-                        mg.group_by_desc_multi(dbs[:k], defer_group=True, stream=st.cuda_stream)
+                        mg.group_by_desc_multi(dbs[:k], owned_windows=True, bounds_check=False, wb_partial=bool(wbp),
+                                               defer_group=True, stream=st.cuda_stream)
                 for _ in range(4):
                     call()
                     mg.finish_group(st.cuda_stream)
@@ -139,7 +143,7 @@ def multi(args, torch, nb, KernelTimer, routes, out):
                 c, g = float(kt.ms().mean()) * 1e3, float(gt.ms().mean()) * 1e3
                 kt.close()
                 gt.close()
-                out[f"{which}_multi{k}_r{rnd}"] = {"classify_us": round(c, 2), "classify_us_per_batch": round(c / k, 2),
+                out[f"{which}_multi{k}_r{rnd}" + (f"_wbp{wbp}" if which == "c3" else "")] = {"classify_us": round(c, 2), "classify_us_per_batch": round(c / k, 2),
                                                    "group_us": round(g, 2), "group_us_per_batch": round(g / k, 2)}
                 mg.close()
                 if which == "c5":

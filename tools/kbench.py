@@ -53,7 +53,7 @@ def main():
     def kw(i):
         extra = dict(lut_lds=True) if args.lut_lds else {}
         if desc:
-            return dict(offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True, **extra)
+            return dict(offsets=offs[i % 8], lens=lens[i % 8], owned_windows=True, bounds_check=False, **extra)
         return dict(stride=stride, frame_len=60, **extra)
 
     variants = {
