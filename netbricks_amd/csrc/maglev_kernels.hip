@@ -29,9 +29,6 @@ namespace nbg {
 
 namespace {
 
-#ifndef NBG_CHAIN_ABL  // measurement builds (tools/build_ab.sh): 1 no tbl24 gather, 2 no LUT gather, 4 no gate stores
-#define NBG_CHAIN_ABL 0
-#endif
 constexpr uint32_t kSentinel = NBG_SENTINEL;
 constexpr uint32_t kEth = 14;
 
@@ -186,17 +183,10 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 // Packet windows are read once: the streaming policy.  Round 1 measured it neutral on C2's 4-stream
 // path (then served by this kernel); round 2, with C2 on the streaming kernel, it cut C3 from 48.9 to
 // 44.8 us and C5 from 28.3 to 26.5 us per batch at 3 streams (profiles/r02_c3_c5_ntloads_ab.txt).
-#ifndef NBG_NT_LOADS
-#define NBG_NT_LOADS 1
-#endif
-#if NBG_NT_LOADS
 __device__ __forceinline__ uint4 ldg16(const uint8_t* p) {
   const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
   return make_uint4(w.x, w.y, w.z, w.w);
 }
-#else
-__device__ __forceinline__ uint4 ldg16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
-#endif
 // Non-temporal 16-B store: in-place window write-back streams ~10 % faster with nt (tools/membench).
 __device__ __forceinline__ void stg16_nt(uint8_t* p, uint4 v) {
   const u32x4_t w = {v.x, v.y, v.z, v.w};
@@ -310,20 +300,11 @@ __device__ __forceinline__ void load_tile(const ClassifyArgs& a, uint32_t wbase,
   for (int k = 0; k < 4; ++k) t.ch[k] = ldg16(addr[k]);
 }
 
-#ifdef NBG_CPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch
-constexpr uint32_t kProbeWaves = 1u << 15;
-__device__ unsigned long long g_cprobe[kProbeWaves * 4];
-#define CPROBE(k)                                                                      \
-  if (lane == 0 && gw < kProbeWaves) g_cprobe[gw * 4 + (k)] = wall_clock64();
-#else
-#define CPROBE(k)
-#endif
-
 // One transposed 64-packet tile of classify_kernel (its loads in `cur`, its chunks 0..2 in the
 // wave's LDS rows `xp`): classify each lane's packet, write back, count.  Packets off the fast
 // path are classified after this tile's loads, stores and gathers are all issued (`slow`): their
 // byte-wise loads would otherwise make the compiler wait for every outstanding load.
-template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL>
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT>
 __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8_t* lut_lds, const uint8_t* xp,
                                               uint32_t* hist, uint32_t lane, uint32_t part, uint32_t quad,
                                               uint32_t wbase, const TileMeta& meta, const TileRegs& cur) {
@@ -347,32 +328,15 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
       const uint32_t src = (c1.z >> 16) | (c1.w << 16);
       const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
       const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
-      if constexpr (ABL == 1) {
-        bin = (src ^ dst ^ ports) % a.nb;
-      } else if constexpr (ABL == 3) {
-        uint32_t lo, hi;
-        fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-        bin = mod_f4(lo, hi) % a.nb;
-      } else if constexpr (ABL == 4) {
-        bin = lut_get<LUTM>(a, lut_lds, (src ^ dst ^ ports) % a.m);
-      } else {
-        uint32_t lo, hi;
-        if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
-          const uint32_t ip = __builtin_bswap32(src);
-#if NBG_CHAIN_ABL & 1  // measurement builds: no tbl24 gather (gate from the address)
-          gate = (ip >> 8) & 1u;
-#else
-          gate = a.tbl24[ip >> 8];
-#endif
-          iplo = ip & 0xffu;
-          resolve = true;
-        }
-        fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-#if NBG_CHAIN_ABL & 2  // measurement builds: no LUT gather
-        if constexpr (CHAIN) bin = lo % a.nb; else
-#endif
-        bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
+      uint32_t lo, hi;
+      if constexpr (CHAIN) {  // tbl24 gather issued here, resolved after the LUT gather
+        const uint32_t ip = __builtin_bswap32(src);
+        gate = a.tbl24[ip >> 8];
+        iplo = ip & 0xffu;
+        resolve = true;
       }
+      fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
+      bin = lookup<LUTM, F4>(a, lut_lds, lo, hi);
     } else {
       slow = true;
     }
@@ -414,9 +378,6 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
     if (slow) bin = classify_slow<LUTM, F4, CHAIN>(a, lut_lds, pown, meta.len, p_own, gate);
     if constexpr (CHAIN) {
       if (resolve && (gate & 0x8000u)) gate = a.tbl_long[((gate & 0x7fffu) << 8) + iplo];
-#if NBG_CHAIN_ABL & 4  // measurement builds: no gate stores
-      if (gate == 0xfffeu)
-#endif
       a.gate[p_own] = static_cast<uint16_t>(gate);
       if (gate >= a.lpm_groups) bin = a.nb;  // test/lpm would panic: never reaches maglev
     }
@@ -437,11 +398,9 @@ __device__ __forceinline__ void classify_tile(const ClassifyArgs& a, const uint8
 // order: stores issued before the gathers would delay their use), then the slow-path packets.
 // One LDS histogram per block (two barriers per launch) is flushed once into the block's partition
 // row (the block's 64 * waves * tiles_per_wave packets divide part_pkts).
-// ABL (diagnostic builds only, selected by NBG_ABL): 1 = no hash/LUT (bin from header bytes);
-// 3 = FNV without the LUT gather; 4 = LUT gather of a trivial hash.
 // The kernel body; `bid` is the block's index within its batch (classify_desc_multi_kernel runs
 // several batches' blocks in one grid).
-template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL, int NT>
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int NT>
 __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint32_t bid) {
   extern __shared__ __align__(16) uint8_t smem[];
   constexpr uint32_t kW = NT / 64u;
@@ -455,11 +414,6 @@ __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint3
   uint32_t* hist = reinterpret_cast<uint32_t*>(smem + lut_bytes + kW * 64u * kXStride);  // per block
   const uint32_t tpw = a.tiles_per_wave;
   const uint32_t t0 = (bid * kW + wave) * tpw;  // first 64-packet tile of this wave
-#ifdef NBG_CPROBE
-  const uint32_t gw = bid * kW + wave;
-  bool first = true;
-#endif
-  CPROBE(0)
 
   // LDS-staged LUT: one 1024-thread block per CU (4 waves per SIMD) leaves VGPRs for kPf tiles'
   // loads in flight beside the tile being classified (a ring of kPf + 1 register tiles; the tile
@@ -517,15 +471,12 @@ __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint3
       const uint32_t wbase = (t0 + i) * 64u;
       if (i >= tpw || wbase >= a.n_pkts) break;  // wave-uniform
       transpose(rt[i % kRing]);
-#ifdef NBG_CPROBE
-      if (first) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); CPROBE(1) first = false; }
-#endif
       const uint32_t j = i + kPf, wb = (t0 + j) * 64u;
       if (j < tpw && wb < a.n_pkts) {
         rm[j % kRing] = load_meta<LAYOUT>(a, wb, lane);
         load_tile<LAYOUT>(a, wb, rm[j % kRing], part, quad, rt[j % kRing]);
       }
-      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, rm[i % kRing],
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT>(a, lut_lds, xp, hist, lane, part, quad, wbase, rm[i % kRing],
                                                            rt[i % kRing]);
     }
   } else if (LAYOUT == kDesc && tpw > 1u && tpw <= 4u) {
@@ -546,7 +497,7 @@ __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint3
       load_tile<LAYOUT>(a, wbase, mq[i], part, quad, cur);
       __builtin_amdgcn_s_setprio(0);
       transpose(cur);
-      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i], cur);
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT>(a, lut_lds, xp, hist, lane, part, quad, wbase, mq[i], cur);
     }
   } else {
     for (uint32_t i = 0; i < tpw; ++i) {
@@ -560,17 +511,10 @@ __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint3
       load_tile<LAYOUT>(a, wbase, meta, part, quad, cur);
       __builtin_amdgcn_s_setprio(0);
       transpose(cur);
-#ifdef NBG_CPROBE
-      if (first) { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); CPROBE(1) first = false; }
-#endif
-      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT, ABL>(a, lut_lds, xp, hist, lane, part, quad, wbase, meta, cur);
+      classify_tile<LUTM, F4, HIST, CHAIN, LAYOUT>(a, lut_lds, xp, hist, lane, part, quad, wbase, meta, cur);
     }
   }
 
-#ifdef NBG_CPROBE
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's gathers and stores are done
-#endif
-  CPROBE(2)
   if constexpr (HIST) {
     // one flush per block into its partition row (the block's packets never straddle two):
     // 4096-packet rows take ~16 blocks' adds, so they rarely contend
@@ -591,13 +535,12 @@ __device__ __forceinline__ void classify_body(const ClassifyArgs& a, const uint3
       }
     }
   }
-  CPROBE(3)
 }
 
 
-template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int ABL = 0, int NT = kBlock>
+template <int LUTM, bool F4, bool HIST, bool CHAIN, int LAYOUT, int NT = kBlock>
 __global__ __launch_bounds__(NT, CHAIN ? 1 : 2048 / NT) void classify_kernel(ClassifyArgs a) {
-  classify_body<LUTM, F4, HIST, CHAIN, LAYOUT, ABL, NT>(a, blockIdx.x);
+  classify_body<LUTM, F4, HIST, CHAIN, LAYOUT, NT>(a, blockIdx.x);
 }
 
 // Several descriptor batches in one grid (several RX queues' bursts per launch): the launch's ramp
@@ -617,7 +560,7 @@ __global__ __launch_bounds__(kBlock, CHAIN ? 1 : 2048 / kBlock) void classify_de
   b.gate = db.gate[j];
   b.part_hist = db.part_hist[j];
   b.n_pkts = db.n_pkts[j];
-  classify_body<LUTM, F4, HIST, CHAIN, kDesc, 0, kBlock>(b, blockIdx.x - db.blk_base[j]);
+  classify_body<LUTM, F4, HIST, CHAIN, kDesc, kBlock>(b, blockIdx.x - db.blk_base[j]);
 }
 
 // Loads at a 32-bit byte offset from a kernel-argument base: the compiler can then use the
@@ -698,21 +641,9 @@ __device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32
 // (MI355X_MICROARCH.md item 7).  hipcc does not count the inline-asm loads, so each tile is waited
 // for with a counted s_waitcnt vmcnt(4 * tiles issued after it): other VM operations issued in
 // between (stores, flush atomics, the compiler's slow-path loads) only make that wait conservative.
-#ifndef NBG_SW
-#define NBG_SW 8
-#endif
-#ifndef NBG_STREAM_WT  // 1: the streaming kernel's in-place window stores write-through (sc1) instead of nt (A/B)
-#define NBG_STREAM_WT 0
-#endif
-#ifndef NBG_SEQWAIT  // 0: the round-2 tile-count waits (A/B)
-#define NBG_SEQWAIT 1
-#endif
-#ifndef NBG_SRING
-#define NBG_SRING 2
-#endif
-constexpr int kStreamNT = 64 * NBG_SW;         // threads per block (8 waves)
+constexpr int kStreamNT = 512;                 // threads per block (8 waves)
 constexpr int kStreamW = kStreamNT / 64;
-constexpr int kRing = NBG_SRING;               // LDS tile buffers per wave
+constexpr int kRing = 2;                       // LDS tile buffers per wave
 [[maybe_unused]] constexpr int kStreamAhead = kRing - 1;  // tiles in flight while one is classified
 static_assert(kRing >= 2 && kRing <= 3, "classify_stream_kernel tracks the counts of three tiles at most");
 // LDS bytes per packet: 48 (chunks 0..2, all the classify reads) for read-only and records; 64 (the
@@ -720,23 +651,9 @@ static_assert(kRing >= 2 && kRing <= 3, "classify_stream_kernel tracks the count
 // 48-B rows read faster, whole-line write-back beats 16-B partial-line stores)
 template <int MODE>
 constexpr uint32_t row_of() { return MODE == 1 ? 64u : 48u; }
-#ifndef NBG_RO_ROW64  // measurement build: whole 64-B rows (every DMA lane active) for read-only / records too
-#define NBG_RO_ROW64 0
-#endif
 template <int MODE>
-constexpr uint32_t stream_row_of() { return NBG_RO_ROW64 ? 64u : row_of<MODE>(); }
+constexpr uint32_t stream_row_of() { return row_of<MODE>(); }
 constexpr uint32_t kLutLds = 65536;            // LUT bytes staged in LDS
-
-#ifdef NBG_SPROBE  // diagnostic build: per-wave timestamps (wall clock, 100 MHz) of the last launch:
-                   // [0] entry, [1] LUT visible (after the barrier), [2 + k] tile k landed, [11] exit
-constexpr uint32_t kSProbeWaves = 4096, kSProbeSlots = 20;
-__device__ unsigned long long g_sprobe[kSProbeWaves * kSProbeSlots];
-#define SPROBE(slot)                                                                              \
-  if (lane == 0 && blockIdx.x * kStreamW + wave < kSProbeWaves && (slot) < kSProbeSlots)          \
-    g_sprobe[(blockIdx.x * kStreamW + wave) * kSProbeSlots + (slot)] = wall_clock64();
-#else
-#define SPROBE(slot)
-#endif
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(
@@ -763,12 +680,9 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
 // with grouping, read-only 16.1 -> 15.8, in place neutral, records 17.8 -> 18.9 (slower).  So nt for
 // read-only and in place (NT = true), the default policy for records.  The LUT pieces keep the
 // default policy: every CU of an XCD re-reads them from L2.
-#ifndef NBG_TILE_NT  // 0: default policy everywhere (A/B builds)
-#define NBG_TILE_NT 1
-#endif
 template <bool NT>
 __device__ __forceinline__ void glds16_tile(const void* src, uint32_t lds_base) {
-  if constexpr (NT && NBG_TILE_NT) {
+  if constexpr (NT) {
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
@@ -871,19 +785,11 @@ __device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uin
   const uint32_t src = (c1.z >> 16) | (c1.w << 16);
   const uint32_t dst = (c1.w >> 16) | (c2.x << 16);
   const uint32_t ports = (c2.x >> 16) | (c2.y << 16);
-#if NBG_SABL == 2  // measurement build: no hash, no lookup (bin from the header bytes)
-  bin_out = (src ^ dst ^ ports) % a.nb;
-#elif NBG_SABL == 3  // measurement build: FNV, no lookup
-  uint32_t lo, hi;
-  fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
-  bin_out = (lo ^ hi) % a.nb;
-#else
   uint32_t lo, hi;
   fnv_flow(lo, hi, src, dst, ports, c1.y >> 24);
   const uint32_t idx = F4 ? mod_f4(lo, hi) : mod_barrett(lo, hi, a.m, a.mu);
   const uint32_t e = lut[idx & 0xffffu];
   bin_out = (idx >> 16) ? a.lut_tail : e;
-#endif
   if constexpr (MODE == 1) {
     static_assert(kRow == 64, "the in-place swap writes whole slots back from 64-B rows");
     // whole-line write-back from the tile's LDS rows: lane (quad, part) stores chunk `part` of packet
@@ -921,9 +827,6 @@ __device__ __forceinline__ bool stream_classify(const ClassifyArgs& a, const uin
 template <bool F4>
 __device__ __forceinline__ uint32_t stream_finish(const ClassifyArgs& a, const uint8_t* lut, uint32_t p, uint32_t bin,
                                                   bool slow) {
-#ifdef NBG_EXP_NOSLOW
-  slow = false;
-#endif
   if (slow) {
     uint32_t gate;
     bin = classify_slow<kLdsU8Tail, F4, false, true>(a, lut, a.pkts + static_cast<size_t>(p) * a.stride, a.fixed_len,
@@ -971,9 +874,6 @@ __device__ __forceinline__ void glds2(const void* src, uint32_t lds_base) {
 // arrive by LDS-DMA with the tile of its step (counted in `seq`), so grouping never drains the tile
 // ring.  The launch then zeroes the lag histogram buffer the launch after next accumulates into
 // (three buffers rotate: classify into one, group from the previous one, zero the third).
-#ifndef NBG_LAG_ABL  // diagnostic ablations (wrong results): bit 0 no prologue, bit 1 no pieces in the
-#define NBG_LAG_ABL 0  // unit loop, bit 2 no perm stores
-#endif
 constexpr uint32_t kLagPiece = 64u * kStreamW;  // packets per piece (one 64-packet rank per wave)
 constexpr uint32_t kLagSlots = 3;                // backend pieces per wave: steps k, k+1, k+2
 
@@ -1004,7 +904,6 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   uint32_t* hist_base = reinterpret_cast<uint32_t*>(smem + kLutLds + kStreamW * kRing * kTileLds);
   const uint32_t ring_lds = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t lut_lds = __builtin_amdgcn_readfirstlane(lds_addr(lut));
-  SPROBE(0)
   // Interleaved units: unit u = tiles [u*W, u*W + W), one per wave; block b takes units b, b + G,
   // b + 2G, ...  At any moment the grid reads consecutive units: one sequential sweep of the batch
   // (contiguous per-wave runs read ~3k streams at a fixed stride and measured 10 % slower:
@@ -1061,7 +960,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
   const uint32_t pbeg = g_own ? b * lg.part_pkts : 0u;
   const uint32_t pend = g_own ? min(pbeg + lg.part_pkts, lg.n_pkts) : 0u;
   const uint32_t pieces = g_own && lg.perm ? (pend - pbeg + kLagPiece - 1) / kLagPiece : 0u;
-  const bool pro = !(NBG_LAG_ABL & 1) && g_own && (lg.perm || b == 0);  // block-uniform; counts from block 0
+  const bool pro = g_own && (lg.perm || b == 0);  // block-uniform; counts from block 0
 
   // Prologue loads (GB > 0): this partition's per-bin perm base (group base + prefix over earlier
   // partitions) is summed straight from the pending batch's partition rows (group_kernel's direct
@@ -1083,11 +982,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 
   // LUT staging: lut_lds_bytes (a multiple of 1 KiB, <= 64 KiB) in 1-KiB pieces over the block's
   // waves (the device LUT is padded to whole pieces); the first tiles go out behind them
-#if NBG_SABL == 1  // measurement build: no LUT staging (wrong backends; timing only)
-  const uint32_t pieces_lut = 0;
-#else
   const uint32_t pieces_lut = a.lut_lds_bytes >> 10;
-#endif
   const uint32_t first = min(nt, static_cast<uint32_t>(kRing));
   // the LUT pieces first, then the first tiles (measured: tiles first, or the LUT through registers
   // off the LDS-DMA path, are both ~0.8 us slower per launch)
@@ -1163,12 +1058,10 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       }
     }
   }
-  SPROBE(10)
   // this wave's LUT pieces are in when at most its tile loads are outstanding; then the barrier
   // makes every wave's pieces visible to every wave
   wait_tile(first);
   lds_sync();
-  SPROBE(1)
 
   // Lagged grouping of piece q runs across three barriers, so that every barrier the unit loop already
   // has carries it (sync point s = the loop step, then tail barriers):
@@ -1202,7 +1095,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if (s >= 2 && s - 2 < pieces) {
         const uint32_t q = s - 2, n_q = min(pend - (pbeg + q * kLagPiece), kLagPiece);
         const uint2 e = g_srt[(q & 1u) * kLagPiece + tid];
-        if (!(NBG_LAG_ABL & 4) && tid < n_q && e.x < lg.n_pkts) lg.perm[e.x] = e.y;
+        if (tid < n_q && e.x < lg.n_pkts) lg.perm[e.x] = e.y;
         if (wave * 64u < n_q) ++seq;  // lane 0 stored
       }
       // piece s-1: its sorted slot
@@ -1256,16 +1149,11 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     seek(cur, u);
     const ClassifyArgs& aj = cur.v;
     const uint32_t tb = first_pkt(cur, u);
-#if NBG_SEQWAIT
     wait_vm_n(seq - sA);  // kStreamAhead tiles (and their stores) stay in flight
-#else
-    wait_tile(min(nt - 1u - k, static_cast<uint32_t>(kStreamAhead)));
-#endif
-    SPROBE(2 + k)
     const uint32_t p = tb + lane;
     uint32_t bin = 0;
     bool slow = false;
-    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE, kRow, NBG_STREAM_WT != 0>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
+    const bool valid = tb < aj.n_pkts && stream_classify<F4, MODE, kRow>(aj, lut, ring + (k % kRing) * kTileLds + lane * kRow,
                                                                     p, bin, slow);
     // tile k + kRing into the buffer just read (its ds_reads are consumed above): while the next
     // tile is classified, kStreamAhead tiles stay in flight
@@ -1284,9 +1172,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       if constexpr (HIST) atomicAdd(&hist[(k & 1u) * hstride + bin], 1u);
     }
     if (tb < aj.n_pkts) ++seq;  // the backend store (lane 0 has a packet)
-    if (k == 4) { SPROBE(12) }
-    if (!(NBG_LAG_ABL & 2) && k < pieces) piece_rank(k);
-    if (k == 4) { SPROBE(13) }
+    if (k < pieces) piece_rank(k);
     sA = sB;
     if constexpr (kRing == 2) {
       sB = sN;
@@ -1299,20 +1185,17 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
       // partition row and zeroes it.  The next barrier (unit k + 1) orders that before unit k + 2
       // counts into the same buffer.
       lds_sync();
-      if (k == 4) { SPROBE(14) }
       if (wave == k % kStreamW) {
         uint32_t* h = hist + (k & 1u) * hstride;
         stream_flush<HIST>(aj, h, nbins, ((u - cur.lo) * kStreamW * 64u) / a.part_pkts, lane);
       }
     }
-    if (k == 4) { SPROBE(15) }
-    if (!(NBG_LAG_ABL & 2)) piece_sync(k);
-    if (k == 4) { SPROBE(16) }
+    piece_sync(k);
   }
   if constexpr (GB > 0) {
     // sync points past the unit steps: pieces beyond them (a pending batch larger than this one),
     // then the last two pieces' sorted slots and stores
-    if (!(NBG_LAG_ABL & 2)) {
+    {
       for (uint32_t s = nt; s < pieces + 2; ++s) {
         if (s < pieces) {
           issue_piece(s);
@@ -1325,10 +1208,6 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
     }
     for (uint32_t i = b * kStreamNT + tid; i < lg.zero_words; i += G * kStreamNT) lg.zero[i] = 0;
   }
-#ifdef NBG_SPROBE
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores retired
-#endif
-  SPROBE(11)
 }
 
 // ---- persistent RX-ring classify (nbg_ring_*) ----------------------------------------------------
@@ -1357,12 +1236,6 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_kernel(ClassifyA
 //   waited for tile k (the unit barrier of step k), the stores of steps <= k - 3 retired.  The
 //   control wave then publishes, per block, the count of batches all of whose units of this block
 //   are complete (to uncached HBM, when the count changes); the relay reports the minimum to the host.
-#ifndef NBG_RING_ABL  // measurement builds (tools/build_ab.sh): 1 plain backend stores, 2 none
-#define NBG_RING_ABL 0
-#endif
-#ifndef NBG_RING_WARM  // the control wave's page touches ahead of a batch (0: off, A/B builds)
-#define NBG_RING_WARM 0
-#endif
 constexpr uint32_t kRingCache = 4;  // batch descriptors in LDS (from the current unit's batch on)
 constexpr uint32_t kRingFetch = 2;  // ring slots per prefetch (one LDS-DMA dword load, 32 lanes)
 constexpr uint32_t kRingCtlWords = kRingCache * 16u + kRingFetch * 16u + 4u + kStreamW * 32u + 16u;
@@ -1382,14 +1255,6 @@ __device__ __forceinline__ void glds4_sys(const void* src, uint32_t lds_base) {
 
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-#ifdef NBG_SPROBE  // diagnostic builds: per block [0] prefetches issued, [1] batches taken from them,
-                   // [2] prefetches that took none, [3] idle entries; [4..19] block 0's last failed stage
-__device__ unsigned int g_ringdbg[1024 * 20];
-#define RINGDBG(i, v) \
-  if (lane == 0) g_ringdbg[blockIdx.x * 20 + (i)] += (v);
-#else
-#define RINGDBG(i, v)
-#endif
 
 // The ring kernel's cursor over the known batches (block-uniform; loaded from the LDS descriptor cache)
 struct RingCursor {
@@ -1514,34 +1379,6 @@ __device__ __forceinline__ void ring_relay(const RingArgs& r, uint32_t lane) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) lag = max(lag, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lag), o)));
     const uint32_t c = known - rfl(lag);
-#ifdef NBG_RING_DEBUG  // diagnostic builds: the relay's state in the host ctl line's pad words
-    if (lane == 0) {
-      volatile uint32_t* dbg = r.ctl->pad;
-      dbg[0] = known;
-      dbg[1] = dbg[1] + 1u;
-      dbg[2] = rfl(lag);
-      dbg[3] = __hip_atomic_load(r.prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      dbg[4] = __hip_atomic_load(r.dstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    {  // blocks behind, the first of them
-      uint32_t behind = 0, first = 0xffffffffu;
-      for (uint32_t b = lane; b < r.grid; b += 64u) {
-        const bool lt = __hip_atomic_load(r.prog + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != known;
-        behind += lt ? 1u : 0u;
-        first = lt ? min(first, b) : first;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        behind += static_cast<uint32_t>(__shfl_xor(static_cast<int>(behind), o));
-        first = min(first, static_cast<uint32_t>(__shfl_xor(static_cast<int>(first), o)));
-      }
-      if (lane == 0) {
-        r.ctl->pad[5] = behind;
-        r.ctl->pad[6] = first;
-        r.ctl->pad[7] = r.grid;
-      }
-    }
-#endif
     if (c != done) {
       done = c;
       if (lane == 0) {
@@ -1599,21 +1436,18 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
   uint32_t* stage = cache + kRingCache * 16u;   // [kRingFetch][16] the control wave's prefetch landing area
   uint32_t* known_l = stage + kRingFetch * 16u;  // [2] known batches, by step parity; [2] exit
   uint16_t* rep = reinterpret_cast<uint16_t*>(known_l + 4) + (ctl ? 0u : wave) * 64u;  // a tile wave's 64 backends
-  uint32_t* warm_l = known_l + 4 + kStreamW * 32u;  // [16] landing words of the control wave's page touches
   const uint32_t ring_lds = rfl(lds_addr(ring)), lut_lds = rfl(lds_addr(lut)), stage_lds = rfl(lds_addr(stage));
   if (blockIdx.x == r.grid) {  // the relay block
     if (wave == 0) ring_relay(r, lane);
     return;
   }
   const uint32_t G = r.grid, b = blockIdx.x;
-  if (!ctl) { SPROBE(0) }
   const uint32_t pieces_lut = ctl ? 0u : a.lut_lds_bytes >> 10;
   for (uint32_t q = wave; q < pieces_lut; q += kStreamW)
     glds16(static_cast<const uint8_t*>(a.lut) + q * 1024u + lane * 16u, lut_lds + q * 1024u);
   if (tid < 4) known_l[tid] = 0;
   wait_vm<0>();
   lds_sync();
-  if (!ctl) { SPROBE(1) }
 
   // cursors (every wave keeps them): the unit being classified, and the unit whose tile is issued
   RingCursor cur{0xffffffffu, 0, 0, nullptr, nullptr, 0}, nxt = cur;
@@ -1623,12 +1457,6 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
   // the control wave's descriptor state
   uint32_t known_w = 0, pf_base = 0, last_pf = 0, pub = 0;
   bool pf = false;
-#if NBG_RING_WARM
-  uint32_t warmed = 0xffffffffu;
-  const uint32_t warm_lds = rfl(lds_addr(warm_l));
-#else
-  (void)warm_l;
-#endif
   uint32_t hA = 0xffffffffu, hB = 0xffffffffu, hC = 0xffffffffu;  // batch of the unit of steps k - 1, k - 2, k - 3
   // a step's backends are stored one step late, behind the next tile issue: the wait for a tile then
   // covers the write-through stores of four steps back, not three, so their longer acks stay off the
@@ -1675,7 +1503,6 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
     uint32_t i_ = 0;                                                                                        \
     for (; i_ < kRingFetch && pf_base + i_ == known_w; ++i_)                                                \
       if (!ring_take(stage + i_ * 16u, cache, known_w, (base), lane)) break;                               \
-    RINGDBG(1, known_w - pf_base)                                                                           \
     if (i_ == kRingFetch) pf = false;                                                                       \
   }
 
@@ -1695,7 +1522,6 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
       wait_vm<0>();
       lds_sync();
       if (ctl) {
-        RINGDBG(3, 1)
         const uint32_t base = cur.j == 0xffffffffu ? 0u : cur.j;
         if (pf) {  // landed (vmcnt(0) above)
           RING_TAKE_STAGED(base)
@@ -1723,7 +1549,6 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
         RING_TAKE_STAGED(cur.j)
         if (known_w == kw0 && k - last_pf >= 6u) {
           pf = false;
-          RINGDBG(2, 1)
         }
       }
       if (!pf && known_w - cur.j < kRingCache && known_w - nxt.j <= 2u) {
@@ -1734,37 +1559,10 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
           glds4_sys(reinterpret_cast<const uint32_t*>(ring_slot(r, known_w + lane / 16u)) + (lane & 15u), stage_lds);
         pf = true;
         last_pf = k;
-        RINGDBG(0, 1)
       }
-#if NBG_RING_WARM
-      // address translation ahead of a batch: once the next batch is known, touch the first line of
-      // each of this block's units in it (packets and backend[]), one LDS-DMA dword per lane that no
-      // wave ever waits for, so the page walks happen steps before its tiles are issued (measured:
-      // a batch boundary cost ~2.5 us more than a step without)
-      if (static_cast<int32_t>(nxt.j + 1u - known_w) < 0 && warmed != nxt.j + 1u) {
-        warmed = nxt.j + 1u;
-        RingCursor w;
-        ring_load(w, cache, warmed);
-        const uint64_t first = w.lo + ((b + Gu - w.lo % Gu) % Gu);  // this block's first unit of the batch
-        const uint64_t unit = first + static_cast<uint64_t>(lane & 7u) * Gu;
-        if (lane < 16u && unit < w.hi) {
-          const uint64_t pkt = (unit - w.lo) * kStreamW * 64u;
-          const void* src = lane < 8u ? static_cast<const void*>(w.pkts + pkt * a.stride)
-                                      : static_cast<const void*>(w.backend + pkt);
-          glds4(src, warm_lds);
-        }
-      }
-#endif
       if (lane == 0) known_l[(k + 1u) & 1u] = known_w;
     } else {
-#if NBG_SEQWAIT
       wait_vm_n(seq - sA);
-#else
-      wait_vm<0>();
-#endif
-#ifdef NBG_SPROBE
-      if (k - r.probe_step < 16u) { SPROBE(2 + (k - r.probe_step)) }
-#endif
       ClassifyArgs v = a;
       v.pkts = cur.pkts;
       v.n_pkts = cur.n;
@@ -1781,12 +1579,7 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
         RING_ISSUE(iss, ok)
       }
       if (pend) {  // the previous step's backends
-#if NBG_RING_ABL == 1  // measurement build: plain stores (results not visible at completion)
-        if (lane < 8u) *reinterpret_cast<uint4*>(pp) = pw;
-#elif NBG_RING_ABL == 2  // measurement build: no backend stores
-#else
         if (lane < 8u) stg16_wt(pp, pw);
-#endif
         ++seq;
         pend = false;
       }
@@ -1827,7 +1620,6 @@ __global__ __launch_bounds__(kRingNT, 1) void classify_ring_kernel(ClassifyArgs 
 #undef RING_ISSUE
 #undef RING_PUBLISH
 #undef RING_TAKE_STAGED
-  if (!ctl) { SPROBE(19) }
   // the block's exit, once every wave's stores have retired: a gate kernel waiting for a batch this
   // ring will never complete (stop, idle exit) returns when every classify block has exited
   wait_vm<0>();
@@ -1892,9 +1684,6 @@ struct DescTile {
   uint32_t r0, r1, r2;  // records: the swapped MAC words
 };
 
-#ifndef NBG_DABL  // diagnostic ablations (wrong results): 1 no gathers, 2 no packet loads, 3 both
-#define NBG_DABL 0
-#endif
 
 // LUTM: kLdsU8Tail (u8 LUT staged in LDS) or kGlobalU16 (u16 LUT gathered from L2).
 // MODE: 0 = read only (always with CHAIN), 1 = in place (whole owned windows), 2 = 12-B records.
@@ -1903,7 +1692,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
   constexpr uint32_t kRow = row_of<MODE>(), kTileLds = 64u * kRow;
   constexpr uint32_t kLut = LUTM == kLdsU8Tail ? kLutLds : 0u;
   constexpr uint32_t kPR = desc_ring_tiles<MODE>();
-  constexpr bool kG = (CHAIN || LUTM == kGlobalU16) && !(NBG_DABL & 1);  // one 2-B gather per packet
+  constexpr bool kG = (CHAIN || LUTM == kGlobalU16) ;  // one 2-B gather per packet
   // store instructions per tile (a lower bound: the compiler may not split them further)
   constexpr uint32_t kS = 1u + (CHAIN ? 1u : 0u) + (MODE == 1 ? 4u : 0u) + (MODE == 2 ? 1u : 0u);
   extern __shared__ __align__(16) uint8_t smem[];
@@ -1953,7 +1742,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
     const uint32_t* o = doff(k);
     const uint32_t buf = ring_lds + (k % kPR) * kTileLds;
     const uint32_t tb = tile_of(k) * 64u;
-    if ((kCh == 4u || lane < 16u * kCh) && !(NBG_DABL & 2)) {
+    if (kCh == 4u || lane < 16u * kCh) {
       const uint32_t pk = lane / kCh, ch = lane - pk * kCh;
       uint32_t off[4];
 #pragma unroll
@@ -1965,7 +1754,7 @@ __global__ __launch_bounds__(kStreamNT, 1) void classify_stream_desc_kernel(Clas
         glds16_tile<MODE != 2>(src, buf + j * (16u * kRow));
       }
     }
-    if (!(NBG_DABL & 2)) seq += 4;
+    seq += 4;
     return seq;
   };
   // hash step k's packets (landed) and issue their gather; returns the count after the gather
@@ -2451,26 +2240,13 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
 // reduced here from the partition histograms staged in LDS, or read from scan_kernel's
 // output.  Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local
 // counting sort in LDS and coalesced perm stores.
-#ifdef NBG_GPROBE  // diagnostic build: phase timestamps of three blocks, printed at exit
-#define GPROBE(k)                                                                          \
-  if (tid == 0 && (c == 0 || c == gridDim.x / 2 || c == gridDim.x - 1)) gpt[k] = wall_clock64();
-#else
-#define GPROBE(k)
-#endif
-#ifndef NBG_GABL  // diagnostic ablations (wrong results): bit 0 no partition-row reads, bit 1 no
-#define NBG_GABL 0  // multisplit ballots, bit 2 no perm stores
-#endif
-#ifndef NBG_GROUP_WAVES
-#define NBG_GROUP_WAVES 4  // waves per SIMD the group kernel is compiled for: <= 64 VGPRs, so a resident
-                           // group block leaves the other streams' classify waves their registers
-#endif
+// 4 waves per SIMD: the group kernel is compiled for <= 64 VGPRs, so a resident group block leaves
+// the other streams' classify waves their registers
+constexpr int kGroupWaves = 4;
 // BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
 template <int SCAN, int BITS>
 // Blocks [j * gm.per, j * gm.per + g[j].n_parts) group batch j (a single batch: j = 0, c = blockIdx.x).
-__global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMulti gm) {
-#ifdef NBG_GPROBE
-  uint64_t gpt[12] = {};
-#endif
+__global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti gm) {
   extern __shared__ __align__(16) uint32_t gs[];
   __shared__ uint32_t s_wave[kGBlock / 64];
   constexpr uint32_t kW = kGBlock / 64;  // waves
@@ -2489,13 +2265,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
     zero_next();
     return;
   }
-  GPROBE(0)
-#ifdef NBG_GROUP_EMPTY  // measurement build: the launch and its stream boundary only
-  return;
-#endif
-#ifdef NBG_GROUP_PRIO  // experiment: the latency-bound group waves ahead of other streams' classify
-  __builtin_amdgcn_s_setprio(NBG_GROUP_PRIO);
-#endif
   const uint32_t nbp = (nbins + 3) & ~3u;
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
   uint32_t* tot = base + nbp;          // [nbins]
@@ -2517,15 +2286,12 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) pre_bin[r] = ld_u16(a.backend, min(wb + r * 64u + lane, a.n_pkts - 1u) * 2u);
   }
-  GPROBE(1)
   // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
   for (uint32_t b = tid; b < nbins; b += kGBlock) {
     base[b] = 0;
     tot[b] = 0;
   }
-  if constexpr (SCAN == kScanDirect && (NBG_GABL & 1)) {
-    lds_sync();
-  } else if constexpr (SCAN == kScanDirect) {
+  if constexpr (SCAN == kScanDirect) {
     lds_sync();
     // L threads per row word, each summing a strided subset of the partition rows straight from
     // L2 (consecutive threads read consecutive words of one row: coalesced)
@@ -2619,7 +2385,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       tot[b] = a.totals[b];
     }
   }
-  GPROBE(2)
   lds_sync();
   // group bases (exclusive scan of the totals over bins).  Loops have compile-time trip counts
   // (bins < 2^BITS) so that their LDS reads issue back to back.
@@ -2666,7 +2431,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
     }
   }
   lds_sync();
-  GPROBE(3)
   if (!a.perm) {
     zero_next();
     return;
@@ -2681,7 +2445,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
 #pragma unroll
     for (uint32_t k = 0; k < (kMaxBins + 8 + 511) / 512; ++k)
       if ((lane + k * 64) * 8 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
-    GPROBE(9)
     uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
@@ -2693,7 +2456,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       const uint32_t mv = valid ? ~0u : 0u;
       const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
       uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
-#if !(NBG_GABL & 2)
 #pragma unroll
       for (int bit = 0; bit < BITS; ++bit) {
         const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
@@ -2701,10 +2463,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
         elo &= ~(static_cast<uint32_t>(bb) ^ m);
         ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
       }
-#else  // every lane alone: counts under-counted, so every perm index stays inside its bin's range
-      elo &= lane < 32 ? 1u << lane : 0u;
-      ehi &= lane >= 32 ? 1u << (lane - 32) : 0u;
-#endif
       // every lane of a bin stores the same new count (no branch); lanes past the end use the
       // scratch slot
       const uint32_t slot = valid ? bin : nbins;
@@ -2713,7 +2471,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       const uint32_t rank = prior + __popc(elo & lt_lo) + __popc(ehi & lt_hi);
       br[r] = valid ? (rank << 16) | bin : 0xffffffffu;
     }
-    GPROBE(10)
     // the next chunk's backends (partitions of more than one chunk): loaded now, behind this
     // chunk's scans and stores
     if (cbase + kChunk < pend) {
@@ -2722,7 +2479,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
         pre_bin[r] = ld_u16(a.backend, min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u) * 2u);
     }
     lds_sync();
-    GPROBE(4)
     // one exclusive scan over the counters in bin-major order (bin, wave): the chunk-local slot
     // where wave w's packets of bin b start
     // (each thread owns kPer consecutive elements: whole bins' wave counters when kPer >= kW)
@@ -2744,7 +2500,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       x += ev[k];
     }
     lds_sync();
-    GPROBE(5)
     // per bin: perm position of chunk slot j of bin b = tot[b] + j; advance past the bin
     for (uint32_t b = tid; b < nbins; b += kGBlock) {
       const uint32_t st = cnt[b];                                // wave 0's start = the bin's start
@@ -2752,7 +2507,6 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       tot[b] = base[b] - st;
       base[b] += en - st;
     }
-    GPROBE(6)
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       if (br[r] != 0xffffffffu) {
@@ -2762,51 +2516,24 @@ __global__ __launch_bounds__(kGBlock, NBG_GROUP_WAVES) void group_kernel(GroupMu
       }
     }
     lds_sync();
-    GPROBE(7)
     // coalesced output: consecutive sorted slots of one bin are consecutive perm entries.  The
     // next chunk's first writes to sidx/sbin/tot come after the barriers of its scan.
     for (uint32_t j = tid; j < ctotal; j += kGBlock) {
-#ifdef NBG_GUARD  // diagnostic build: a store whose slot comes from inconsistent histograms is dropped
-      if (tot[sslot[j] >> 12] + j >= a.n_pkts) continue;
-#endif
-#if !(NBG_GABL & 4)
       const uint32_t sv = sslot[j];
       a.perm[tot[sv >> 12] + j] = cbase + (sv & 0xfffu);
-#else
-      if (sslot[j] == 0xffffffffu) a.perm[0] = tot[sslot[j] >> 12];
-#endif
     }
   }
   zero_next();
-  GPROBE(8)
-#ifdef NBG_GPROBE
-  if (tid == 0 && (c == 0 || c == gridDim.x / 2 || c == gridDim.x - 1))
-    printf("GPROBE blk %u split %llu %llu %llu t0 %llu d: %llu %llu %llu %llu %llu %llu %llu %llu\n", c,
-           (unsigned long long)(gpt[9] - gpt[3]), (unsigned long long)(gpt[10] - gpt[9]),
-           (unsigned long long)(gpt[4] - gpt[10]), (unsigned long long)gpt[0],
-           (unsigned long long)(gpt[1] - gpt[0]), (unsigned long long)(gpt[2] - gpt[1]),
-           (unsigned long long)(gpt[3] - gpt[2]), (unsigned long long)(gpt[4] - gpt[3]),
-           (unsigned long long)(gpt[5] - gpt[4]), (unsigned long long)(gpt[6] - gpt[5]),
-           (unsigned long long)(gpt[7] - gpt[6]), (unsigned long long)(gpt[8] - gpt[7]));
-#endif
 }
 
 template <int LUTM, bool F4, bool HIST, bool CHAIN>
 int launch_one(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   constexpr int NT = (LUTM == kLdsU8 || LUTM == kLdsU16) ? kLdsBlock : kBlock;
-  auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, kDesc, 0, NT>
-                  : (a.lean ? classify_kernel<LUTM, F4, HIST, CHAIN, kLean, 0, NT>
-                            : classify_kernel<LUTM, F4, HIST, CHAIN, kFixed, 0, NT>);
+  auto fn = a.off ? classify_kernel<LUTM, F4, HIST, CHAIN, kDesc, NT>
+                  : (a.lean ? classify_kernel<LUTM, F4, HIST, CHAIN, kLean, NT>
+                            : classify_kernel<LUTM, F4, HIST, CHAIN, kFixed, NT>);
 
   hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), lds, s, a);
-  const hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
-  return NBG_OK;
-}
-
-template <int LUTM, bool F4, bool HIST, int ABL>
-int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL((classify_kernel<LUTM, F4, HIST, false, kLean, ABL>), dim3(grid), dim3(kBlock), lds, s, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "classify launch: %s", hipGetErrorString(e));
   return NBG_OK;
@@ -2815,15 +2542,6 @@ int launch_abl(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
 template <int LUTM, bool F4, bool HIST>
 int launch_v(const ClassifyArgs& a, int grid, size_t lds, hipStream_t s) {
   if (a.tbl24) return launch_one<LUTM, F4, HIST, true>(a, grid, lds, s);
-  if constexpr (LUTM == kGlobalU8 && F4 && !HIST) {
-    static const int abl = [] {
-      const char* e = std::getenv("NBG_ABL");
-      return e ? std::atoi(e) : 0;
-    }();
-    if (a.lean && abl == 1) return launch_abl<LUTM, F4, HIST, 1>(a, grid, lds, s);
-    if (a.lean && abl == 3) return launch_abl<LUTM, F4, HIST, 3>(a, grid, lds, s);
-    if (a.lean && abl == 4) return launch_abl<LUTM, F4, HIST, 4>(a, grid, lds, s);
-  }
   return launch_one<LUTM, F4, HIST, false>(a, grid, lds, s);
 }
 
@@ -2971,12 +2689,8 @@ size_t ring_lds(int mode) {
 
 int launch_classify_ring(const ClassifyArgs& a, const RingArgs& r, int mode, int grid, void* stream) {
   const bool f4 = a.m == 65537u;
-#ifdef NBG_RING_ONE
-  auto fn = classify_ring_kernel<true, 0>;
-#else
   auto fn = mode == 1 ? (f4 ? classify_ring_kernel<true, 1> : classify_ring_kernel<false, 1>)
                       : (f4 ? classify_ring_kernel<true, 0> : classify_ring_kernel<false, 0>);
-#endif
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
       hipSuccess)
     return set_error(NBG_EIO, "ring classify: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
@@ -3223,16 +2937,10 @@ int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
   }();
   if (forced == kScanKernel || forced == kScanDirect) return forced;
   if (forced == kScanLds && group_lds(nbins, n_parts, kScanLds) <= 100 * 1024) return kScanLds;
-#ifndef NBG_SCAN_DIRECT_MAX
-#define NBG_SCAN_DIRECT_MAX (32 * 1024)
-#endif
-  return static_cast<size_t>(nbins) * n_parts <= NBG_SCAN_DIRECT_MAX ? kScanDirect : kScanKernel;
+  return static_cast<size_t>(nbins) * n_parts <= 32u * 1024u ? kScanDirect : kScanKernel;
 }
 
 int launch_group(const GroupArgs& a, int scan, void* stream) {
-#ifdef NBG_SKIP_GROUP_LAUNCH  // measurement build: classify + histograms only
-  return 0;
-#endif
   const size_t lds = group_lds(a.nb + 1, a.n_parts, scan);
   auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7>
                                                 : (scan == kScanLds ? group_kernel<kScanLds, 7> : group_kernel<kScanKernel, 7>))
@@ -3285,27 +2993,6 @@ int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int
 }
 
 }  // namespace nbg
-
-#ifdef NBG_SPROBE
-// Diagnostic builds only (not part of include/nbgpu.h): the streaming kernel's per-wave timestamps.
-extern "C" int nbg_debug_sprobe(unsigned long long* out, uint64_t n) {
-  if (n > nbg::kSProbeWaves * nbg::kSProbeSlots) n = nbg::kSProbeWaves * nbg::kSProbeSlots;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_sprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
-}
-#endif
-#ifdef NBG_SPROBE
-extern "C" int nbg_debug_ringdbg(unsigned int* out, uint64_t n) {
-  if (n > 1024 * 20) n = 1024 * 20;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_ringdbg), n * 4) == hipSuccess ? 0 : NBG_EIO;
-}
-#endif
-#ifdef NBG_CPROBE
-// Diagnostic builds only (not part of include/nbgpu.h): the per-wave timestamps of the last launch.
-extern "C" int nbg_debug_cprobe(unsigned long long* out, uint64_t n) {
-  if (n > nbg::kProbeWaves * 4) n = nbg::kProbeWaves * 4;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(nbg::g_cprobe), n * 8) == hipSuccess ? 0 : NBG_EIO;
-}
-#endif
 
 // Diagnostics (not in include/nbgpu.h; tests only): `blocks` one-wave workgroups that each hold
 // `lds_bytes` of a CU's LDS for `us` microseconds (100 MHz wall clock; every wave exits by time) —

@@ -578,18 +578,10 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
 namespace {
 
 // The partition rows of a captured call are zeroed inside the graph, by a kernel node.  A memset node
-// (NBG_CAPTURE_ZERO_KERNEL=0, kept for the record) faults on its second replay when the graph is
-// launched on the legacy null stream under PyTorch's bundled HIP 7.0 runtime, as torch.cuda.graph
-// replays do by default; the image's HIP 7.2 replays it clean, and so does HIP 7.0 on a created
-// stream (DESIGN.md §4 "hipGraph capture", profiles/r03_graph_*.txt).
-int zero_captured(uint32_t* p, size_t words, void* stream) {
-#if NBG_CAPTURE_ZERO_KERNEL
-  return launch_zero(p, words, stream);
-#else
-  NBG_HIP(hipMemsetAsync(p, 0, words * 4, static_cast<hipStream_t>(stream)));
-  return NBG_OK;
-#endif
-}
+// faults on its second replay when the graph is launched on the legacy null stream under PyTorch's
+// bundled HIP 7.0 runtime, as torch.cuda.graph replays do by default; the image's HIP 7.2 replays it
+// clean, and so does HIP 7.0 on a created stream (profiles/DESIGN_r01-r03_history.md, r03_graph_*.txt).
+int zero_captured(uint32_t* p, size_t words, void* stream) { return launch_zero(p, words, stream); }
 
 // The pending lagged group (NBG_GROUP_LAG) as a group launch of its own on `s` (already ordered
 // after the handle's last launch).  Its rows live in the lag set it was classified into; the
@@ -1380,6 +1372,7 @@ struct nbg_ring {
   // (the ended kernel makes each return) before it closes the queues or frees anything
   uint32_t calls = 0;
   bool leaked = false;                 // the kernel did not end at stop: every call returns NBG_EBUSY
+  bool stopping = false;               // nbg_ring_stop has begun: posts are refused
   hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
   hipEvent_t ev_start = nullptr, ev_end = nullptr;  // around the kernel on `stream` (its duration)
   size_t hbytes = 0, dbytes = 0;       // the pinned host ring and the uncached device ring
@@ -1626,6 +1619,7 @@ int ring_post_one(nbg_ring* r, nbg_ring_queue* q, uint8_t* d_pkts, uint64_t n_pk
       std::lock_guard<std::mutex> g(r->mu);
       if (r->leaked) return ring_leaked_error();
       if (q && q->closed) return set_error(NBG_EINVAL, "ring_queue_post: the queue was closed by nbg_ring_stop");
+      if (r->stopping) return set_error(NBG_EINVAL, "ring_post: the ring is stopping");
       ring_refresh(r);
       if (ring_gone(r)) return ring_state_error(r);
       if (r->posted - r->completed < r->slots) {
@@ -1876,6 +1870,7 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   r->moved = Clock::now();
   r->posted = r->units = r->completed = 0;
   r->ended = false;
+  r->stopping = false;
   r->rec.assign(r->slots, {nullptr, 0});
   std::memset(r->host, 0, r->hbytes);
   {
@@ -1921,8 +1916,6 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   ra.reps = r->reps;
   ra.grid = static_cast<uint32_t>(r->grid);
   ra.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
-  const char* ps = std::getenv("NBG_RING_PROBE_STEP");  // NBG_SPROBE builds only
-  ra.probe_step = ps ? static_cast<uint32_t>(std::atoi(ps)) : 0u;
   (void)hipEventRecord(r->ev_start, r->stream);
   if ((rc = launch_classify_ring(a, ra, a.swap ? 1 : 0, r->grid + 1, r->stream))) {
     ring_free(r);
@@ -1950,6 +1943,7 @@ int nbg_ring_post_burst(nbg_ring* r, const nbg_ring_batch* batches, uint32_t n_b
   }
   std::lock_guard<std::mutex> g(r->mu);
   if (r->leaked) return ring_leaked_error();
+  if (r->stopping) return set_error(NBG_EINVAL, "ring_post_burst: the ring is stopping");
   *first_ticket = r->posted;
   ring_refresh(r);
   if (ring_gone(r)) return ring_state_error(r);
@@ -2021,6 +2015,7 @@ int nbg_ring_stop(nbg_ring* r) {
   std::unique_lock<std::mutex> lk(r->mu);
   if (r->leaked) return ring_leaked_error();
   DeviceGuard g(r->device);
+  r->stopping = true;  // the lock is released while the kernel drains: no post may follow the stop word
   __atomic_store_n(&const_cast<RingCtl*>(const_cast<volatile RingCtl*>(r->ctl))->stop, 1u, __ATOMIC_RELEASE);
   const auto t0 = Clock::now();
   int rc = NBG_OK;

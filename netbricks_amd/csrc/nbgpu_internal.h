@@ -7,10 +7,6 @@
 
 #include "../../include/nbgpu.h"
 
-#ifndef NBG_CAPTURE_ZERO_KERNEL  // 0: memset nodes in captured calls (the HIP 7.0 null-stream fault)
-#define NBG_CAPTURE_ZERO_KERNEL 1
-#endif
-
 namespace nbg {
 
 // Thread-local last-error string (nbg_last_error); returns `code` for chaining.
@@ -27,23 +23,11 @@ constexpr int kBlock = 256;          // classify threads per workgroup (4 waves)
 constexpr int kLdsBlock = 1024;      // classify threads per workgroup with the LDS-staged LUT (1 per CU)
 constexpr int kXStride = 48;         // LDS bytes per packet in the transpose: chunks 0..2 (a 12-dword row
                                      // stride keeps the b128 reads conflict-free; 8 blocks fit per CU)
-#ifndef NBG_LOAD_PRIO
-#define NBG_LOAD_PRIO 3
-#endif
-constexpr int kLoadPrio = NBG_LOAD_PRIO;  // s_setprio while a classify wave issues its tile loads
-#ifndef NBG_GBLOCK
-#define NBG_GBLOCK 512
-#endif
-constexpr int kGBlock = NBG_GBLOCK;  // group kernel threads per workgroup (8 waves: overlaps classify better)
-#ifndef NBG_KCHUNK  // measurement builds only (tools/build_ab.sh): group-kernel chunk size
-#define NBG_KCHUNK 4096
-#endif
-#ifndef NBG_KMAXPARTS
-#define NBG_KMAXPARTS 256
-#endif
-constexpr int kChunk = NBG_KCHUNK;   // packets per group-kernel chunk
+constexpr int kLoadPrio = 3;         // s_setprio while a classify wave issues its tile loads
+constexpr int kGBlock = 512;         // group kernel threads per workgroup (8 waves: overlaps classify better)
+constexpr int kChunk = 4096;         // packets per group-kernel chunk
 constexpr int kGRounds = kChunk / kGBlock;  // group kernel rounds of 64 packets per wave per chunk
-constexpr uint32_t kMaxParts = NBG_KMAXPARTS;  // partitions per batch (part_pkts is a multiple of kChunk)
+constexpr uint32_t kMaxParts = 256;  // partitions per batch (part_pkts is a multiple of kChunk)
 constexpr uint32_t kMaxGroupBins = 1024;  // multisplit group kernel: n_backends + 1 <= 1024
 constexpr uint32_t kMaxWideBins = 32768;  // wide grouping path: n_backends <= 32767 (LUT sentinel bound,
                                           // test/maglev/src/nf.rs:46)
@@ -144,7 +128,6 @@ struct RingArgs {
   uint32_t slots;         // power of two
   uint32_t reps;          // power of two: replicas of the device ring
   uint32_t grid;          // classify blocks (block `grid` is the relay)
-  uint32_t probe_step;    // NBG_SPROBE builds: the first of the 16 unit steps recorded
   uint64_t idle_ticks;    // exit after this long (100 MHz wall clock) without a new batch
 };
 #ifdef __HIPCC__
