@@ -2235,11 +2235,11 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
   }
 }
 
-// One 1024-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
+// One 512-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
 // Prologue: prefix of this partition over earlier partitions and the group bases, either
-// reduced here from the partition histograms staged in LDS, or read from scan_kernel's
-// output.  Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local
-// counting sort in LDS and coalesced perm stores.
+// summed here from the L2-resident partition histograms, or read from scan_kernel's output.
+// Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local counting sort
+// in LDS and coalesced perm stores.
 // 4 waves per SIMD: the group kernel is compiled for <= 64 VGPRs, so a resident group block leaves
 // the other streams' classify waves their registers
 constexpr int kGroupWaves = 4;
@@ -2275,7 +2275,6 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   const uint32_t cst = (nbins + 8) & ~7u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
   uint16_t* cnt = reinterpret_cast<uint16_t*>(tot + nbp);  // [kW][cst]
   uint32_t* sslot = reinterpret_cast<uint32_t*>(cnt + kW * cst);  // [kChunk]
-  uint32_t* ph = sslot + kChunk;       // [n_parts][nbins] (kScanLds)
 
   // ---- the first chunk's backends are loaded up front: their latency overlaps the prologue
   const uint32_t pbeg = c * a.part_pkts;
@@ -2345,38 +2344,6 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       if (pre) atomicAdd(&base[b], pre);
       if (all) atomicAdd(&tot[b], all);
     }
-    }
-  } else if constexpr (SCAN == kScanLds) {
-    // stage the partition histograms: every load issued before any LDS store (one round trip)
-    const uint32_t words = a.n_parts * nbins;
-    constexpr int kStage = 8;  // 8 x 1024 x 16 B = 128 KiB >= the kScanLds limit
-    const uint32_t nvec = words / 4;
-    const uint4* src = reinterpret_cast<const uint4*>(a.part_hist);
-    uint4 tmp[kStage];
-#pragma unroll
-    for (int k = 0; k < kStage; ++k) {
-      const uint32_t v = tid + k * kGBlock;
-      tmp[k] = v < nvec ? src[v] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < kStage; ++k) {
-      const uint32_t v = tid + k * kGBlock;
-      if (v < nvec) reinterpret_cast<uint4*>(ph)[v] = tmp[k];
-    }
-    for (uint32_t i = nvec * 4 + tid; i < words; i += kGBlock) ph[i] = a.part_hist[i];
-    lds_sync();
-    // L threads per bin, each summing a strided subset of the partitions
-    const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
-    for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
-      const uint32_t b = t / L, j = t - b * L;
-      uint32_t pre = 0, all = 0;
-      for (uint32_t q = j; q < a.n_parts; q += L) {
-        const uint32_t h = ph[q * nbins + b];
-        pre += q < c ? h : 0u;
-        all += h;
-      }
-      if (pre) atomicAdd(&base[b], pre);
-      if (all) atomicAdd(&tot[b], all);
     }
   } else {
     lds_sync();
@@ -2522,6 +2489,264 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       const uint32_t sv = sslot[j];
       a.perm[tot[sv >> 12] + j] = cbase + (sv & 0xfffu);
     }
+  }
+  zero_next();
+}
+
+// group_direct_kernel: the compact form of group_kernel, for many bins beside an in-place
+// persistent ring (whose blocks leave ~30 KB of a CU's LDS; group_kernel takes 40 KB at 1001 bins
+// and would wait for the ring to end).  Same grid, arguments and outputs.  One 512-thread block per
+// partition (part_pkts packets, processed in 4096-packet chunks): the stable per-group FIFO order
+// of group_by.rs:46-51.  Wave w owns the contiguous 512-packet segment [512w, 512w + 512) of every
+// chunk, 8 rounds of 64 packets.
+//   Ranks: per round a ballot multisplit (one ballot per bin bit) gives every lane its rank among
+//     the round's lanes of its bin; the wave's LDS counter row (16 bit per bin) carries the counts
+//     of its earlier rounds.  The first chunk is ranked while the prologue's loads are in flight.
+//   Prologue: this partition's prefix over earlier partitions and the bin totals, summed from the
+//     L2-resident partition rows (few bins) or read from scan_kernel's output; group bases (an
+//     exclusive scan of the totals over bins) give run[b], the perm position of the partition's
+//     first packet of bin b.
+//   Per chunk, one pass over the bins turns each bin's 8 wave counts into exclusive prefixes (and
+//     advances run[] past the chunk), then every lane stores perm[run[b] + prefix[w][b] + rank] =
+//     its packet directly, without the local sort (measured 1-2 us per 1M batch slower than
+//     group_kernel's coalesced stores: profiles/r05_group_ab.txt).
+// LDS: run[2][nbins] + tot[nbins] u32, cnt[8][nbins] u16: 28 KB at 1001 bins.
+template <int SCAN, int BITS>
+__global__ __launch_bounds__(kGBlock, kGroupWaves) void group_direct_kernel(GroupMulti gm) {
+  extern __shared__ __align__(16) uint32_t gs[];
+  __shared__ uint32_t s_wave[kGBlock / 64];
+  constexpr uint32_t kW = kGBlock / 64;  // waves
+  static_assert(kChunk == kGBlock * kGRounds && kChunk / kW <= 65535, "16-bit per-wave counters");
+  const uint32_t bj = blockIdx.x / gm.per;
+  const GroupArgs a = gm.g[bj];
+  const uint32_t nbins = a.nb + 1;
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+  const uint32_t c = blockIdx.x - bj * gm.per;  // partition of batch bj
+  // The next call accumulates into the other histogram buffer: every block of the grid zeroes a
+  // slice of it, last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the
+  // first wait for a backend load would also wait for them (the counter retires in issue order).
+  auto zero_next = [&] {
+    for (uint32_t i = blockIdx.x * kGBlock + tid; i < a.next_words; i += gridDim.x * kGBlock) a.part_hist_next[i] = 0;
+  };
+  if (c >= a.n_parts) {  // a smaller batch of a multi-batch launch
+    zero_next();
+    return;
+  }
+  const uint32_t nbp = (nbins + 3) & ~3u;
+  const uint32_t cst = (nbins + 8) & ~7u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
+  uint32_t* run = gs;                      // [2][nbp] by chunk parity
+  uint32_t* tot = run + 2 * nbp;           // [nbp] bin totals (prologue)
+  uint16_t* cnt = reinterpret_cast<uint16_t*>(tot + nbp);  // [kW][cst]
+  uint16_t* mycnt = cnt + wave * cst;
+  constexpr uint32_t kMaxBins = 1u << BITS;
+
+  // ---- the first chunk's backends, then the prologue's loads: all in flight together
+  const uint32_t pbeg = c * a.part_pkts;
+  const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
+  uint32_t pre_bin[kGRounds];
+  {
+    const uint32_t wb = pbeg + wave * (64u * kGRounds);
+#pragma unroll
+    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = ld_u16(a.backend, min(wb + r * 64u + lane, a.n_pkts - 1u) * 2u);
+  }
+  // kScanDirect: L threads per row word, each summing a strided subset of the partition rows (its
+  // first kU rows loaded here); kScanKernel: this partition's prefix row and the totals
+  constexpr uint32_t kU = 24;
+  const uint32_t hw = a.hist16 ? (nbins + 1) >> 1 : nbins;  // row words
+  const uint32_t L = hw >= kGBlock ? 1u : kGBlock / hw;
+  uint32_t h[kU];
+  constexpr uint32_t kCh = (kMaxBins + kGBlock - 1) / kGBlock;
+  uint32_t pk[kCh], tk[kCh];
+  auto load_rows = [&](uint32_t t, uint32_t q0) {
+#pragma unroll
+    for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * hw + t % hw) * 4u);
+  };
+  if constexpr (SCAN == kScanDirect) {
+    if (tid < hw * L) load_rows(tid, tid / hw);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kCh; ++k) {
+      const uint32_t b = min(tid + k * kGBlock, nbins - 1u);
+      pk[k] = a.part_prefix[static_cast<size_t>(c) * nbins + b];
+      tk[k] = a.totals[b];
+    }
+  }
+
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
+  uint32_t br[kGRounds];  // rank << 16 | bin, or ~0 past the end
+  // one chunk's ranks (its backends in pre_bin); afterwards the next chunk's backends are loaded
+  auto rank_chunk = [&](uint32_t cbase) {
+#pragma unroll
+    for (uint32_t k = 0; k < (kMaxBins + 8 + 511) / 512; ++k)
+      if ((lane + k * 64) * 8 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
+    const uint32_t wbase = cbase + wave * (64u * kGRounds);
+#pragma unroll
+    for (int r = 0; r < kGRounds; ++r) {
+      const uint32_t i = wbase + r * 64u + lane;
+      const bool valid = i < pend;
+      const uint32_t bin = min(pre_bin[r], a.nb);  // the sentinel (and any value > nb, as in hist_kernel)
+      // lanes with my bin (and my validity): per bit, keep the lanes whose ballot bit equals mine
+      const uint32_t mv = valid ? ~0u : 0u;
+      const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
+      uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
+#pragma unroll
+      for (int bit = 0; bit < BITS; ++bit) {
+        const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
+        const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
+        elo &= ~(static_cast<uint32_t>(bb) ^ m);
+        ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
+      }
+      // every lane of a bin stores the same new count (no branch); lanes past the end use the
+      // scratch slot
+      const uint32_t slot = valid ? bin : nbins;
+      const uint32_t prior = mycnt[slot];
+      mycnt[slot] = static_cast<uint16_t>(prior + __popc(elo) + __popc(ehi));
+      const uint32_t rank = prior + __popc(elo & lt_lo) + __popc(ehi & lt_hi);
+      br[r] = valid ? (rank << 16) | bin : 0xffffffffu;
+    }
+    if (cbase + kChunk < pend) {
+#pragma unroll
+      for (int r = 0; r < kGRounds; ++r)
+        pre_bin[r] = ld_u16(a.backend, min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u) * 2u);
+    }
+  };
+  if (a.perm) rank_chunk(pbeg);
+
+  // ---- prologue: per-bin prefix over earlier partitions (run[0]) and totals
+  if constexpr (SCAN == kScanDirect) {
+    for (uint32_t b = tid; b < nbp; b += kGBlock) {
+      run[b] = 0;
+      tot[b] = 0;
+    }
+    lds_sync();
+    // the first (thread, word) pair's rows are loaded already; more than kGBlock row words (many bins,
+    // 16-bit rows off) take further pairs
+    for (uint32_t t = tid; t < hw * L; t += kGBlock) {
+      const uint32_t w = t % hw, j = t / hw;
+      if (t != tid) load_rows(t, j);
+      uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
+      for (uint32_t q0 = j;;) {
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+          const uint32_t q = q0 + k * L;
+          const uint32_t lo = q < a.n_parts ? (a.hist16 ? h[k] & 0xffffu : h[k]) : 0u;
+          const uint32_t hi = q < a.n_parts && a.hist16 ? h[k] >> 16 : 0u;
+          all_lo += lo;
+          all_hi += hi;
+          pre_lo += q < c ? lo : 0u;
+          pre_hi += q < c ? hi : 0u;
+        }
+        q0 += kU * L;
+        if (q0 >= a.n_parts) break;
+        load_rows(t, q0);
+      }
+      const uint32_t b0 = a.hist16 ? 2 * w : w;
+      if (pre_lo) atomicAdd(&run[b0], pre_lo);
+      if (all_lo) atomicAdd(&tot[b0], all_lo);
+      if (a.hist16 && b0 + 1 < nbins) {
+        if (pre_hi) atomicAdd(&run[b0 + 1], pre_hi);
+        if (all_hi) atomicAdd(&tot[b0 + 1], all_hi);
+      }
+    }
+    lds_sync();
+  }
+  // group bases: an exclusive scan of the totals over bins.  Loops have compile-time trip counts
+  // (bins < 2^BITS) so that their LDS reads issue back to back.
+  if constexpr (SCAN == kScanDirect && kMaxBins <= 128) {  // one wave, <= 2 bins per lane
+    if (wave == 0) {
+      uint32_t t2[2], s = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        t2[k] = b < nbins ? tot[b] : 0u;
+        s += t2[k];
+      }
+      uint32_t gb = wave_incl_scan(s) - s;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        if (b < nbins) {
+          if (c == 0 && a.counts) a.counts[b] = t2[k];
+          run[b] += gb;  // group base + prefix over earlier partitions
+        }
+        gb += t2[k];
+      }
+    }
+  } else {  // the whole block; bin b = tid + k * kGBlock... scanned in thread-major order below
+    constexpr uint32_t kCb = (kMaxBins + kGBlock - 1) / kGBlock;  // consecutive bins per thread
+    uint32_t tb[kCb], pb[kCb], s = 0;
+    if constexpr (SCAN == kScanDirect) {
+#pragma unroll
+      for (uint32_t k = 0; k < kCb; ++k) {
+        const uint32_t b = tid * kCb + k;
+        tb[k] = b < nbins ? tot[b] : 0u;
+        pb[k] = b < nbins ? run[b] : 0u;
+      }
+    } else {  // this thread's loaded bins (tid + k * kGBlock) to consecutive ones through LDS
+#pragma unroll
+      for (uint32_t k = 0; k < kCh; ++k) {
+        const uint32_t b = tid + k * kGBlock;
+        if (b < nbins) {
+          run[b] = pk[k];
+          tot[b] = tk[k];
+        }
+      }
+      lds_sync();
+#pragma unroll
+      for (uint32_t k = 0; k < kCb; ++k) {
+        const uint32_t b = tid * kCb + k;
+        tb[k] = b < nbins ? tot[b] : 0u;
+        pb[k] = b < nbins ? run[b] : 0u;
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) s += tb[k];
+    uint32_t all;
+    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave, all);
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) {
+      const uint32_t b = tid * kCb + k;
+      if (b < nbins) {
+        if (c == 0 && a.counts) a.counts[b] = tb[k];
+        run[b] = pb[k] + gb;
+      }
+      gb += tb[k];
+    }
+  }
+  if (!a.perm) {
+    zero_next();
+    return;
+  }
+
+  // ---- per chunk: wave prefixes per bin, then the stores (the first chunk is ranked already)
+  uint32_t par = 0;
+  for (uint32_t cbase = pbeg;;) {
+    lds_sync();  // every wave's counts of the chunk (and, the first time, run[]) are in LDS
+    for (uint32_t b = tid; b < nbins; b += kGBlock) {
+      uint32_t s = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kW; ++w) {
+        const uint32_t t = cnt[w * cst + b];
+        cnt[w * cst + b] = static_cast<uint16_t>(s);
+        s += t;
+      }
+      run[(par ^ 1u) * nbp + b] = run[par * nbp + b] + s;
+    }
+    lds_sync();
+    const uint32_t* rb = run + par * nbp;
+    const uint32_t wbase = cbase + wave * (64u * kGRounds);
+#pragma unroll
+    for (int r = 0; r < kGRounds; ++r) {
+      if (br[r] != 0xffffffffu) {
+        const uint32_t bin = br[r] & 0xffffu;
+        a.perm[rb[bin] + mycnt[bin] + (br[r] >> 16)] = wbase + r * 64u + lane;
+      }
+    }
+    cbase += kChunk;
+    if (cbase >= pend) break;
+    par ^= 1u;
+    rank_chunk(cbase);  // its own counter row only: the other waves' prefixes are read by now
   }
   zero_next();
 }
@@ -2910,16 +3135,24 @@ int launch_group_wide(const GroupArgs& a, void* stream) {
   return NBG_OK;
 }
 
-size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan) {
+// group_kernel: base[nbp] + tot[nbp] u32, cnt[waves][cst] u16, sslot[kChunk] u32 (40 KB at 1001 bins);
+// compact (group_direct_kernel): run[2][nbp] + tot[nbp] u32, cnt[waves][cst] u16 (28 KB at 1001 bins)
+size_t group_lds(uint32_t nbins, bool compact) {
   const size_t nbp = (nbins + 3) & ~3u, cst = (nbins + 8) & ~7u;
-  size_t w = nbp * 2 + cst * (kGBlock / 64) / 2 + kChunk;
-  if (scan == kScanLds) w += static_cast<size_t>(n_parts) * nbins;
-  return w * 4;
+  return ((compact ? nbp * 3 : nbp * 2 + kChunk) + cst * (kGBlock / 64) / 2) * 4;
+}
+
+// What an in-place persistent ring leaves of a CU's LDS for a co-resident group block (ring_lds(1)
+// of 160 KiB, less allocation granularity and a hist_kernel block's share).
+constexpr size_t kGroupLdsBesideRing = 26u * 1024u;
+bool group_compact(uint32_t nbins, bool ring_running) {
+  if (const char* e = std::getenv("NBG_GROUP_COMPACT")) return std::atoi(e) != 0;  // tests and measurements
+  return ring_running && group_lds(nbins, false) > kGroupLdsBesideRing;
 }
 
 // Default: sum the partition histograms from L2 inside the group kernel while the rows are
-// small (every block reads all of them), else a separate scan kernel.  NBG_GSCAN=0/1/2 forces
-// a mode (diagnostics; 1 falls back when the rows do not fit in LDS).
+// small (every block reads all of them), else a separate scan kernel.  NBG_GSCAN=0/2 forces a mode
+// (measurements).
 // Partition histograms from the classify kernel's per-block flush for few bins, from hist_kernel
 // for many (NBG_HIST_KERNEL_BINS overrides the threshold, for measurements).
 bool hist_in_classify(uint32_t nbins) {
@@ -2936,44 +3169,33 @@ int pick_group_scan(uint32_t nbins, uint32_t n_parts) {
     return e ? std::atoi(e) : -1;
   }();
   if (forced == kScanKernel || forced == kScanDirect) return forced;
-  if (forced == kScanLds && group_lds(nbins, n_parts, kScanLds) <= 100 * 1024) return kScanLds;
   return static_cast<size_t>(nbins) * n_parts <= 32u * 1024u ? kScanDirect : kScanKernel;
 }
 
-int launch_group(const GroupArgs& a, int scan, void* stream) {
-  const size_t lds = group_lds(a.nb + 1, a.n_parts, scan);
-  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7>
-                                                : (scan == kScanLds ? group_kernel<kScanLds, 7> : group_kernel<kScanKernel, 7>))
-                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10>
-                                               : (scan == kScanLds ? group_kernel<kScanLds, 10> : group_kernel<kScanKernel, 10>));
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds)) != hipSuccess)
-      (void)hipGetLastError();
-  }
+auto group_fn(uint32_t bits, int scan, bool compact) {
+  if (compact)
+    return bits <= 7 ? (scan == kScanDirect ? group_direct_kernel<kScanDirect, 7> : group_direct_kernel<kScanKernel, 7>)
+                     : (scan == kScanDirect ? group_direct_kernel<kScanDirect, 10> : group_direct_kernel<kScanKernel, 10>);
+  return bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7> : group_kernel<kScanKernel, 7>)
+                   : (scan == kScanDirect ? group_kernel<kScanDirect, 10> : group_kernel<kScanKernel, 10>);
+}
+
+int launch_group(const GroupArgs& a, int scan, void* stream, bool compact) {
   GroupMulti gm{};
   gm.g[0] = a;
   gm.per = a.n_parts;
-  hipLaunchKernelGGL(fn, dim3(a.n_parts), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), gm);
+  hipLaunchKernelGGL(group_fn(a.bits, scan, compact), dim3(a.n_parts), dim3(kGBlock), group_lds(a.nb + 1, compact),
+                     static_cast<hipStream_t>(stream), gm);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "group launch: %s", hipGetErrorString(e));
   return NBG_OK;
 }
 
-int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream) {
+int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream, bool compact) {
   const GroupArgs& a = gm.g[0];
   if (n == 0 || n > kMaxMulti) return set_error(NBG_EINVAL, "group (multi): %u batches", n);
-  const size_t lds = group_lds(a.nb + 1, gm.per, scan);
-  auto fn = a.bits <= 7 ? (scan == kScanDirect ? group_kernel<kScanDirect, 7>
-                                                : (scan == kScanLds ? group_kernel<kScanLds, 7> : group_kernel<kScanKernel, 7>))
-                        : (scan == kScanDirect ? group_kernel<kScanDirect, 10>
-                                               : (scan == kScanLds ? group_kernel<kScanLds, 10> : group_kernel<kScanKernel, 10>));
-  if (lds > 64 * 1024) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            static_cast<int>(lds)) != hipSuccess)
-      (void)hipGetLastError();
-  }
-  hipLaunchKernelGGL(fn, dim3(gm.per * n), dim3(kGBlock), lds, static_cast<hipStream_t>(stream), gm);
+  hipLaunchKernelGGL(group_fn(a.bits, scan, compact), dim3(gm.per * n), dim3(kGBlock), group_lds(a.nb + 1, compact),
+                     static_cast<hipStream_t>(stream), gm);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "group launch (multi): %s", hipGetErrorString(e));
   return NBG_OK;

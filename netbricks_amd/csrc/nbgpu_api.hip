@@ -349,6 +349,10 @@ int upload(nbg_maglev* h) {
 // While a persistent ring runs on the device, kernels that need a whole CU's LDS (the streaming
 // kernels, the LDS-staged LUT) would wait for it to end: batches of other handles then take the
 // tile-per-wave kernel, which co-runs in the LDS the ring leaves free.
+// Many bins while a persistent ring runs on the device: the LDS-light group kernel, which co-runs
+// beside the ring instead of waiting for its end.
+bool compact_group(const nbg_maglev* h) { return group_compact(h->nb + 1, device_ring_running(h->device)); }
+
 bool use_lds_lut(const nbg_maglev* h, uint32_t flags) {
   return (flags & NBG_LUT_LDS) && h->lut_bytes <= 72 * 1024 && !device_ring_running(h->device);
 }
@@ -588,7 +592,7 @@ int zero_captured(uint32_t* p, size_t words, void* stream) { return launch_zero(
 // standalone group kernel zeroes nothing there (the next lagged classify zeroes the sets).
 int flush_lag(nbg_maglev* h, hipStream_t s) {
   h->pending = h->pending_lag = false;
-  return launch_group(h->pending_args, kScanDirect, s);
+  return launch_group(h->pending_args, kScanDirect, s, compact_group(h));
 }
 
 // A lagged classify (NBG_GROUP_LAG): the streaming kernel accumulates this batch's partition rows
@@ -894,7 +898,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
     } else {
       if (hist_k && (rc = launch_hist(ha, stream))) return rc;
       if (scan == kScanKernel && (rc = launch_scan(sa, stream))) return rc;
-      if ((rc = wide ? launch_group_wide(ga, stream) : launch_group(ga, scan, stream))) return rc;
+      if ((rc = wide ? launch_group_wide(ga, stream) : launch_group(ga, scan, stream, compact_group(h)))) return rc;
     }
   }
   return NBG_OK;
@@ -1071,7 +1075,7 @@ int desc_multi_common(nbg_maglev* h, const nbg_desc_batch* batches, uint32_t n_b
   }
   if (hist_k && (rc = launch_hist_multi(hm, n_batches, stream))) return rc;
   if (scan == kScanKernel && (rc = launch_scan_multi(sm, n_batches, stream))) return rc;
-  return launch_group_multi(gm, n_batches, scan, stream);
+  return launch_group_multi(gm, n_batches, scan, stream, compact_group(h));
 }
 
 }  // namespace
@@ -1252,7 +1256,7 @@ int nbg_maglev_classify_device_multi(nbg_maglev* h, const nbg_batch* batches, ui
       return NBG_OK;
     }
     if (hist_k && (rc = launch_hist_multi(hm, n_batches, stream))) return rc;
-    if ((rc = launch_group_multi(gm, n_batches, scan, stream))) return rc;
+    if ((rc = launch_group_multi(gm, n_batches, scan, stream, compact_group(h)))) return rc;
   }
   return NBG_OK;
 }
@@ -1333,12 +1337,12 @@ int nbg_maglev_finish_group(nbg_maglev* h, void* stream) {
     h->pending_multi = 0;
     if (h->pending_hist_multi && (rc = launch_hist_multi(h->pending_hm, n, stream))) return rc;
     if (h->pending_scan_mode == kScanKernel && (rc = launch_scan_multi(h->pending_sm, n, stream))) return rc;
-    return launch_group_multi(h->pending_gm, n, h->pending_scan_mode, stream);
+    return launch_group_multi(h->pending_gm, n, h->pending_scan_mode, stream, compact_group(h));
   }
   if (h->pending_hist && (rc = launch_hist(h->pending_hist_args, stream))) return rc;
   if (h->pending_scan_mode == kScanKernel && (rc = launch_scan(h->pending_scan, stream))) return rc;
   if ((rc = h->pending_wide ? launch_group_wide(h->pending_args, stream)
-                            : launch_group(h->pending_args, h->pending_scan_mode, stream)))
+                            : launch_group(h->pending_args, h->pending_scan_mode, stream, compact_group(h))))
     return rc;
   return NBG_OK;
 }
@@ -1731,7 +1735,7 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
   ga.hist16 = 0;
   ga.counts = d_counts;
   ga.perm = d_perm;
-  return launch_group(ga, scan, s);
+  return launch_group(ga, scan, s, group_compact(nbins, true));
 }
 
 // Batches first .. first + n - 1 grouped by one gate, one hist and one group launch on s (a
@@ -1808,7 +1812,7 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
   hm.per = n_parts_max;
   gm.per = n_parts_max;
   if ((rc = launch_hist_multi(hm, n, s))) return rc;
-  return launch_group_multi(gm, n, scan, s);
+  return launch_group_multi(gm, n, scan, s, group_compact(nbins, true));
 }
 
 // Wait until `done()` holds, the ring has gone, or timeout_ms (0: none).  `done` runs under r->mu

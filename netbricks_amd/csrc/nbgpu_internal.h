@@ -211,7 +211,7 @@ struct GroupArgs {
   uint32_t bits;              // ceil(log2(nb+1))
   uint32_t n_parts;
   uint32_t part_pkts;
-  const uint32_t* part_hist;  // [n_parts][nb+1]      (kScanLds / kScanDirect)
+  const uint32_t* part_hist;  // [n_parts][nb+1]      (kScanDirect)
   const uint32_t* part_prefix;// [n_parts][nb+1]      (scan_kernel path)
   const uint32_t* totals;     // [nb+1]               (scan_kernel path)
   uint32_t hist16;            // kScanDirect: rows of two 16-bit bins per word ((nbins + 1) / 2 words)
@@ -229,9 +229,9 @@ struct GroupMulti {
   uint32_t per;
 };
 
-// How the group kernel gets each partition's per-bin prefix: from scan_kernel's output, by
-// summing the partition histograms staged in LDS, or by summing them straight from L2.
-enum GroupScan { kScanKernel = 0, kScanLds = 1, kScanDirect = 2 };
+// How the group kernel gets each partition's per-bin prefix: from scan_kernel's output, or by
+// summing the partition histograms straight from L2.
+enum GroupScan { kScanKernel = 0, kScanDirect = 2 };
 
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
@@ -269,9 +269,11 @@ int launch_hist_multi(const HistMulti& hm, uint32_t n, void* stream);  // nb + 1
 bool hist_in_classify(uint32_t nbins);
 int launch_lpm_lookup(const uint16_t* tbl24, const uint16_t* tbl_long, const uint32_t* ips, uint64_t n,
                       uint16_t* gate, void* stream);
-int launch_group(const GroupArgs& a, int scan, void* stream);
+// compact: the LDS-light group kernel (group_compact(): many bins while a persistent ring runs)
+int launch_group(const GroupArgs& a, int scan, void* stream, bool compact);
 // one launch grouping gm.g[0 .. n): blocks per batch gm.per (the largest n_parts)
-int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream);
+int launch_group_multi(const GroupMulti& gm, uint32_t n, int scan, void* stream, bool compact);
+bool group_compact(uint32_t nbins, bool ring_running);
 int launch_group_wide(const GroupArgs& a, void* stream);  // nb + 1 > kMaxGroupBins
 // One launch for a batch of at most small_max() packets and at most kMaxGroupBins bins: classify
 // and (when g.perm / g.counts) group.  The batch base must be 16-B aligned.
@@ -280,7 +282,7 @@ uint32_t small_max();
 int launch_classify_idx(const ClassifyArgs& a, int grid, void* stream);  // kIdx classify (tile per wave)
 int launch_tiled_lookup(const TileArgs& a, void* stream);
 uint32_t lut_tiles(uint64_t m);
-size_t group_lds(uint32_t nbins, uint32_t n_parts, int scan);
+size_t group_lds(uint32_t nbins, bool compact);
 int pick_group_scan(uint32_t nbins, uint32_t n_parts);
 int classify_grid(bool lds_lut, uint32_t lut_bytes, uint32_t nb, int device, int* grid);
 

@@ -68,6 +68,8 @@ def _check_owned(name: str, pkts, offsets, n_pkts: int) -> None:
     that checked their descriptors once)."""
     import torch
 
+    if torch.cuda.is_current_stream_capturing():
+        return  # no reduction inside a graph capture: the caller's descriptors are taken as they are
     if n_pkts and offsets is not None:
         top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
         if top + 64 > pkts.numel():

@@ -7,6 +7,7 @@ for the chain the lpm gate (test/maglev/src/nf.rs:92-106, test/lpm/src/nf.rs:212
 import ctypes as C
 import json
 import os
+import time
 
 import numpy as np
 import pytest
@@ -196,10 +197,13 @@ def test_desc_multi_refusals(torch_cuda):
     mg.close()
 
 
-def test_desc_multi_beside_running_ring(torch_cuda):
+@pytest.mark.parametrize("swap", [False, True])
+def test_desc_multi_beside_running_ring(torch_cuda, swap):
     """Several RX queues' IMIX batches (C3 and the C5 chain, multi-batch launches on other handles)
-    while the device's persistent ring runs and takes fixed-slot batches: the tile-per-wave blocks
-    co-run in the LDS the ring leaves, every output bit-exact, and the ring's batches too."""
+    while the device's persistent ring runs and takes fixed-slot batches, read only or in place: the
+    tile-per-wave classify blocks and the group blocks (C3's 1001 bins included: 28 KB of LDS) co-run
+    in the LDS the ring leaves, so the grouping finishes while the ring still runs (well before its
+    5 s idle exit); every output bit-exact, and the ring's batches too."""
     import netbricks_amd as nb
     from netbricks_amd import Lpm, Maglev, chain_lpm_maglev_multi
 
@@ -221,16 +225,20 @@ def test_desc_multi_beside_running_ring(torch_cuda):
     db5 = [_dev_batch(torch, *t) for t in tr5]
     torch.cuda.synchronize()
     s3, s5 = torch.cuda.Stream(), torch.cuda.Stream()
-    with ring_mg.ring(swap_macs=False) as ring:
+    with ring_mg.ring(swap_macs=swap, idle_ms=5000) as ring:
         t = ring.post(rd, n, rout)
+        t0 = time.perf_counter()
         r3 = c3.group_by_desc_multi(db3, stream=s3.cuda_stream)
         r5 = chain_lpm_maglev_multi(c5, lpm, db5, stream=s5.cuda_stream)
         ring.wait(t)
         s3.synchronize()
         s5.synchronize()
+        assert time.perf_counter() - t0 < 2.0  # the ring (5 s idle exit) is still resident
     c3.check()
     c5.check()
-    np.testing.assert_array_equal(_np16(rout, n), orc.classify(rbuf.copy(), n, lut65, swap=False))
+    ref = rbuf.copy()
+    np.testing.assert_array_equal(_np16(rout, n), orc.classify(ref, n, lut65, swap=swap))
+    np.testing.assert_array_equal(rd.cpu().numpy(), ref)
     _check_maglev(torch, c3, tr3, r3, db3, lut1000, 1000)
     for (buf, off, ln, m), r in zip(tr5, r5):
         eg, eb = orc.chain_classify(buf, m, t24, tl, lut65, offs=off, lens=ln)

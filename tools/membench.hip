@@ -60,6 +60,8 @@ __global__ __launch_bounds__(256) void pattern(uint4* __restrict__ buf, uint4* _
     if (MODE == 6 && (threadIdx.x & 3) == 0)
       nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
     if (MODE == 7) wt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+    if (MODE == 8 && (threadIdx.x & 3) < 2)  // the first 32-B sector of every 64-B slot (chunks 0..1)
+      nt_store(&buf[base + k * 256], make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
   }
   if (acc == 0x12345678u) sink[0] = acc;
 }
@@ -107,6 +109,8 @@ __global__ __launch_bounds__(256) void windows(uint8_t* __restrict__ buf, const 
     acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
     const uint32_t o = static_cast<uint32_t>(__shfl(static_cast<int>(own), k * 16 + quad));
     if (MODE == 1) nt_store(reinterpret_cast<uint4*>(buf + o + part * 16u), make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
+    if ((MODE == 3 && part == 0u) || (MODE == 4 && part < 2u))  // 16 B / the first 32-B sector per window
+      nt_store(reinterpret_cast<uint4*>(buf + o + part * 16u), make_uint4(v[k].y, v[k].x, v[k].z, v[k].w));
     if (MODE == 2 && part == 0u) {
       uint32_t* m = reinterpret_cast<uint32_t*>(dst + static_cast<size_t>(wbase + k * 16 + quad) * 12u);
       m[0] = v[k].y; m[1] = v[k].x; m[2] = v[k].z;
@@ -183,6 +187,8 @@ int main(int argc, char** argv) {
       const int grid = static_cast<int>(n16 / (256 * 4));
       report("read U4 nt-load", time_it([&](int i) { pattern<4, 0, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, 0);
       report("rw full nt-load nt-store U4", time_it([&](int i) { pattern<4, 5, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
+      report("rw 32B sector (chunks 0-1) nt-load nt-store U4", time_it([&](int i) { pattern<4, 8, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 2);
+      report("rw chunk0 (16B) nt-load nt-store U4", time_it([&](int i) { pattern<4, 6, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 4);
       report("rw full nt-load sc1-store U4 (ring)", time_it([&](int i) { pattern<4, 7, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B);
       report("read nt-load + dense 16B/pkt out U4", time_it([&](int i) { pattern<4, 4, true><<<grid, 256>>>(bufs[i % kBufs], dst, sink); }, iters), B, B / 4);
       // four 64 MiB buffers' worth in one launch (the multi-batch launch's read ceiling), rotating over
@@ -196,6 +202,7 @@ int main(int argc, char** argv) {
       report("read 256 MiB in one launch U4 nt-load", time_it([&](int i) { pattern<4, 0, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 0);
       // the same rewrite shapes without a launch ramp every 64 MiB (the persistent ring's regime)
       report("rw full nt-load nt-store, 256 MiB per launch", time_it([&](int i) { pattern<4, 5, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 4 * B);
+      report("rw 32B sector nt, 256 MiB per launch", time_it([&](int i) { pattern<4, 8, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 2 * B);
       report("rw full nt-load sc1-store, 256 MiB per launch", time_it([&](int i) { pattern<4, 7, true><<<g4, 256>>>(big[i % 8], dst, sink); }, iters), 4 * B, 4 * B);
       for (auto& p : big) CK(hipFree(p));
     }
@@ -238,6 +245,10 @@ int main(int argc, char** argv) {
     report("imix windows read nt-load", us, W + D, 0);
     us = time_it([&](int i) { windows<1, true><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
     report("imix windows rw nt-load nt-store", us, W + D, W);
+    us = time_it([&](int i) { windows<3, true><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
+    report("imix windows rw 16B (chunk 0) nt", us, W + D, W / 4);
+    us = time_it([&](int i) { windows<4, true><<<grid, 256>>>(ib[i % ib.size()], d_off, mo, sink, n); }, iters);
+    report("imix windows rw 32B sector nt", us, W + D, W / 2);
   }
   return 0;
 }
