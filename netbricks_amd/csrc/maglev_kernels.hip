@@ -1932,6 +1932,12 @@ __global__ __launch_bounds__(kGBlock) void hist_kernel(HistMulti hm) {
     }
   }
   lds_sync();
+  if (a.hist16) {  // half the row bytes the group kernel's direct prefix reads
+    const uint32_t hw = (nbins + 1) >> 1;
+    uint32_t* row = a.part_hist + static_cast<size_t>(c) * hw;
+    for (uint32_t w = tid; w < hw; w += kGBlock) row[w] = hs[2 * w] | (2 * w + 1 < nbins ? hs[2 * w + 1] << 16 : 0u);
+    return;
+  }
   uint32_t* row = a.part_hist + static_cast<size_t>(c) * nbins;
   for (uint32_t b = tid; b < nbins; b += kGBlock) row[b] = hs[b];
 }
@@ -2235,21 +2241,32 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
   }
 }
 
-// One 512-thread block per partition (part_pkts packets, processed in 4096-packet chunks).
-// Prologue: prefix of this partition over earlier partitions and the group bases, either
-// summed here from the L2-resident partition histograms, or read from scan_kernel's output.
-// Then per chunk: wave ballot multisplit ranks (stable), per-bin offsets, a local counting sort
-// in LDS and coalesced perm stores.
-// 4 waves per SIMD: the group kernel is compiled for <= 64 VGPRs, so a resident group block leaves
-// the other streams' classify waves their registers
+// One 512-thread block per partition (part_pkts packets, processed in 4096-packet chunks): the
+// stable per-group FIFO order of group_by.rs:46-51.  Wave w owns rounds [8w, 8w + 8) of 64 packets of
+// every chunk (packet = chunk base + 512 w + 64 r + lane).
+//   Entry: every global load of the block is issued at once: the first chunk's backends, then the
+//     prologue's (kScanDirect: this partition's share of the L2-resident partition rows; kScanKernel:
+//     scan_kernel's prefix row and the bin totals).  The first chunk is ranked while the prologue's
+//     loads are in flight (a wave ballot multisplit per 64-packet round, one ballot per bin bit; the
+//     wave's 16-bit LDS counter row carries its earlier rounds).
+//   Then four barrier-separated phases per chunk: (1) the prologue's sums and the first half of the
+//     chunk's bin-major exclusive scan over the (bin, wave) counters; (2) the group bases (exclusive
+//     scan of the totals over bins) and the scan's write-back; (3) per bin, the perm position of the
+//     chunk's first packet of the bin, and the local counting sort into LDS; (4) coalesced perm
+//     stores (consecutive sorted slots of one bin are consecutive perm entries).
+// The round-4 form ranked only after the prologue and took 8 barriers per chunk; its phase timeline
+// (tools/gprobe.py, profiles/r05_gprobe.txt) had the row prologue (1.84 us) and the ranks (1.55 us,
+// VALU-bound) one after the other on each block's critical path.
+// 4 waves per SIMD (two resident blocks per CU, <= 128 VGPRs).
 constexpr int kGroupWaves = 4;
 // BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
 template <int SCAN, int BITS>
 // Blocks [j * gm.per, j * gm.per + g[j].n_parts) group batch j (a single batch: j = 0, c = blockIdx.x).
 __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti gm) {
   extern __shared__ __align__(16) uint32_t gs[];
-  __shared__ uint32_t s_wave[kGBlock / 64];
+  __shared__ uint32_t s_wave[2][kGBlock / 64];
   constexpr uint32_t kW = kGBlock / 64;  // waves
+  constexpr uint32_t kMaxBins = 1u << BITS;
   const uint32_t bj = blockIdx.x / gm.per;
   const GroupArgs a = gm.g[bj];
   const uint32_t nbins = a.nb + 1;
@@ -2267,16 +2284,17 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   }
   const uint32_t nbp = (nbins + 3) & ~3u;
   uint32_t* base = gs;                 // [nbins] next perm position of this partition, per bin
-  uint32_t* tot = base + nbp;          // [nbins]
+  uint32_t* tot = base + nbp;          // [nbins] bin totals (prologue), then the chunk's perm bases
   // 16-bit per-wave counters (a wave counts <= 512 packets of a chunk; chunk slots < kChunk) and one
-  // word per sorted slot (bin << 12 | packet within the chunk): 40 KB of LDS at 1001 bins instead of
-  // 64 KB, so that a resident group block leaves other streams' classify blocks their LDS
-  static_assert(kChunk <= 4096, "sorted slots hold a 12-bit packet index");
+  // word per sorted slot (bin << 12 | packet within the chunk): 40 KB of LDS at 1001 bins
+  static_assert(kChunk <= 4096 && kChunk == kGBlock * kGRounds, "sorted slots hold a 12-bit packet index");
   const uint32_t cst = (nbins + 8) & ~7u;  // cnt row stride: a scratch slot for lanes past the end; 16-B rows
   uint16_t* cnt = reinterpret_cast<uint16_t*>(tot + nbp);  // [kW][cst]
   uint32_t* sslot = reinterpret_cast<uint32_t*>(cnt + kW * cst);  // [kChunk]
+  uint16_t* mycnt = cnt + wave * cst;
+  const bool perm = a.perm != nullptr;
 
-  // ---- the first chunk's backends are loaded up front: their latency overlaps the prologue
+  // ---- entry: the first chunk's backends, then the prologue's loads, all in flight together
   const uint32_t pbeg = c * a.part_pkts;
   const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
   uint32_t pre_bin[kGRounds];
@@ -2285,134 +2303,52 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) pre_bin[r] = ld_u16(a.backend, min(wb + r * 64u + lane, a.n_pkts - 1u) * 2u);
   }
-  // ---- prologue: per-bin prefix over earlier partitions, totals, group bases
-  for (uint32_t b = tid; b < nbins; b += kGBlock) {
+  // the scheduler keeps the backend loads ahead of the prologue's (vmcnt retires in issue order: the
+  // ranks then wait for the backends only)
+  __builtin_amdgcn_sched_barrier(0);
+  // kScanDirect: thread (w, j) = (tid % hw, tid / hw) sums rows j, j + L, ... of row word w (L threads
+  // per word; consecutive threads read consecutive words of one row); the first kU of its rows are
+  // loaded here.  kScanKernel: this thread's consecutive bins of the prefix row and the totals.
+  constexpr uint32_t kU = 18;  // 65 backends, 16-bit rows: 33 words, L = 15, 18 rows per thread
+  constexpr uint32_t kCb = kMaxBins > kGBlock ? kMaxBins / kGBlock : 1u;  // consecutive bins per thread
+  const uint32_t hw = a.hist16 ? (nbins + 1) >> 1 : nbins;  // row words
+  const uint32_t L = hw >= kGBlock ? 1u : kGBlock / hw;
+  uint32_t h[kU];
+  uint32_t pk[kCb], tk[kCb];
+  // rows q0, q0 + L, ... of row word w
+  auto load_rows = [&](uint32_t w, uint32_t q0) {
+#pragma unroll
+    for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * hw + w) * 4u);
+  };
+  if constexpr (SCAN == kScanDirect) {
+    // every thread loads its first (word, row) pair's rows (clamped; a thread past hw * L ignores
+    // them): a load inside a branch makes the compiler wait for all of them at the join, before the
+    // ranks.  More than kGBlock row words (many bins, 32-bit rows) take a second pair later.
+    load_rows(tid % hw, tid / hw);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) {
+      const uint32_t b = min(tid * kCb + k, nbins - 1u);
+      pk[k] = ld_u32(a.part_prefix, (c * nbins + b) * 4u);
+      tk[k] = ld_u32(a.totals, b * 4u);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  for (uint32_t b = tid; b < nbp; b += kGBlock) {
     base[b] = 0;
     tot[b] = 0;
-  }
-  if constexpr (SCAN == kScanDirect) {
-    lds_sync();
-    // L threads per row word, each summing a strided subset of the partition rows straight from
-    // L2 (consecutive threads read consecutive words of one row: coalesced)
-    if (a.hist16) {
-      const uint32_t hw = (nbins + 1) >> 1;
-      const uint32_t L = hw >= kGBlock ? 1u : kGBlock / hw;
-      for (uint32_t t = tid; t < hw * L; t += kGBlock) {
-        const uint32_t w = t % hw, j = t / hw;
-        uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
-        // 65 backends: 33 words, L = 15, 18 rows per thread: one L2 round trip
-        constexpr uint32_t kU = 24;
-        for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
-          uint32_t h[kU];
-#pragma unroll
-          for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * hw + w) * 4u);
-#pragma unroll
-          for (uint32_t k = 0; k < kU; ++k) {
-            const uint32_t q = q0 + k * L;
-            const uint32_t lo = q < a.n_parts ? h[k] & 0xffffu : 0u, hi = q < a.n_parts ? h[k] >> 16 : 0u;
-            all_lo += lo;
-            all_hi += hi;
-            pre_lo += q < c ? lo : 0u;
-            pre_hi += q < c ? hi : 0u;
-          }
-        }
-        if (pre_lo) atomicAdd(&base[2 * w], pre_lo);
-        if (all_lo) atomicAdd(&tot[2 * w], all_lo);
-        if (2 * w + 1 < nbins) {
-          if (pre_hi) atomicAdd(&base[2 * w + 1], pre_hi);
-          if (all_hi) atomicAdd(&tot[2 * w + 1], all_hi);
-        }
-      }
-    } else {
-    const uint32_t L = nbins >= kGBlock ? 1u : kGBlock / nbins;
-    for (uint32_t t = tid; t < nbins * L; t += kGBlock) {
-      const uint32_t b = t % nbins, j = t / nbins;
-      uint32_t pre = 0, all = 0;
-      // kU loads in flight per thread: one L2 round trip per kU rows (n_parts <= 256, L >= 1;
-      // 65 backends: L = 7, 37 rows per thread, one round trip)
-      constexpr uint32_t kU = 40;
-      for (uint32_t q0 = j; q0 < a.n_parts; q0 += kU * L) {
-        uint32_t h[kU];
-#pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * nbins + b) * 4u);
-#pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) {
-          pre += q0 + k * L < c ? h[k] : 0u;
-          all += q0 + k * L < a.n_parts ? h[k] : 0u;
-        }
-      }
-      if (pre) atomicAdd(&base[b], pre);
-      if (all) atomicAdd(&tot[b], all);
-    }
-    }
-  } else {
-    lds_sync();
-    for (uint32_t b = tid; b < nbins; b += kGBlock) {
-      base[b] = a.part_prefix[static_cast<size_t>(c) * nbins + b];
-      tot[b] = a.totals[b];
-    }
-  }
-  lds_sync();
-  // group bases (exclusive scan of the totals over bins).  Loops have compile-time trip counts
-  // (bins < 2^BITS) so that their LDS reads issue back to back.
-  constexpr uint32_t kMaxBins = 1u << BITS;
-  if constexpr (kMaxBins <= 128) {  // one wave, <= 2 bins per lane (no block-wide scan)
-    if (wave == 0) {
-      uint32_t t2[2], s = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        const uint32_t b = lane * 2 + k;
-        t2[k] = b < nbins ? tot[b] : 0u;
-        s += t2[k];
-      }
-      uint32_t gb = wave_incl_scan(s) - s;
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        const uint32_t b = lane * 2 + k;
-        if (b < nbins) {
-          if (c == 0 && a.counts) a.counts[b] = t2[k];
-          base[b] += gb;  // group base + prefix over earlier partitions
-        }
-        gb += t2[k];
-      }
-    }
-  } else {  // the whole block, <= kMaxBins / kGBlock bins per thread
-    constexpr uint32_t kCh = (kMaxBins + kGBlock - 1) / kGBlock;
-    uint32_t tk[kCh], s = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kCh; ++k) {
-      const uint32_t b = tid * kCh + k;
-      tk[k] = b < nbins ? tot[b] : 0u;
-      s += tk[k];
-    }
-    uint32_t all;
-    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave, all);
-#pragma unroll
-    for (uint32_t k = 0; k < kCh; ++k) {
-      const uint32_t b = tid * kCh + k;
-      if (b < nbins) {
-        if (c == 0 && a.counts) a.counts[b] = tk[k];
-        base[b] += gb;
-      }
-      gb += tk[k];
-    }
-  }
-  lds_sync();
-  if (!a.perm) {
-    zero_next();
-    return;
   }
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
-  uint16_t* mycnt = cnt + wave * cst;
-  for (uint32_t cbase = pbeg; cbase < pend; cbase += kChunk) {
-    // each wave zeroes its own counter row: every reader of the previous chunk's counters has
-    // passed a barrier since, and one wave's LDS operations execute in order
+  uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
+  // one chunk's ranks (its backends in pre_bin); afterwards the next chunk's backends are loaded
+  auto rank_chunk = [&](uint32_t cbase) {
+    // each wave zeroes its own counter row: every reader of the previous chunk's counters has passed
+    // a barrier since, and one wave's LDS operations execute in order
 #pragma unroll
     for (uint32_t k = 0; k < (kMaxBins + 8 + 511) / 512; ++k)
       if ((lane + k * 64) * 8 < cst) reinterpret_cast<uint4*>(mycnt)[lane + k * 64] = make_uint4(0, 0, 0, 0);
-    uint32_t br[kGRounds];  // rank << 16 | bin (bins < kMaxGroupBins, ranks < kChunk), or ~0 past the end
     const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
@@ -2445,35 +2381,156 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       for (int r = 0; r < kGRounds; ++r)
         pre_bin[r] = ld_u16(a.backend, min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u) * 2u);
     }
-    lds_sync();
-    // one exclusive scan over the counters in bin-major order (bin, wave): the chunk-local slot
-    // where wave w's packets of bin b start
-    // (each thread owns kPer consecutive elements: whole bins' wave counters when kPer >= kW)
-    constexpr uint32_t kPer = (kMaxBins * kW + kGBlock - 1) / kGBlock;
-    const uint32_t ne = nbins * kW;
-    uint32_t ev[kPer], esum = 0;
+  };
+  if (perm) rank_chunk(pbeg);
+
+  // bin-major exclusive scan over the chunk's (bin, wave) counters: the chunk-local slot where wave
+  // w's packets of bin b start (each thread owns kPer consecutive elements: whole bins' wave counters
+  // when kPer >= kW); first half: the wave-level scan
+  constexpr uint32_t kPer = (kMaxBins * kW + kGBlock - 1) / kGBlock;
+  const uint32_t ne = nbins * kW;
+  uint32_t ev[kPer], esum = 0, ex = 0;
+  auto chunk_scan_begin = [&] {
+    esum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t e = tid * kPer + k;
       ev[k] = e < ne ? cnt[(e % kW) * cst + e / kW] : 0u;
       esum += ev[k];
     }
-    uint32_t ctotal;
-    uint32_t x = block_excl_scan_n<kGBlock>(esum, s_wave, ctotal);
+    ex = wave_incl_scan(esum);
+    if (lane == 63u) s_wave[0][wave] = ex;
+  };
+  // second half (after a barrier): the wave's offset, the write-back; returns the chunk's packets
+  auto chunk_scan_end = [&]() -> uint32_t {
+    uint32_t wpre = 0, ctotal = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kW; ++w) {
+      const uint32_t t = s_wave[0][w];
+      wpre += w < wave ? t : 0u;
+      ctotal += t;
+    }
+    uint32_t x = wpre + ex - esum;
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t e = tid * kPer + k;
       if (e < ne) cnt[(e % kW) * cst + e / kW] = static_cast<uint16_t>(x);
       x += ev[k];
     }
-    lds_sync();
-    // per bin: perm position of chunk slot j of bin b = tot[b] + j; advance past the bin
+    return ctotal;
+  };
+
+  lds_sync();  // (B1) base / tot zeroed, every wave's counts of the first chunk in LDS
+
+  // ---- (1) prologue sums, the chunk scan's first half
+  uint32_t gs_incl = 0, gs_own = 0;  // kScanKernel: this thread's bins' totals, scanned over the wave
+  if constexpr (SCAN == kScanDirect) {
+    for (uint32_t t = tid; t < hw * L; t += kGBlock) {
+      const uint32_t rw = t % hw, rj = t / hw;
+      if (t != tid) load_rows(rw, rj);
+      uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
+      for (uint32_t q0 = rj;;) {
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) {
+          const uint32_t q = q0 + k * L;
+          const uint32_t lo = q < a.n_parts ? (a.hist16 ? h[k] & 0xffffu : h[k]) : 0u;
+          const uint32_t hi = q < a.n_parts && a.hist16 ? h[k] >> 16 : 0u;
+          all_lo += lo;
+          all_hi += hi;
+          pre_lo += q < c ? lo : 0u;
+          pre_hi += q < c ? hi : 0u;
+        }
+        q0 += kU * L;
+        if (q0 >= a.n_parts) break;
+        load_rows(rw, q0);  // more rows than kU per thread (many bins over many partitions)
+      }
+      const uint32_t b0 = a.hist16 ? 2 * rw : rw;
+      if (pre_lo) atomicAdd(&base[b0], pre_lo);
+      if (all_lo) atomicAdd(&tot[b0], all_lo);
+      if (a.hist16 && b0 + 1 < nbins) {
+        if (pre_hi) atomicAdd(&base[b0 + 1], pre_hi);
+        if (all_hi) atomicAdd(&tot[b0 + 1], all_hi);
+      }
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) gs_own += tid * kCb + k < nbins ? tk[k] : 0u;
+    gs_incl = wave_incl_scan(gs_own);
+    if (lane == 63u) s_wave[1][wave] = gs_incl;
+  }
+  if (perm) chunk_scan_begin();
+  lds_sync();  // (B2)
+
+  // ---- (2) group bases (exclusive scan of the totals over bins), the chunk scan's write-back
+  if constexpr (SCAN == kScanDirect && kMaxBins <= 128) {  // one wave, <= 2 bins per lane
+    if (wave == 0) {
+      uint32_t t2[2], s = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        t2[k] = b < nbins ? tot[b] : 0u;
+        s += t2[k];
+      }
+      uint32_t gb = wave_incl_scan(s) - s;
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t b = lane * 2 + k;
+        if (b < nbins) {
+          if (c == 0 && a.counts) a.counts[b] = t2[k];
+          base[b] += gb;  // group base + prefix over earlier partitions
+        }
+        gb += t2[k];
+      }
+    }
+  } else if constexpr (SCAN == kScanDirect) {  // many bins summed here: a block-wide scan of tot[]
+    uint32_t tb[kCb], s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) {
+      const uint32_t b = tid * kCb + k;
+      tb[k] = b < nbins ? tot[b] : 0u;
+      s += tb[k];
+    }
+    uint32_t all;
+    uint32_t gb = block_excl_scan_n<kGBlock>(s, s_wave[1], all);
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) {
+      const uint32_t b = tid * kCb + k;
+      if (b < nbins) {
+        if (c == 0 && a.counts) a.counts[b] = tb[k];
+        base[b] += gb;
+      }
+      gb += tb[k];
+    }
+  } else {  // the wave-level scan of (1) completed across waves
+    uint32_t gb = gs_incl - gs_own;
+#pragma unroll
+    for (uint32_t w = 0; w < kW; ++w) gb += w < wave ? s_wave[1][w] : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kCb; ++k) {
+      const uint32_t b = tid * kCb + k;
+      if (b < nbins) {
+        if (c == 0 && a.counts) a.counts[b] = tk[k];
+        base[b] = pk[k] + gb;
+      }
+      gb += tk[k];
+    }
+  }
+  if (!perm) {
+    zero_next();
+    return;
+  }
+  uint32_t ctotal = chunk_scan_end();
+  for (uint32_t cbase = pbeg;;) {
+    lds_sync();  // (B3)
+    // ---- (3) per bin: perm position of chunk slot j of bin b = tot[b] + j; advance past the bin.
+    // Local counting sort of the chunk's packets into LDS.
     for (uint32_t b = tid; b < nbins; b += kGBlock) {
       const uint32_t st = cnt[b];                                // wave 0's start = the bin's start
       const uint32_t en = b + 1 < nbins ? cnt[b + 1] : ctotal;
       tot[b] = base[b] - st;
       base[b] += en - st;
     }
+    const uint32_t wbase = cbase + wave * (64u * kGRounds);
 #pragma unroll
     for (int r = 0; r < kGRounds; ++r) {
       if (br[r] != 0xffffffffu) {
@@ -2482,13 +2539,20 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
         sslot[j] = (bin << 12) | (wbase - cbase + r * 64u + lane);
       }
     }
-    lds_sync();
-    // coalesced output: consecutive sorted slots of one bin are consecutive perm entries.  The
-    // next chunk's first writes to sidx/sbin/tot come after the barriers of its scan.
+    lds_sync();  // (B4)
+    // ---- (4) coalesced output
     for (uint32_t j = tid; j < ctotal; j += kGBlock) {
       const uint32_t sv = sslot[j];
       a.perm[tot[sv >> 12] + j] = cbase + (sv & 0xfffu);
     }
+    cbase += kChunk;
+    if (cbase >= pend) break;
+    // the next chunk (its backends are loaded): ranks, then the scan's two halves
+    rank_chunk(cbase);
+    lds_sync();
+    chunk_scan_begin();
+    lds_sync();
+    ctotal = chunk_scan_end();
   }
   zero_next();
 }

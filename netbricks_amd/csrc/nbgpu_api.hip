@@ -1709,8 +1709,9 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
   ha.part_pkts = part_pkts;
   ha.n_parts = n_parts;
   ha.part_hist = gs->rows;
-  if ((rc = launch_hist(ha, s))) return rc;
   const int scan = pick_group_scan(nbins, n_parts);
+  ha.hist16 = scan == kScanDirect && part_pkts < 65536 ? 1u : 0u;  // packed rows for the direct prefix
+  if ((rc = launch_hist(ha, s))) return rc;
   if (scan == kScanKernel) {
     ScanArgs sa{};
     sa.part_hist = gs->rows;
@@ -1732,7 +1733,7 @@ int ring_group_locked(nbg_ring* r, uint64_t ticket, uint32_t* d_perm, uint32_t* 
   ga.part_hist = gs->rows;
   ga.part_prefix = gs->prefix;
   ga.totals = gs->totals;
-  ga.hist16 = 0;
+  ga.hist16 = ha.hist16;
   ga.counts = d_counts;
   ga.perm = d_perm;
   return launch_group(ga, scan, s, group_compact(nbins, true));
@@ -1797,6 +1798,7 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
     ha.part_pkts = part_pkts;
     ha.n_parts = static_cast<uint32_t>((n_pkts + part_pkts - 1) / part_pkts);
     ha.part_hist = rows;
+    ha.hist16 = part_pkts < 65536 ? 1u : 0u;  // the direct prefix (scan == kScanDirect here)
     GroupArgs& ga = gm.g[j];
     ga.backend = backend;
     ga.n_pkts = static_cast<uint32_t>(n_pkts);
@@ -1805,7 +1807,7 @@ int ring_group_burst_locked(nbg_ring* r, uint64_t first, uint32_t n, uint32_t* c
     ga.n_parts = ha.n_parts;
     ga.part_pkts = part_pkts;
     ga.part_hist = rows;
-    ga.hist16 = 0;
+    ga.hist16 = ha.hist16;
     ga.counts = d_counts[j];
     ga.perm = d_perm[j];
   }

@@ -167,7 +167,9 @@ struct HistArgs {
   uint32_t nb;
   uint32_t part_pkts;
   uint32_t n_parts;
-  uint32_t* part_hist;      // [n_parts][nb+1], every entry stored
+  uint32_t* part_hist;      // [n_parts][nb+1] (hist16: [n_parts][(nb+2)/2]), every entry stored
+  uint32_t hist16;          // rows of two 16-bit bins per word (partitions < 65536 packets; for the
+                            // group kernel's direct prefix, not for scan_kernel)
 };
 
 // hist_kernel over several batches: blocks [j * per, j * per + h[j].n_parts) count batch j.
