@@ -2313,18 +2313,15 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   constexpr uint32_t kCb = kMaxBins > kGBlock ? kMaxBins / kGBlock : 1u;  // consecutive bins per thread
   const uint32_t hw = a.hist16 ? (nbins + 1) >> 1 : nbins;  // row words
   const uint32_t L = hw >= kGBlock ? 1u : kGBlock / hw;
+  const uint32_t rw0 = tid % hw, rj0 = tid / hw;  // this thread's first (word, row) pair
   uint32_t h[kU];
   uint32_t pk[kCb], tk[kCb];
-  // rows q0, q0 + L, ... of row word w
-  auto load_rows = [&](uint32_t w, uint32_t q0) {
-#pragma unroll
-    for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(q0 + k * L, a.n_parts - 1u) * hw + w) * 4u);
-  };
   if constexpr (SCAN == kScanDirect) {
-    // every thread loads its first (word, row) pair's rows (clamped; a thread past hw * L ignores
-    // them): a load inside a branch makes the compiler wait for all of them at the join, before the
-    // ranks.  More than kGBlock row words (many bins, 32-bit rows) take a second pair later.
-    load_rows(tid % hw, tid / hw);
+    // every thread loads its first (word, row) pair's first kU rows (clamped; a thread past hw * L
+    // ignores them): a load inside a branch makes the compiler wait for all of them at the join,
+    // before the ranks
+#pragma unroll
+    for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(rj0 + k * L, a.n_parts - 1u) * hw + rw0) * 4u);
   } else {
 #pragma unroll
     for (uint32_t k = 0; k < kCb; ++k) {
@@ -2390,8 +2387,24 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   constexpr uint32_t kPer = (kMaxBins * kW + kGBlock - 1) / kGBlock;
   const uint32_t ne = nbins * kW;
   uint32_t ev[kPer], esum = 0, ex = 0;
+  // kPer == 2 * kW (10 bits): a thread's elements are bins 2t and 2t + 1 of every wave's row, one
+  // 32-bit LDS word per wave (the rows are 16-B aligned, cst even)
+  constexpr bool kPair = kPer == 2 * kW;
   auto chunk_scan_begin = [&] {
     esum = 0;
+    if constexpr (kPair) {
+#pragma unroll
+      for (uint32_t w = 0; w < kW; ++w) {
+        const uint32_t v = 2 * tid < nbins ? reinterpret_cast<const uint32_t*>(cnt + w * cst)[tid] : 0u;
+        ev[w] = v & 0xffffu;
+        ev[kW + w] = 2 * tid + 1 < nbins ? v >> 16 : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kPer; ++k) esum += ev[k];
+      ex = wave_incl_scan(esum);
+      if (lane == 63u) s_wave[0][wave] = ex;
+      return;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t e = tid * kPer + k;
@@ -2411,6 +2424,20 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       ctotal += t;
     }
     uint32_t x = wpre + ex - esum;
+    if constexpr (kPair) {
+      uint32_t lo[kW];
+#pragma unroll
+      for (uint32_t w = 0; w < kW; ++w) {  // bin 2t over the waves, then bin 2t + 1
+        lo[w] = x;
+        x += ev[w];
+      }
+#pragma unroll
+      for (uint32_t w = 0; w < kW; ++w) {
+        if (2 * tid < nbins) reinterpret_cast<uint32_t*>(cnt + w * cst)[tid] = lo[w] | (x << 16);
+        x += ev[kW + w];
+      }
+      return ctotal;
+    }
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t e = tid * kPer + k;
@@ -2425,32 +2452,38 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   // ---- (1) prologue sums, the chunk scan's first half
   uint32_t gs_incl = 0, gs_own = 0;  // kScanKernel: this thread's bins' totals, scanned over the wave
   if constexpr (SCAN == kScanDirect) {
-    for (uint32_t t = tid; t < hw * L; t += kGBlock) {
-      const uint32_t rw = t % hw, rj = t / hw;
-      if (t != tid) load_rows(rw, rj);
-      uint32_t pre_lo = 0, pre_hi = 0, all_lo = 0, all_hi = 0;
-      for (uint32_t q0 = rj;;) {
-#pragma unroll
-        for (uint32_t k = 0; k < kU; ++k) {
-          const uint32_t q = q0 + k * L;
-          const uint32_t lo = q < a.n_parts ? (a.hist16 ? h[k] & 0xffffu : h[k]) : 0u;
-          const uint32_t hi = q < a.n_parts && a.hist16 ? h[k] >> 16 : 0u;
-          all_lo += lo;
-          all_hi += hi;
-          pre_lo += q < c ? lo : 0u;
-          pre_hi += q < c ? hi : 0u;
-        }
-        q0 += kU * L;
-        if (q0 >= a.n_parts) break;
-        load_rows(rw, q0);  // more rows than kU per thread (many bins over many partitions)
-      }
+    // (word, row) pair (rw, rj): rows rj, rj + L, ...; the first kU of the first pair's rows are in
+    // h[] (static indices only, so that h stays in registers), any further rows are loaded one by one
+    // (more than kU rows per thread, or more than kGBlock row words: many bins, rare)
+    auto add_row = [&](uint32_t q, uint32_t v, uint32_t (&acc)[4]) {
+      const uint32_t lo = q < a.n_parts ? (a.hist16 ? v & 0xffffu : v) : 0u;
+      const uint32_t hi = q < a.n_parts && a.hist16 ? v >> 16 : 0u;
+      acc[0] += q < c ? lo : 0u;
+      acc[1] += q < c ? hi : 0u;
+      acc[2] += lo;
+      acc[3] += hi;
+    };
+    auto publish = [&](uint32_t rw, const uint32_t (&acc)[4]) {
       const uint32_t b0 = a.hist16 ? 2 * rw : rw;
-      if (pre_lo) atomicAdd(&base[b0], pre_lo);
-      if (all_lo) atomicAdd(&tot[b0], all_lo);
+      atomicAdd(&base[b0], acc[0]);
+      atomicAdd(&tot[b0], acc[2]);
       if (a.hist16 && b0 + 1 < nbins) {
-        if (pre_hi) atomicAdd(&base[b0 + 1], pre_hi);
-        if (all_hi) atomicAdd(&tot[b0 + 1], all_hi);
+        atomicAdd(&base[b0 + 1], acc[1]);
+        atomicAdd(&tot[b0 + 1], acc[3]);
       }
+    };
+    if (tid < hw * L) {
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t k = 0; k < kU; ++k) add_row(rj0 + k * L, h[k], acc);
+      for (uint32_t q = rj0 + kU * L; q < a.n_parts; q += L) add_row(q, ld_u32(a.part_hist, (q * hw + rw0) * 4u), acc);
+      publish(rw0, acc);
+    }
+    for (uint32_t t = tid + kGBlock; t < hw * L; t += kGBlock) {
+      uint32_t acc[4] = {0u, 0u, 0u, 0u};
+      const uint32_t rw = t % hw;
+      for (uint32_t q = t / hw; q < a.n_parts; q += L) add_row(q, ld_u32(a.part_hist, (q * hw + rw) * 4u), acc);
+      publish(rw, acc);
     }
   } else {
 #pragma unroll
@@ -2540,10 +2573,19 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       }
     }
     lds_sync();  // (B4)
-    // ---- (4) coalesced output
-    for (uint32_t j = tid; j < ctotal; j += kGBlock) {
-      const uint32_t sv = sslot[j];
-      a.perm[tot[sv >> 12] + j] = cbase + (sv & 0xfffu);
+    // ---- (4) coalesced output, unrolled: the slot reads, then the dependent base reads, issue back
+    // to back (a loop paid two LDS round trips per iteration)
+    {
+      uint32_t sv[kGRounds], pb[kGRounds];
+#pragma unroll
+      for (int k = 0; k < kGRounds; ++k) sv[k] = sslot[tid + k * kGBlock];  // < kChunk; slots >= ctotal unused
+#pragma unroll
+      for (int k = 0; k < kGRounds; ++k) pb[k] = tot[min(sv[k] >> 12, nbins - 1u)];
+#pragma unroll
+      for (int k = 0; k < kGRounds; ++k) {
+        const uint32_t j = tid + k * kGBlock;
+        if (j < ctotal) a.perm[pb[k] + j] = cbase + (sv[k] & 0xfffu);
+      }
     }
     cbase += kChunk;
     if (cbase >= pend) break;
