@@ -1108,10 +1108,16 @@ def run_rank(args) -> None:
         t0 = time.perf_counter()
         ring = mgs[0].ring(swap_macs=True, stream=streams[0])
         rr = ring._r
+        stamps = []  # (time, batches complete on the ring) at every change seen by the producer
         try:
             posted = grouped = safe = done = 0  # safe: every grouping of posts < safe has run
             last_move, last_state = time.perf_counter(), None
             while grouped < batches:
+                if poll(rr, C.byref(cc)):
+                    raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
+                if cc.value != done:
+                    done = cc.value
+                    stamps.append((time.perf_counter(), done))
                 state = (posted, grouped, safe, done)
                 if state != last_state:
                     last_move, last_state = time.perf_counter(), state
@@ -1120,10 +1126,6 @@ def run_rank(args) -> None:
                     raise RuntimeError(f"ring_path stalled: posted {posted} grouped {grouped} safe {safe} done {done} "
                                        f"ring completed {cc.value} cap {cap} n {n} gburst {gburst} "
                                        f"pending group bursts {sorted(evs)[:4]}")
-                if posted - done >= cap:  # the next input's previous batch (or the oldest slot) may be in flight
-                    if poll(rr, C.byref(cc)):
-                        raise RuntimeError(f"nbg_ring_poll: {nb._lib.last_error()}")
-                    done = cc.value
                 # ... and every post stays groupable: a group burst names tickets among the last 64 posted
                 want = min(batches - posted, slots - (posted - grouped), safe + nbe - posted, cap - (posted - done))
                 if want <= 0:  # the backend[] buffers of the next posts still wait for their grouping
@@ -1163,18 +1165,31 @@ def run_rank(args) -> None:
             groups = [(f + j, ring_res["perm"][q][j], ring_res["cnt"][q][j])
                       for q, lo in enumerate(last_on) if lo is not None for f, c in [lo] for j in range(c)]
             out_check = ring_check(True, rotate, n, batches, lambda i: rd["be"][i % nbe], groups)
-        return wall, float(kms.value), out_check
+        # steady state, as ring_pass measures the ring alone: the slope of ring completions over the
+        # middle three quarters of the run.  Posting is held back by the groupings (a backend[] buffer is
+        # reposted only after the grouping that reads it ran), so the slope is the rate of ring +
+        # grouping together; `wall` adds the ring's start and stop and the last groupings' drain.
+        slope = None
+        if len(stamps) > 8:
+            ts = np.array([x[0] for x in stamps])
+            cs = np.array([x[1] for x in stamps])
+            i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
+            if i1 > i0 and i1 < len(cs):
+                slope = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]))
+        return wall, float(kms.value), out_check, slope
 
     def ring_grouped(batches, n=BATCH, gstreams=RING_GROUP_STREAMS, gburst=RING_GROUP_BURST):
         """variants.ring_in_place_grouped / c4_shard_ring_grouped: ring_path over `batches` batches (the
         ring's buffers warmed by a first short run), whole-job wall time, the ring kernel's own time and
         the output check of the timed run."""
         ring_path(2 * BATCHES_PER_STEP, n=n, gstreams=gstreams, gburst=gburst)
-        wall, kms, chk = ring_path(batches, n=n, gstreams=gstreams, gburst=gburst, check=True)
-        us = wall / batches * 1e6
+        wall, kms, chk, slope = ring_path(batches, n=n, gstreams=gstreams, gburst=gburst, check=True)
+        wall_us = wall / batches * 1e6
+        us = slope * 1e6 if slope else wall_us
         ach_path = n * PATH_BYTES["in_place"] / us / 1e3
         ach = batches * n * CLASSIFY_BYTES["in_place"] / (kms * 1e-3) / 1e9
-        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2), "batches": batches,
+        return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
+                "wall_us_per_batch": round(wall_us, 2), "batches": batches,
                 "pkts_per_batch": n, "path_bytes_per_pkt": PATH_BYTES["in_place"],
                 "path_frac": round(ach_path / HBM_PEAK_GBPS, 4),
                 "group_streams": gstreams, "group_burst": gburst, "working_set_mib": RING_ROTATE * BATCH * SLOT >> 20,
@@ -1183,8 +1198,10 @@ def run_rank(args) -> None:
                 "what": "in place + grouping on the persistent ring: RX bursts posted to the resident classify kernel, "
                         "each burst's grouping enqueued right after the post (nbg_ring_group_burst: a gate kernel "
                         "waits on the side stream for the batches' completion word in HBM, then hist + group co-run "
-                        "with the ring), no host poll; whole-job wall time incl. ring start/stop (path_frac at 82 "
-                        "B/pkt); frac from the ring kernel's HIP-event time"}
+                        "with the ring), no host poll; us_per_batch from the slope of ring completions over the middle "
+                        "3/4 of the run (posting is held back by the groupings: the rate of ring + grouping), "
+                        "wall_us_per_batch the whole job incl. ring start/stop (path_frac at 82 B/pkt); frac from "
+                        "the ring kernel's HIP-event time"}
 
     def timed_ring(steps, warmup, barrier=False):
         """The headline on the ring: `steps` rotations (steps x 8 batches) through ring_path, bracketed
@@ -1195,7 +1212,7 @@ def run_rank(args) -> None:
             dist.barrier()
         sync_all()
         t_start = time.perf_counter()
-        _, kms, _ = ring_path(steps * BATCHES_PER_STEP)
+        _, kms, _, _ = ring_path(steps * BATCHES_PER_STEP)
         sync_all()
         el = time.perf_counter() - t_start
         if barrier and world > 1:
@@ -1331,7 +1348,7 @@ def run_rank(args) -> None:
             sync_all()
             # ring_path's own wall time: ring start, every shard posted and grouped, ring stop (its input
             # restore for the output check runs before that clock starts)
-            el, _, chk = ring_path(n_batches, n=shard_n, gstreams=gstreams, gburst=gburst, check=True)
+            el, _, chk, _ = ring_path(n_batches, n=shard_n, gstreams=gstreams, gburst=gburst, check=True)
             if not chk["ok"]:
                 raise RuntimeError(f"C4 device-resident output check failed on rank {rank}: {chk}")
         else:  # --selftest: no HIP; the timing fields are not a measurement

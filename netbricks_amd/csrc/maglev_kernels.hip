@@ -626,6 +626,49 @@ __device__ __forceinline__ void wave_match_rank(uint32_t bin, bool valid, uint32
   count = __popc(elo) + __popc(ehi);
 }
 
+// N (2..4) consecutive bin bits b .. b + N - 1 of a wave ballot multisplit, four VALU operations per
+// bit: the lane's bit as 0 / ~0 (v_bfe), the wave's ballot of it (v_cmp into an SGPR pair), and per
+// 32-lane half acc |= ballot ^ bit in one v_bitop3 (truth table 0xde over (ballot, acc, bit)).  The
+// compiler's own form of the accumulation took ~6 operations per bit (v_lshlrev + v_cmp for the
+// ballot, two v_xor, v_or3), and the group kernel's ranks are VALU-bound (profiles/r05_group_pmc.txt).
+// The N compares are one asm statement and the bitop3s follow in others: a VALU read of an SGPR that a
+// VALU just wrote needs wait states on gfx950, which the compiler's hazard pass inserts between
+// statements (one s_nop per group instead of one per bit).
+template <int N>
+__device__ __forceinline__ void mismatch_bits(uint32_t bin, int b, uint32_t& mlo, uint32_t& mhi) {
+  static_assert(N >= 2 && N <= 4, "2 to 4 bits per group");
+  uint32_t m[4];
+  unsigned long long q[4];
+#pragma unroll
+  for (int k = 0; k < N; ++k) m[k] = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), b + k, 1));
+  if constexpr (N == 4)
+    asm("v_cmp_ne_u32_e64 %0, 0, %4\n\tv_cmp_ne_u32_e64 %1, 0, %5\n\t"
+        "v_cmp_ne_u32_e64 %2, 0, %6\n\tv_cmp_ne_u32_e64 %3, 0, %7"
+        : "=&s"(q[0]), "=&s"(q[1]), "=&s"(q[2]), "=&s"(q[3])
+        : "v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]));
+  else if constexpr (N == 3)
+    asm("v_cmp_ne_u32_e64 %0, 0, %3\n\tv_cmp_ne_u32_e64 %1, 0, %4\n\tv_cmp_ne_u32_e64 %2, 0, %5"
+        : "=&s"(q[0]), "=&s"(q[1]), "=&s"(q[2])
+        : "v"(m[0]), "v"(m[1]), "v"(m[2]));
+  else
+    asm("v_cmp_ne_u32_e64 %0, 0, %2\n\tv_cmp_ne_u32_e64 %1, 0, %3" : "=&s"(q[0]), "=&s"(q[1]) : "v"(m[0]), "v"(m[1]));
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0xde" : "+v"(mlo) : "s"(static_cast<uint32_t>(q[k])), "v"(m[k]));
+    asm("v_bitop3_b32 %0, %1, %0, %2 bitop3:0xde" : "+v"(mhi) : "s"(static_cast<uint32_t>(q[k] >> 32)), "v"(m[k]));
+  }
+}
+
+// All BITS bin bits (7 or 10): groups of 4, then the remaining 3 or 2
+template <int BITS>
+__device__ __forceinline__ void mismatch_all(uint32_t bin, uint32_t& mlo, uint32_t& mhi) {
+  static_assert(BITS % 4 >= 2 || BITS % 4 == 0, "groups of 2 to 4 bits");
+#pragma unroll
+  for (int b = 0; b + 4 <= BITS; b += 4) mismatch_bits<4>(bin, b, mlo, mhi);
+  if constexpr (BITS % 4 == 3) mismatch_bits<3>(bin, BITS - 3, mlo, mhi);
+  if constexpr (BITS % 4 == 2) mismatch_bits<2>(bin, BITS - 2, mlo, mhi);
+}
+
 // ---- streaming classify (fixed 64-B-aligned slots, u8 LUT <= 65537 entries) -------------------
 //
 // One 512-thread block per CU (persistent).  The block stages the LUT in LDS once with LDS-DMA
@@ -2352,17 +2395,13 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
       const uint32_t bin = min(pre_bin[r], a.nb);  // the sentinel (and any value > nb, as in hist_kernel)
-      // lanes with my bin (and my validity): per bit, keep the lanes whose ballot bit equals mine
+      // lanes with my bin (and my validity): accumulate, per bit, the lanes whose ballot bit differs
+      // from mine; the rest match
       const uint32_t mv = valid ? ~0u : 0u;
       const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
-      uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
-#pragma unroll
-      for (int bit = 0; bit < BITS; ++bit) {
-        const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
-        const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
-        elo &= ~(static_cast<uint32_t>(bb) ^ m);
-        ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
-      }
+      uint32_t mlo = static_cast<uint32_t>(bv) ^ mv, mhi = static_cast<uint32_t>(bv >> 32) ^ mv;
+      mismatch_all<BITS>(bin, mlo, mhi);
+      const uint32_t elo = ~mlo, ehi = ~mhi;
       // every lane of a bin stores the same new count (no branch); lanes past the end use the
       // scratch slot
       const uint32_t slot = valid ? bin : nbins;
@@ -2692,17 +2731,13 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_direct_kernel(Grou
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
       const uint32_t bin = min(pre_bin[r], a.nb);  // the sentinel (and any value > nb, as in hist_kernel)
-      // lanes with my bin (and my validity): per bit, keep the lanes whose ballot bit equals mine
+      // lanes with my bin (and my validity): accumulate, per bit, the lanes whose ballot bit differs
+      // from mine; the rest match
       const uint32_t mv = valid ? ~0u : 0u;
       const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
-      uint32_t elo = ~(static_cast<uint32_t>(bv) ^ mv), ehi = ~(static_cast<uint32_t>(bv >> 32) ^ mv);
-#pragma unroll
-      for (int bit = 0; bit < BITS; ++bit) {
-        const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(bin), bit, 1));  // 0 or ~0
-        const unsigned long long bb = __builtin_amdgcn_ballot_w64(m != 0);
-        elo &= ~(static_cast<uint32_t>(bb) ^ m);
-        ehi &= ~(static_cast<uint32_t>(bb >> 32) ^ m);
-      }
+      uint32_t mlo = static_cast<uint32_t>(bv) ^ mv, mhi = static_cast<uint32_t>(bv >> 32) ^ mv;
+      mismatch_all<BITS>(bin, mlo, mhi);
+      const uint32_t elo = ~mlo, ehi = ~mhi;
       // every lane of a bin stores the same new count (no branch); lanes past the end use the
       // scratch slot
       const uint32_t slot = valid ? bin : nbins;
