@@ -568,6 +568,12 @@ __global__ __launch_bounds__(kBlock, CHAIN ? 1 : 2048 / kBlock) void classify_de
 __device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t byte_off) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
 }
+// Raw buffer resource over `bytes` bytes at p (gfx9 descriptor word 3: CK_BUFFER_RESOURCE_3RD_DWORD):
+// a load past `bytes` returns 0 without touching memory, so the group kernel's loads need neither an
+// index clamp nor a 64-bit address per lane (one 32-bit offset, constant parts in the instruction).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t raw_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
 __device__ __forceinline__ uint32_t ld_u16(const uint16_t* base, uint32_t byte_off) {
   return *reinterpret_cast<const uint16_t*>(reinterpret_cast<const uint8_t*>(base) + byte_off);
 }
@@ -2340,11 +2346,12 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   // ---- entry: the first chunk's backends, then the prologue's loads, all in flight together
   const uint32_t pbeg = c * a.part_pkts;
   const uint32_t pend = min(pbeg + a.part_pkts, a.n_pkts);
+  const __amdgpu_buffer_rsrc_t rbe = raw_rsrc(a.backend, a.n_pkts * 2u);  // packets past the batch read 0
   uint32_t pre_bin[kGRounds];
   {
     const uint32_t wb = pbeg + wave * (64u * kGRounds);
 #pragma unroll
-    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = ld_u16(a.backend, min(wb + r * 64u + lane, a.n_pkts - 1u) * 2u);
+    for (int r = 0; r < kGRounds; ++r) pre_bin[r] = __builtin_amdgcn_raw_buffer_load_b16(rbe, (wb + r * 64u + lane) * 2u, 0, 0);
   }
   // the scheduler keeps the backend loads ahead of the prologue's (vmcnt retires in issue order: the
   // ranks then wait for the backends only)
@@ -2363,8 +2370,9 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
     // every thread loads its first (word, row) pair's first kU rows (clamped; a thread past hw * L
     // ignores them): a load inside a branch makes the compiler wait for all of them at the join,
     // before the ranks
+    const __amdgpu_buffer_rsrc_t rrows = raw_rsrc(a.part_hist, a.n_parts * hw * 4u);  // rows past the last read 0
 #pragma unroll
-    for (uint32_t k = 0; k < kU; ++k) h[k] = ld_u32(a.part_hist, (min(rj0 + k * L, a.n_parts - 1u) * hw + rw0) * 4u);
+    for (uint32_t k = 0; k < kU; ++k) h[k] = __builtin_amdgcn_raw_buffer_load_b32(rrows, ((rj0 + k * L) * hw + rw0) * 4u, 0, 0);
   } else {
 #pragma unroll
     for (uint32_t k = 0; k < kCb; ++k) {
@@ -2415,7 +2423,7 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
     if (cbase + kChunk < pend) {
 #pragma unroll
       for (int r = 0; r < kGRounds; ++r)
-        pre_bin[r] = ld_u16(a.backend, min(wbase + kChunk + r * 64u + lane, a.n_pkts - 1u) * 2u);
+        pre_bin[r] = __builtin_amdgcn_raw_buffer_load_b16(rbe, (wbase + kChunk + r * 64u + lane) * 2u, 0, 0);
     }
   };
   if (perm) rank_chunk(pbeg);
@@ -2513,8 +2521,26 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
     };
     if (tid < hw * L) {
       uint32_t acc[4] = {0u, 0u, 0u, 0u};
+      if (a.hist16 && a.part_pkts * 15u < 65536u) {
+        // packed: the two 16-bit bins of a row word are summed by one 32-bit add, at most 15 rows per
+        // partial sum (15 partitions' counts of one bin fit 16 bits); rows past the last read 0
+        uint32_t pall = 0, ppre = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < kU; ++k) add_row(rj0 + k * L, h[k], acc);
+        for (uint32_t k = 0; k < kU; ++k) {
+          pall += h[k];
+          ppre += rj0 + k * L < c ? h[k] : 0u;
+          if (k % 15u == 14u || k == kU - 1u) {
+            acc[0] += ppre & 0xffffu;
+            acc[1] += ppre >> 16;
+            acc[2] += pall & 0xffffu;
+            acc[3] += pall >> 16;
+            pall = ppre = 0;
+          }
+        }
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kU; ++k) add_row(rj0 + k * L, h[k], acc);
+      }
       for (uint32_t q = rj0 + kU * L; q < a.n_parts; q += L) add_row(q, ld_u32(a.part_hist, (q * hw + rw0) * 4u), acc);
       publish(rw0, acc);
     }
