@@ -2304,8 +2304,10 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
 //     chunk's first packet of the bin, and the local counting sort into LDS; (4) coalesced perm
 //     stores (consecutive sorted slots of one bin are consecutive perm entries).
 // The round-4 form ranked only after the prologue and took 8 barriers per chunk; its phase timeline
-// (tools/gprobe.py, profiles/r05_gprobe.txt) had the row prologue (1.84 us) and the ranks (1.55 us,
-// VALU-bound) one after the other on each block's critical path.
+// (tools/gprobe.py, profiles/r05_gprobe_v1.txt) had the row prologue (1.84 us) and the ranks (1.55 us,
+// VALU-bound) one after the other on each block's critical path.  The ranks take 4 VALU operations per
+// bin bit (mismatch_all), the backends and the rows are raw buffer loads (no clamps, one 32-bit offset
+// per lane): 11,324 instead of 14,954 cycles per C2 block (profiles/r05_gprobe_final.txt).
 // 4 waves per SIMD (two resident blocks per CU, <= 128 VGPRs).
 constexpr int kGroupWaves = 4;
 // BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
@@ -2367,9 +2369,9 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   uint32_t h[kU];
   uint32_t pk[kCb], tk[kCb];
   if constexpr (SCAN == kScanDirect) {
-    // every thread loads its first (word, row) pair's first kU rows (clamped; a thread past hw * L
-    // ignores them): a load inside a branch makes the compiler wait for all of them at the join,
-    // before the ranks
+    // every thread loads its first (word, row) pair's first kU rows (a thread past hw * L ignores
+    // them): a load inside a branch makes the compiler wait for all of them at the join, before the
+    // ranks
     const __amdgpu_buffer_rsrc_t rrows = raw_rsrc(a.part_hist, a.n_parts * hw * 4u);  // rows past the last read 0
 #pragma unroll
     for (uint32_t k = 0; k < kU; ++k) h[k] = __builtin_amdgcn_raw_buffer_load_b32(rrows, ((rj0 + k * L) * hw + rw0) * 4u, 0, 0);
