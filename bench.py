@@ -347,6 +347,20 @@ def gather_results(backend, counts, gbuf, gcounts, rank: int, world: int) -> Non
         dist.gather(c, None, dst=0)
 
 
+def completion_slope(stamps, batches: int):
+    """Seconds per batch of a persistent ring in steady state: the slope of (time, batches complete)
+    stamps over the middle three quarters of a run of `batches` batches (the ramp after the start and
+    the drain at the stop left out).  None when the stamps do not span that window."""
+    if len(stamps) < 2:
+        return None
+    ts = np.array([x[0] for x in stamps], dtype=np.float64)
+    cs = np.array([x[1] for x in stamps], dtype=np.int64)
+    i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
+    if i1 >= len(cs) or i1 <= i0 or cs[i1] == cs[i0]:
+        return None
+    return float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]))
+
+
 def aggregate_frac(total_pkts: float, seconds: float, bytes_per_pkt: int, world: int) -> float:
     """Whole-job HBM fraction: all ranks' algorithmic bytes per second over N x the HBM peak."""
     return round(total_pkts * bytes_per_pkt / seconds / 1e9 / (world * HBM_PEAK_GBPS), 4)
@@ -1051,8 +1065,8 @@ def run_rank(args) -> None:
             fn = os.path.join(os.environ["NBG_BENCH_DUMP"], f"ring_{variant}_n{n}_rot{rotate}_b{batches}.csv")
             np.savetxt(fn, np.stack([(ts - ts[0]) * 1e6, cs], 1), fmt="%.3f,%d", header="us_since_first,completed",
                        comments="")
-        i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
-        us = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]) * 1e6)
+        slope = completion_slope(stamps, batches)
+        us = slope * 1e6 if slope else wall / batches * 1e6
         bpp = CLASSIFY_BYTES[variant]
         ach = n * bpp / us / 1e3
         return {"value": round(n / us, 1), "unit": "Mpps", "us_per_batch": round(us, 2),
@@ -1169,14 +1183,7 @@ def run_rank(args) -> None:
         # middle three quarters of the run.  Posting is held back by the groupings (a backend[] buffer is
         # reposted only after the grouping that reads it ran), so the slope is the rate of ring +
         # grouping together; `wall` adds the ring's start and stop and the last groupings' drain.
-        slope = None
-        if len(stamps) > 8:
-            ts = np.array([x[0] for x in stamps])
-            cs = np.array([x[1] for x in stamps])
-            i0, i1 = np.searchsorted(cs, batches // 8), np.searchsorted(cs, batches - batches // 8)
-            if i1 > i0 and i1 < len(cs):
-                slope = float((ts[i1] - ts[i0]) / (cs[i1] - cs[i0]))
-        return wall, float(kms.value), out_check, slope
+        return wall, float(kms.value), out_check, completion_slope(stamps, batches)
 
     def ring_grouped(batches, n=BATCH, gstreams=RING_GROUP_STREAMS, gburst=RING_GROUP_BURST):
         """variants.ring_in_place_grouped / c4_shard_ring_grouped: ring_path over `batches` batches (the

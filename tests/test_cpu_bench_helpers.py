@@ -141,3 +141,22 @@ def test_emit_line_fails_loudly_over_limit(tmp_path, monkeypatch, capsys):
     full["variants"].update({f"extra_{i}": {"us_per_batch": 1.0, "frac": 0.5} for i in range(400)})
     with pytest.raises(SystemExit):
         bench.emit_line(full)
+
+
+def test_completion_slope_uses_the_middle_of_the_run():
+    """The ring's per-batch time (ring_pass, ring_path): the slope of (time, completed) stamps over the
+    middle three quarters of the run, so a slow start (ring launch, LUT staging) and the drain at the
+    stop do not enter it; None when the stamps do not span that window."""
+    batches = 800
+    stamps = [(0.0, 0)]
+    t = 1e-3  # a 1 ms start-up before the first completion
+    for c in range(1, batches + 1):
+        t += 20e-6 if 100 <= c <= 700 else 50e-6  # steady 20 us per batch in the middle
+        stamps.append((t, c))
+    s = bench.completion_slope(stamps, batches)
+    assert abs(s - 20e-6) < 1e-9
+    # completions seen in bursts (the producer polls between posts): the slope is unchanged
+    burst = [x for x in stamps if x[1] % 4 == 0 or x[1] in (0, batches)]
+    assert abs(bench.completion_slope(burst, batches) - 20e-6) < 1e-9
+    assert bench.completion_slope(stamps[:50], batches) is None
+    assert bench.completion_slope([(0.0, 0)], batches) is None
