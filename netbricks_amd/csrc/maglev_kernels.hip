@@ -2307,7 +2307,10 @@ __global__ __launch_bounds__(64) void group_wide_kernel(GroupArgs a) {
 // (tools/gprobe.py, profiles/r05_gprobe_v1.txt) had the row prologue (1.84 us) and the ranks (1.55 us,
 // VALU-bound) one after the other on each block's critical path.  The ranks take 4 VALU operations per
 // bin bit (mismatch_all), the backends and the rows are raw buffer loads (no clamps, one 32-bit offset
-// per lane): 11,324 instead of 14,954 cycles per C2 block (profiles/r05_gprobe_final.txt).
+// per lane): 11,324 instead of 14,954 cycles per C2 block (profiles/r05_gprobe_final.txt).  Up to 128
+// bins a lane's peers come from a per-wave LDS table of lane masks instead (one OR, one read, one clear
+// per round; 1,069 instead of 1,565 VALU instructions in the kernel): 11,026 cycles
+// (profiles/r05_gprobe_peer.txt), the ranks now wait on the backends' HBM latency.
 // 4 waves per SIMD (two resident blocks per CU, <= 128 VGPRs).
 constexpr int kGroupWaves = 4;
 // BITS: bin bits the multisplit compares (7 for up to 128 bins, else 10); unused high bits are 0
@@ -2343,6 +2346,10 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   uint16_t* cnt = reinterpret_cast<uint16_t*>(tot + nbp);  // [kW][cst]
   uint32_t* sslot = reinterpret_cast<uint32_t*>(cnt + kW * cst);  // [kChunk]
   uint16_t* mycnt = cnt + wave * cst;
+  // <= 128 bins: the lanes that share a lane's bin come from a per-wave table of 64-bit lane masks
+  // [kW][nbins + 1] (slot nbins: lanes past the end), else from the ballot multisplit
+  constexpr bool kPeer = BITS <= 7;
+  unsigned long long* peer = reinterpret_cast<unsigned long long*>(sslot + kChunk) + wave * (nbins + 1);
   const bool perm = a.perm != nullptr;
 
   // ---- entry: the first chunk's backends, then the prologue's loads, all in flight together
@@ -2388,6 +2395,9 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
     base[b] = 0;
     tot[b] = 0;
   }
+  // each wave clears its own peer table (its LDS operations execute in order: no barrier)
+  if constexpr (kPeer)
+    for (uint32_t b = lane; b <= nbins; b += 64) peer[b] = 0;
 
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const uint32_t lt_lo = static_cast<uint32_t>(lt), lt_hi = static_cast<uint32_t>(lt >> 32);
@@ -2405,16 +2415,29 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
       const uint32_t i = wbase + r * 64u + lane;
       const bool valid = i < pend;
       const uint32_t bin = min(pre_bin[r], a.nb);  // the sentinel (and any value > nb, as in hist_kernel)
-      // lanes with my bin (and my validity): accumulate, per bit, the lanes whose ballot bit differs
-      // from mine; the rest match
-      const uint32_t mv = valid ? ~0u : 0u;
-      const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
-      uint32_t mlo = static_cast<uint32_t>(bv) ^ mv, mhi = static_cast<uint32_t>(bv >> 32) ^ mv;
-      mismatch_all<BITS>(bin, mlo, mhi);
-      const uint32_t elo = ~mlo, ehi = ~mhi;
-      // every lane of a bin stores the same new count (no branch); lanes past the end use the
-      // scratch slot
-      const uint32_t slot = valid ? bin : nbins;
+      const uint32_t slot = valid ? bin : nbins;   // lanes past the end use the scratch slot
+      uint32_t elo, ehi;                           // the lanes with my bin (and my validity)
+      if constexpr (kPeer) {
+        // every lane ORs its bit into its slot's mask, reads the mask back and clears it: three LDS
+        // instructions of one wave, executed in order (the compiler barriers keep them in order)
+        unsigned long long* pw = peer + slot;
+        __hip_atomic_fetch_or(pw, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __asm__ volatile("" ::: "memory");
+        const unsigned long long pm = *pw;
+        __asm__ volatile("" ::: "memory");
+        *pw = 0;
+        elo = static_cast<uint32_t>(pm);
+        ehi = static_cast<uint32_t>(pm >> 32);
+      } else {
+        // accumulate, per bin bit, the lanes whose ballot bit differs from mine; the rest match
+        const uint32_t mv = valid ? ~0u : 0u;
+        const unsigned long long bv = __builtin_amdgcn_ballot_w64(valid);
+        uint32_t mlo = static_cast<uint32_t>(bv) ^ mv, mhi = static_cast<uint32_t>(bv >> 32) ^ mv;
+        mismatch_all<BITS>(bin, mlo, mhi);
+        elo = ~mlo;
+        ehi = ~mhi;
+      }
+      // every lane of a bin stores the same new count (no branch)
       const uint32_t prior = mycnt[slot];
       mycnt[slot] = static_cast<uint16_t>(prior + __popc(elo) + __popc(ehi));
       const uint32_t rank = prior + __popc(elo & lt_lo) + __popc(ehi & lt_hi);
@@ -3304,11 +3327,14 @@ int launch_group_wide(const GroupArgs& a, void* stream) {
   return NBG_OK;
 }
 
-// group_kernel: base[nbp] + tot[nbp] u32, cnt[waves][cst] u16, sslot[kChunk] u32 (40 KB at 1001 bins);
+// group_kernel: base[nbp] + tot[nbp] u32, cnt[waves][cst] u16, sslot[kChunk] u32 (40 KB at 1001 bins),
+// and <= 128 bins peer[waves][nbins + 1] u64 (22 KB at 66 bins);
 // compact (group_direct_kernel): run[2][nbp] + tot[nbp] u32, cnt[waves][cst] u16 (28 KB at 1001 bins)
 size_t group_lds(uint32_t nbins, bool compact) {
   const size_t nbp = (nbins + 3) & ~3u, cst = (nbins + 8) & ~7u;
-  return ((compact ? nbp * 3 : nbp * 2 + kChunk) + cst * (kGBlock / 64) / 2) * 4;
+  if (compact) return (nbp * 3 + cst * (kGBlock / 64) / 2) * 4;
+  const size_t peer = nbins <= 128 ? (kGBlock / 64) * (nbins + 1) * 8 : 0;
+  return (nbp * 2 + kChunk + cst * (kGBlock / 64) / 2) * 4 + peer;
 }
 
 // What an in-place persistent ring leaves of a CU's LDS for a co-resident group block (ring_lds(1)
