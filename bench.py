@@ -1823,9 +1823,11 @@ def run_rank(args) -> None:
                     "in flight per wave): removes the LUT's L2 gather from every wave's critical path")
                 variants[f"c3_multi{IMIX_MULTI_K}"] = imix_multi_variant("c3", args.steps, args.warmup)
                 variants[f"c5_multi{IMIX_MULTI_K}"] = imix_multi_variant("c5", args.steps, args.warmup)
-                # C5's classify at the API's maximum of 16 batches per launch (the ramp paid once per 16M
-                # packets; the whole-job rate is the 8-per-launch variant's)
-                variants["c5_multi16"] = imix_multi_variant("c5", args.steps, args.warmup, k=16)
+                # C3 and C5 at the API's maximum of 16 batches per launch (the ramp paid once per 16M
+                # packets; profiles/r05_sweep_multi_burst.txt: C3's path 1-1.5 us per batch faster, C5's slower)
+                if IMIX_MULTI_K != 16:
+                    variants["c3_multi16"] = imix_multi_variant("c3", args.steps, args.warmup, k=16)
+                    variants["c5_multi16"] = imix_multi_variant("c5", args.steps, args.warmup, k=16)
                 sweep_spec = os.environ.get("NBG_BENCH_IMIX_SWEEP", "")  # measurement: "KxS,..."
                 if sweep_spec:
                     isw = {}
