@@ -1,0 +1,15 @@
+# round 5: where the grouped ring's +2.4 us per batch goes: ablation builds of nbg_ring_group_burst
+# (tools/abpatch.py; results wrong by design, timing only): ghist = gate + hist_kernel, no group launch;
+# gnone = gate only.  Bench ring variants (the others skipped), alternating with the tree.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r05_t
+mkdir -p $O
+for r in 0 1; do
+  for v in tree ghist gnone; do
+    L=""; [ $v != tree ] && L=tools/ab/lib_$v.so
+    NBG_LIB_OVERRIDE=$L NBG_BENCH_FULL=$O/full_${v}_$r.json timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-pmc --no-e2e --no-cpu-baseline --no-multi --no-imix --no-c4 > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || exit 1
+  done
+done
+echo "rc=$?" >> $O/done.txt
