@@ -101,6 +101,26 @@ def test_c2_multi_chunk_partitions(torch_cuda, mg65, n):
     _assert_same(got, exp)
 
 
+@pytest.mark.parametrize("nb", [1, 63, 64, 127, 128])
+@pytest.mark.parametrize("n", [2 * 4096 + 37, 300001, (1 << 21) + 777])
+def test_group_bin_widths(torch_cuda, nb, n):
+    """The group kernel's rank forms at their edges: up to 128 bins the per-wave LDS table of lane
+    masks (nb = 127: 128 bins, the table's scratch entry 128 for lanes past the end; nb = 1: every lane
+    of a round in one of two bins), 129 bins the ballot multisplit; batches with a ragged last round,
+    several partitions, and partitions of several chunks (group_by.rs:46-51 FIFO order)."""
+    import netbricks_amd as nb_
+    from netbricks_amd import make_trace
+
+    names = [f"backend-{i}" for i in range(nb)]
+    mg = nb_.Maglev(names, 65537)
+    try:
+        buf, _, _ = make_trace(n, 0, seed=nb * 7919 + n % 1000)
+        lut = orc.lut_build(names, 65537)
+        _assert_same(_run(torch_cuda, mg, buf, n), _oracle(buf, n, lut, nb, stride=64, fixed_len=60))
+    finally:
+        mg.close()
+
+
 def test_many_backends_multi_chunk(torch_cuda):
     """1000 backends at 16.8M packets: hist_kernel + scan_kernel over partitions of several chunks
     (partition counts above 16 bits)."""
