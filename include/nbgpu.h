@@ -250,9 +250,9 @@ int nbg_maglev_classify_desc_multi(nbg_maglev* h, const nbg_desc_batch* batches,
  * NBG_EBUSY: their kernels would queue behind the resident one.  Other handles' batches on the same
  * device co-run in the LDS the ring leaves free (about 30 KB per CU in place): while a
  * ring runs they take the tile-per-wave classify kernel (never the streaming ones or NBG_LUT_LDS,
- * which need a whole CU's LDS), with identical results.  A grouping launch whose block needs more
- * LDS than that (many backends: the 1001-bin group block of C3 takes about 40 KB) waits until the
- * ring's kernel ends.
+ * which need a whole CU's LDS), with identical results.  A grouping launch whose block would need
+ * more LDS than that (many backends: the 1001-bin group block of C3 takes about 40 KB) takes the
+ * compact group kernel while a ring runs (28 KB at 1001 bins), with identical results.
  * Requires <= 255 backends and M <= 65537 (the u8 LUT in LDS).
  * flags: 0 (read only) or NBG_SWAP_MACS (in place).
  * The nbg_ring_* calls of one ring are thread-safe (one mutex per ring).
