@@ -121,6 +121,34 @@ def test_group_bin_widths(torch_cuda, nb, n):
         mg.close()
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_backend_output_alignment(torch_cuda, mg65, shift):
+    """backend[] at any 2-B alignment: the streaming kernel stores a whole tile's backends as 16-B
+    words only into a 16-B-aligned buffer, else one 2-B store per lane (same values)."""
+    from netbricks_amd import make_trace
+
+    torch = torch_cuda
+    n = 300001
+    buf, _, _ = make_trace(n, 0, seed=4242 + shift)
+    dev = torch.device("cuda:0")
+    d_buf = torch.from_numpy(buf.copy()).to(dev)
+    room = torch.zeros(n + 16, dtype=torch.int16, device=dev).view(torch.uint16)
+    be = room[shift:shift + n]
+    r = mg65.group_by(d_buf, n, backend=be)
+    torch.cuda.synchronize()
+    mg65.check()
+    lut = orc.lut_build(NAMES65, 65537)
+    ref = buf.copy()
+    ebe = orc.classify(ref, n, lut, stride=64, fixed_len=60)
+    eperm, ecnt = orc.group(ebe, 65)
+    got = room.view(torch.int16).cpu().numpy().view(np.uint16)
+    np.testing.assert_array_equal(got[shift:shift + n], ebe)
+    assert not got[:shift].any() and not got[shift + n:].any()  # nothing written outside the view
+    np.testing.assert_array_equal(r.perm.view(torch.int32).cpu().numpy().view(np.uint32)[:n], eperm)
+    np.testing.assert_array_equal(r.counts.view(torch.int32).cpu().numpy().view(np.uint32), ecnt)
+    np.testing.assert_array_equal(d_buf.cpu().numpy(), ref)
+
+
 def test_many_backends_multi_chunk(torch_cuda):
     """1000 backends at 16.8M packets: hist_kernel + scan_kernel over partitions of several chunks
     (partition counts above 16 bits)."""

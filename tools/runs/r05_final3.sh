@@ -1,4 +1,5 @@
-# round 5, final tree (peer-mask group ranks, packed backend stores in the streaming classify): GPU suite, smoke, the driver's
+# round 5, final tree (peer-mask group ranks, packed backend stores in the streaming classify): GPU suite, smoke, the
+# driver's bench command (PMC traffic, end-to-end,
 # CPU baseline), kernel traces of the bench and of --multi-only (csv, for tools/kshapes.py), then the two SQ
 # PMC passes of tools/group_kbench.py
 set -o pipefail
