@@ -2350,7 +2350,13 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_kernel(GroupMulti 
   const GroupArgs a = gm.g[bj];
   const uint32_t nbins = a.nb + 1;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-  const uint32_t c = blockIdx.x - bj * gm.per;  // partition of batch bj
+  // partition of batch bj, XCD-aware: the dispatcher deals blocks round-robin over the 8 XCDs, and
+  // neighbouring partitions write adjacent pieces of every bin's perm run (~4 packets per bin and chunk
+  // at 1001 bins), so XCD x takes partitions [x n / 8, (x + 1) n / 8) and the pieces of one line meet
+  // in one L2: C3 hist + scan + group 20.5 -> 19.5 us, 8 per launch 6.8 -> 6.2 us per batch, C2 9.3 ->
+  // 9.1 us (profiles/r05_group_xcd_ab.txt)
+  const uint32_t c_lin = blockIdx.x - bj * gm.per;
+  const uint32_t c = (a.n_parts % 8u == 0u && c_lin < a.n_parts) ? (c_lin % 8u) * (a.n_parts / 8u) + c_lin / 8u : c_lin;
   // The next call accumulates into the other histogram buffer: every block of the grid zeroes a
   // slice of it, last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the
   // first wait for a backend load would also wait for them (the counter retires in issue order).
