@@ -2748,7 +2748,9 @@ __global__ __launch_bounds__(kGBlock, kGroupWaves) void group_direct_kernel(Grou
   const GroupArgs a = gm.g[bj];
   const uint32_t nbins = a.nb + 1;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-  const uint32_t c = blockIdx.x - bj * gm.per;  // partition of batch bj
+  // partition of batch bj, XCD-aware as in group_kernel (neighbouring partitions on one XCD)
+  const uint32_t c_lin = blockIdx.x - bj * gm.per;
+  const uint32_t c = (a.n_parts % 8u == 0u && c_lin < a.n_parts) ? (c_lin % 8u) * (a.n_parts / 8u) + c_lin / 8u : c_lin;
   // The next call accumulates into the other histogram buffer: every block of the grid zeroes a
   // slice of it, last, after its perm stores.  Stores issued earlier would sit in vmcnt, and the
   // first wait for a backend load would also wait for them (the counter retires in issue order).
