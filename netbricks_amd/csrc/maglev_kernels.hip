@@ -1988,7 +1988,10 @@ __global__ __launch_bounds__(kGBlock) void hist_kernel(HistMulti hm) {
   extern __shared__ __align__(16) uint32_t hs[];
   const uint32_t bj = blockIdx.x / hm.per;
   const HistArgs a = hm.h[bj];
-  const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c = blockIdx.x - bj * hm.per;
+  const uint32_t nbins = a.nb + 1, tid = threadIdx.x, c_lin = blockIdx.x - bj * hm.per;
+  // the group kernel's XCD-aware partition order: partition c's backends, read here, are read again by
+  // the group block of partition c on the same XCD, from its L2
+  const uint32_t c = (a.n_parts % 8u == 0u && c_lin < a.n_parts) ? (c_lin % 8u) * (a.n_parts / 8u) + c_lin / 8u : c_lin;
   if (c >= a.n_parts) return;
   const uint32_t pbeg = c * a.part_pkts, pend = min(pbeg + a.part_pkts, a.n_pkts);
   for (uint32_t b = tid; b < nbins; b += kGBlock) hs[b] = 0;
