@@ -184,7 +184,7 @@ def compact_line(full: dict) -> dict:
     if isinstance(variants, dict):
         rows = {}
         for k, v in variants.items():
-            if k in ("ws_sweep", "ring_output_checks", "ring_group_sweep", "imix_multi_sweep"):
+            if k in ("ws_sweep", "ring_output_checks", "ring_group_sweep", "imix_multi_sweep", "imix_output_checks"):
                 continue
             row = _variant_row(k, v, pmc)
             if row is not None:
@@ -199,8 +199,9 @@ def compact_line(full: dict) -> dict:
                             rows[f"ws{rot}_{k}"] = r
         line["variants_fields"] = list(VARIANT_FIELDS)
         line["variants"] = rows
-        if isinstance(variants.get("ring_output_checks"), dict):
-            line["ring_output_checks"] = variants["ring_output_checks"]
+        for ck in ("ring_output_checks", "imix_output_checks"):
+            if isinstance(variants.get(ck), dict):
+                line[ck] = variants[ck]
     if isinstance(pmc, dict) and "error" in pmc:
         line["pmc_error"] = str(pmc["error"])[:200]
     line["full_record"] = FULL_RECORD
@@ -1458,7 +1459,7 @@ def run_rank(args) -> None:
             bufs.append(torch.from_numpy(buf).to(dev))
             offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
             lens.append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
-        imix.update(bufs=bufs, offs=offs, lens=lens,
+        imix.update(bufs=bufs, offs=offs, lens=lens, pristine=[b.clone() for b in bufs], swaps=[0] * len(bufs),
                     c3=[nb.Maglev([f"be{i}" for i in range(1000)], 655373, device=local) for _ in range(S)],
                     lpm=nb.Lpm(routes["reference"] + routes["mixed"], device=local),
                     gates=[torch.empty(BATCH, dtype=torch.uint16, device=dev) for _ in range(S)],
@@ -1472,6 +1473,7 @@ def run_rank(args) -> None:
         k = g % IMIX_BATCHES
         st = sts[j] if stream is None else stream
         if cfg == "c3":
+            x["swaps"][k] += 1
             x["c3"][j].group_by(x["bufs"][k], BATCH, offsets=x["offs"][k], lens=x["lens"][k], owned_windows=True,
                                 bounds_check=False, defer_group=defer, stream=st, **x["c3out"][j])
         else:
@@ -1533,7 +1535,7 @@ def run_rank(args) -> None:
         per-batch outputs, one nbg_desc_batch array per (config, k, stream)."""
         x = imix_setup()
         x.setdefault("marr", {})
-        x.setdefault("mkeep", [])
+        x.setdefault("mout", {})
         if ("c3", k, ms - 1) in x["marr"]:
             return x
         from netbricks_amd._lib import NbgDescBatch
@@ -1542,14 +1544,17 @@ def run_rank(args) -> None:
             x["bufs"].append(torch.from_numpy(buf).to(dev))
             x["offs"].append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
             x["lens"].append(torch.from_numpy(ln.view(np.int16)).to(dev).view(torch.uint16))
+            x["pristine"].append(x["bufs"][-1].clone())
+            x["swaps"].append(0)
         for cfg, nbins in (("c3", 1001), ("c5", N_BACKENDS + 1)):
             for j in range(ms):
                 arr = (NbgDescBatch * k)()
+                x["mout"][(cfg, k, j)] = []
                 for q in range(k):
                     i = j * k + q
                     o = [torch.empty(BATCH, dtype=torch.uint16, device=dev), torch.empty(BATCH, dtype=torch.uint32, device=dev),
                          torch.empty(nbins, dtype=torch.uint32, device=dev), torch.empty(BATCH, dtype=torch.uint16, device=dev)]
-                    x["mkeep"].append(o)
+                    x["mout"][(cfg, k, j)].append(o)
                     arr[q] = NbgDescBatch(x["bufs"][i].data_ptr(), x["offs"][i].data_ptr(), x["lens"][i].data_ptr(), BATCH,
                                           o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(),
                                           o[3].data_ptr() if cfg == "c5" else None)
@@ -1560,6 +1565,8 @@ def run_rank(args) -> None:
         x = imix
         flags = NBG_OWNED_WINDOWS | (NBG_DEFER_GROUP if defer else 0)
         if cfg == "c3":
+            for q in range(k):  # every batch of the call has its MACs swapped in place once more
+                x["swaps"][j * k + q] += 1
             rc = clib.nbg_maglev_classify_desc_multi(x["c3"][j]._h, x["marr"][("c3", k, j)], k, flags | NBG_SWAP_MACS,
                                                      stream)
         else:
@@ -1567,6 +1574,45 @@ def run_rank(args) -> None:
         if rc:
             from netbricks_amd._lib import last_error
             raise RuntimeError(f"{cfg} multi call: {rc} {last_error()}")
+
+    def mac_swapped(buf, off):
+        """buf with the MACs of every frame (bytes [off, off + 12)) swapped: what an odd number of
+        in-place classify calls leaves (the IMIX frames are all >= 14 B)."""
+        o = off.to(torch.int64).unsqueeze(1)
+        ar = torch.arange(12, device=dev, dtype=torch.int64)
+        dst = (o + ar).reshape(-1)
+        src = (o + torch.cat([ar[6:], ar[:6]])).reshape(-1)
+        out = buf.clone()
+        out[dst] = buf[src]
+        return out
+
+    def imix_output_check(cfg, k, ms):
+        """After an IMIX multi pass: every batch's outputs of its stream's last multi call (backend, perm,
+        counts, and the chain's gate) against the single-batch HIP path (nbg_maglev_classify_device_ex /
+        nbg_chain_lpm_maglev_device, read only) on the same input, and every input's bytes against its
+        pristine copy (C3: MACs swapped iff the pass and earlier ones swapped it an odd number of times;
+        C5: untouched)."""
+        x = imix
+        sync_all()
+        bad = []
+        for j in range(ms):
+            for q, o in enumerate(x["mout"][(cfg, k, j)]):
+                i = j * k + q
+                if cfg == "c3":
+                    r = x["c3"][j].group_by(x["bufs"][i], BATCH, offsets=x["offs"][i], lens=x["lens"][i],
+                                            owned_windows=True, swap_macs=False, bounds_check=False, stream=sts[j])
+                    ref = (r.backend, r.perm, r.counts)
+                    exp = mac_swapped(x["pristine"][i], x["offs"][i]) if x["swaps"][i] % 2 else x["pristine"][i]
+                else:
+                    r = nb.chain_lpm_maglev(mgs[j], x["lpm"], x["bufs"][i], BATCH, offsets=x["offs"][i],
+                                            lens=x["lens"][i], owned_windows=True, bounds_check=False, stream=sts[j])
+                    ref = (r.backend, r.perm, r.counts, r.gate)
+                    exp = x["pristine"][i]
+                sync_all()
+                same = all(torch.equal(a[:b.numel()], b) for a, b in zip(o, ref))
+                if not same or not torch.equal(x["bufs"][i], exp):
+                    bad.append(i)
+        return {"ok": not bad, "batches": k * ms, "bad_batches": bad[:8]}
 
     def imix_multi_variant(cfg, steps, warmup, k=IMIX_MULTI_K, ms=IMIX_MULTI_STREAMS):
         """C3 / C5 with k IMIX batches of 1M per call on ms streams (whole-job rate), then the
@@ -1599,9 +1645,10 @@ def run_rank(args) -> None:
             m.check()
         kus = float(kt.ms().mean()) * 1e3
         kt.close()
+        check = imix_output_check(cfg, k, ms)
         cb = C3_BYTES if cfg == "c3" else C5_BYTES
         ach = k * BATCH * cb["classify"] / kus / 1e3
-        return {"value": round(k * BATCH * calls / el / 1e6, 1), "unit": "Mpps",
+        return {"output_check": check, "value": round(k * BATCH * calls / el / 1e6, 1), "unit": "Mpps",
                 "ms_per_batch": round(el / (calls * k) * 1e3, 5), "batches_per_launch": k, "streams": ms,
                 "avg_launch_us": round(kus, 2), "classify_us_per_batch": round(kus / k, 2),
                 "classify_bytes_per_pkt": cb["classify"], "path_bytes_per_pkt": cb["path"],
@@ -1828,6 +1875,10 @@ def run_rank(args) -> None:
                 if IMIX_MULTI_K != 16:
                     variants["c3_multi16"] = imix_multi_variant("c3", args.steps, args.warmup, k=16)
                     variants["c5_multi16"] = imix_multi_variant("c5", args.steps, args.warmup, k=16)
+                ichecks = [v["output_check"] for name_, v in variants.items()
+                           if name_.startswith(("c3_multi", "c5_multi")) and isinstance(v, dict) and "output_check" in v]
+                variants["imix_output_checks"] = {"passes": len(ichecks), "ok": all(c["ok"] for c in ichecks),
+                                                  "batches": sum(c["batches"] for c in ichecks)}
                 sweep_spec = os.environ.get("NBG_BENCH_IMIX_SWEEP", "")  # measurement: "KxS,..."
                 if sweep_spec:
                     isw = {}

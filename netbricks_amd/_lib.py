@@ -113,6 +113,15 @@ SIGNATURES = {
 }
 
 
+# diagnostics the library exports beside include/nbgpu.h (tests only; not part of the C-ABI)
+DEBUG_SIGNATURES = {
+    "nbg_debug_set_group_compact": (C.c_int, [C.c_int]),
+    "nbg_debug_group_lds": (C.c_uint64, [C.c_uint32, C.c_int]),
+    "nbg_debug_lds_beside_ring": (C.c_uint64, []),
+    "nbg_debug_hold_cus": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+}
+
+
 class NbgError(RuntimeError):
     def __init__(self, code: int, where: str):
         self.code = code
@@ -133,6 +142,11 @@ def _load() -> C.CDLL:
             raise ImportError(f"{LIB_PATH}: missing {name}")
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in DEBUG_SIGNATURES.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.restype = res
+            fn.argtypes = args
     return lib
 
 

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "nbgpu_internal.h"
@@ -3374,12 +3375,33 @@ size_t group_lds(uint32_t nbins, bool compact) {
   return (nbp * 2 + kChunk + cst * (kGBlock / 64) / 2) * 4 + peer;
 }
 
-// What an in-place persistent ring leaves of a CU's LDS for a co-resident group block (ring_lds(1)
-// of 160 KiB, less allocation granularity and a hist_kernel block's share).
-constexpr size_t kGroupLdsBesideRing = 26u * 1024u;
+// What an in-place persistent ring leaves of a CU's LDS for one co-resident group block: 160 KiB less
+// the ring block's LDS, rounded up to the allocation granule (one ring block per CU; the grouping's
+// hist and group kernels run in stream order, so one group block is what must fit beside it).
+constexpr size_t kLdsGranule = 512u;
+size_t group_lds_beside_ring() {
+  const size_t ring = (ring_lds(1) + kLdsGranule - 1) / kLdsGranule * kLdsGranule;
+  return 160u * 1024u - ring;
+}
+
+// The grouping beside a running ring takes the compact kernel when the default one's block would not
+// fit in what the ring leaves.  The compact block fits for every bin count the group kernels take
+// (<= 1024 bins: group_lds(1024, true) = 28,800 B, checked by tests/test_cpu_wrapper.py through
+// nbg_debug_group_lds); a block that did not would simply wait for the ring to end (stop or idle
+// exit), never deadlock: the ring completes its batches without the grouping.
+// g_group_compact: -1 = that rule, 0 / 1 = forced (tests and measurements: nbg_debug_set_group_compact,
+// or NBG_GROUP_COMPACT read once at the first grouping).
+std::atomic<int> g_group_compact{-2};
 bool group_compact(uint32_t nbins, bool ring_running) {
-  if (const char* e = std::getenv("NBG_GROUP_COMPACT")) return std::atoi(e) != 0;  // tests and measurements
-  return ring_running && group_lds(nbins, false) > kGroupLdsBesideRing;
+  int f = g_group_compact.load(std::memory_order_relaxed);
+  if (f == -2) {
+    const char* e = std::getenv("NBG_GROUP_COMPACT");
+    int v = e ? (std::atoi(e) != 0) : -1;
+    g_group_compact.compare_exchange_strong(f, v);
+    f = g_group_compact.load(std::memory_order_relaxed);
+  }
+  if (f >= 0) return f != 0;
+  return ring_running && group_lds(nbins, false) > group_lds_beside_ring();
 }
 
 // Default: sum the partition histograms from L2 inside the group kernel while the rows are
@@ -3470,3 +3492,13 @@ extern "C" int nbg_debug_hold_cus(uint32_t blocks, uint32_t lds_bytes, uint32_t 
                      static_cast<uint64_t>(us) * 100u, static_cast<uint32_t*>(nullptr));
   return hipGetLastError() == hipSuccess ? NBG_OK : NBG_EIO;
 }
+
+// Diagnostics (not in include/nbgpu.h; tests only, no GPU needed): force the compact group kernel
+// (mode 1), the default one (0) or the library's rule (-1); and the LDS sizes the rule compares.
+extern "C" int nbg_debug_set_group_compact(int mode) {
+  if (mode < -1 || mode > 1) return NBG_EINVAL;
+  nbg::g_group_compact.store(mode);
+  return NBG_OK;
+}
+extern "C" uint64_t nbg_debug_group_lds(uint32_t nbins, int compact) { return nbg::group_lds(nbins, compact != 0); }
+extern "C" uint64_t nbg_debug_lds_beside_ring(void) { return nbg::group_lds_beside_ring(); }

@@ -1377,6 +1377,8 @@ struct nbg_ring {
   uint32_t calls = 0;
   bool leaked = false;                 // the kernel did not end at stop: every call returns NBG_EBUSY
   bool stopping = false;               // nbg_ring_stop has begun: posts are refused
+  bool stopped = false;                // nbg_ring_stop has finished: a repeat stop returns stop_rc, touching nothing
+  int stop_rc = NBG_OK;
   hipStream_t stream = nullptr;        // the ring kernel's (private, highest priority)
   hipEvent_t ev_start = nullptr, ev_end = nullptr;  // around the kernel on `stream` (its duration)
   size_t hbytes = 0, dbytes = 0;       // the pinned host ring and the uncached device ring
@@ -1877,6 +1879,8 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   r->posted = r->units = r->completed = 0;
   r->ended = false;
   r->stopping = false;
+  r->stopped = false;
+  r->stop_rc = NBG_OK;
   r->rec.assign(r->slots, {nullptr, 0});
   std::memset(r->host, 0, r->hbytes);
   {
@@ -2020,6 +2024,15 @@ int nbg_ring_stop(nbg_ring* r) {
   if (!r) return set_error(NBG_EINVAL, "ring_stop: null ring");
   std::unique_lock<std::mutex> lk(r->mu);
   if (r->leaked) return ring_leaked_error();
+  // a repeat stop (or a stale one from another thread) reports the first stop's result: the ring is
+  // already in the handle's spare or dead list and must not be detached or listed twice
+  while (r->stopping && !r->stopped && !r->leaked) {  // another thread's stop is draining the kernel
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    lk.lock();
+  }
+  if (r->leaked) return ring_leaked_error();
+  if (r->stopped) return r->stop_rc ? set_error(r->stop_rc, "ring_stop: already stopped (%d)", r->stop_rc) : NBG_OK;
   DeviceGuard g(r->device);
   r->stopping = true;  // the lock is released while the kernel drains: no post may follow the stop word
   __atomic_store_n(&const_cast<RingCtl*>(const_cast<volatile RingCtl*>(r->ctl))->stop, 1u, __ATOMIC_RELEASE);
@@ -2030,7 +2043,7 @@ int nbg_ring_stop(nbg_ring* r) {
       // never free memory a running kernel may still read: leak the ring (and the handle's device
       // memory, nbg_maglev_destroy) instead; the device stays marked busy, and every later call on
       // the ring returns NBG_EBUSY without touching the handle
-      r->h->ring = nullptr;
+      if (r->h->ring == r) r->h->ring = nullptr;
       r->h->ring_leaked = true;
       r->leaked = true;
       return set_error(NBG_EBUSY, "ring_stop: the kernel did not end (its memory is leaked, the device stays busy)");
@@ -2055,7 +2068,9 @@ int nbg_ring_stop(nbg_ring* r) {
   if (e != hipSuccess) rc = set_error(NBG_EIO, "ring_stop: %s", hipGetErrorString(e));
   else if (r->completed < r->posted) rc = ring_state_error(r);
   nbg_maglev* h = r->h;
-  h->ring = nullptr;
+  if (h->ring == r) h->ring = nullptr;
+  r->stopped = true;
+  r->stop_rc = rc;
   float ms = -1.f;
   if (e == hipSuccess && hipEventElapsedTime(&ms, r->ev_start, r->ev_end) == hipSuccess) h->ring_kernel_ms = ms;
   ring_close_queues(r);

@@ -96,8 +96,10 @@ def chain_lpm_maglev(mg: Maglev, lpm: Lpm, pkts, n_pkts: int, *, lpm_groups: int
     import torch
 
     dev = pkts.device
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
     if owned_windows and bounds_check:
-        _check_owned("offsets", pkts, offsets, n_pkts)
+        _check_owned("offsets", pkts, offsets, n_pkts, stream)
     if gate is None:
         gate = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
     if backend is None:
@@ -125,9 +127,9 @@ def chain_lpm_maglev_multi(mg: Maglev, lpm: Lpm, batches, *, lpm_groups: int = 3
     chain_lpm_maglev would give it for that batch alone."""
     import torch
 
-    arr, out = mg._desc_batches(batches, group, True, True, owned_windows and bounds_check)
     if stream is None:
         stream = torch.cuda.current_stream(torch.device("cuda", mg.device)).cuda_stream
+    arr, out = mg._desc_batches(batches, group, True, True, owned_windows and bounds_check, stream)
     flags = (NBG_OWNED_WINDOWS if owned_windows else 0) | (NBG_DEFER_GROUP if defer_group else 0)
     check(lib.nbg_chain_lpm_maglev_multi(mg._h, lpm._h, lpm_groups, arr, len(batches), flags, stream),
           "nbg_chain_lpm_maglev_multi")

@@ -62,16 +62,23 @@ def _slot_tail(stride: int, frame_len: int) -> int:
     return max(64, frame_len) if stride >= 64 else frame_len
 
 
-def _check_owned(name: str, pkts, offsets, n_pkts: int) -> None:
+def _check_owned(name: str, pkts, offsets, n_pkts: int, stream=None) -> None:
     """NBG_OWNED_WINDOWS: the kernels read, and in place rewrite, the whole 64-B window at every offset,
-    so each window must lie inside pkts (one device reduction; bounds_check=False skips it for callers
-    that checked their descriptors once)."""
+    so each window must lie inside pkts.  One device reduction, run on `stream` (the raw stream the
+    kernels are launched on; None = torch's current stream), so that offsets the caller wrote there
+    are read in order; its .item() synchronises the host with that stream once per call, which a
+    multi-stream pipeline avoids with bounds_check=False after checking its descriptors once."""
+    import contextlib
+
     import torch
 
     if torch.cuda.is_current_stream_capturing():
         return  # no reduction inside a graph capture: the caller's descriptors are taken as they are
     if n_pkts and offsets is not None:
-        top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
+        ctx = (torch.cuda.stream(torch.cuda.ExternalStream(stream, device=pkts.device)) if stream
+               else contextlib.nullcontext())
+        with ctx:
+            top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
         if top + 64 > pkts.numel():
             raise ValueError(f"{name}: the 64-B owned window at offset {top} runs past the end of pkts "
                              f"({pkts.numel()} B); pass owned_windows=False for frames without a 64-B data room")
@@ -221,7 +228,7 @@ class Maglev:
         _check_dev("offsets", offsets, torch.uint32, n_pkts, dev)
         _check_dev("lens", lens, torch.uint16, n_pkts, dev)
         if owned_windows and bounds_check:
-            _check_owned("offsets", pkts, offsets, n_pkts)
+            _check_owned("offsets", pkts, offsets, n_pkts, stream)
         _check_dev("backend", backend, torch.uint16, n_pkts, dev)
         _check_dev("perm", perm, torch.uint32, n_pkts, dev)
         _check_dev("counts", counts, torch.uint32, self.n_backends + 1, dev)
@@ -281,7 +288,7 @@ class Maglev:
         self._multi_keep = arr
         return [g for g, _ in out] if not records else out
 
-    def _desc_batches(self, batches, group: bool, scatter: bool, gates: bool, owned: bool = False):
+    def _desc_batches(self, batches, group: bool, scatter: bool, gates: bool, owned: bool = False, stream=None):
         """ctypes array of nbg_desc_batch for group_by_desc_multi / chain_lpm_maglev_multi: `batches`
         is a list of (pkts, offsets, lens, n_pkts) device tensors (u8, u32, u16) on this device."""
         import torch
@@ -301,7 +308,7 @@ class Maglev:
             if n_pkts and (offsets is None or lens is None):
                 raise ValueError(f"batch {j}: offsets and lens are required")
             if owned:
-                _check_owned(f"batch {j} offsets", pkts, offsets, n_pkts)
+                _check_owned(f"batch {j} offsets", pkts, offsets, n_pkts, stream)
             backend = torch.empty(max(n_pkts, 1), dtype=torch.uint16, device=dev)
             perm = torch.empty(max(n_pkts, 1), dtype=torch.uint32, device=dev) if group and scatter else None
             counts = torch.empty(self.n_backends + 1, dtype=torch.uint32, device=dev) if group else None
@@ -322,9 +329,9 @@ class Maglev:
         Returns one GroupedBatch per batch."""
         import torch
 
-        arr, out = self._desc_batches(batches, group, scatter, False, owned_windows and bounds_check)
         if stream is None:
             stream = torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream
+        arr, out = self._desc_batches(batches, group, scatter, False, owned_windows and bounds_check, stream)
         flags = ((NBG_SWAP_MACS if swap_macs else 0) | (NBG_OWNED_WINDOWS if owned_windows else 0)
                  | (NBG_DEFER_GROUP if defer_group else 0) | (NBG_WB_PARTIAL if wb_partial else 0))
         check(lib.nbg_maglev_classify_desc_multi(self._h, arr, len(batches), flags, stream),

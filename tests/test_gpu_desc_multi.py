@@ -63,10 +63,12 @@ def _check_maglev(torch, mg, traces, results, dbatches, lut, nb_, swap=True):
         np.testing.assert_array_equal(db[0].cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("owned", [False, True])
 @pytest.mark.parametrize("sizes", [[262161, 0, 1, 5000, 70000], [1 << 20, 1 << 20], [7, 64, 65, 255, 256, 257, 4097, 3]])
-def test_desc_multi_c3(torch_cuda, sizes):
+def test_desc_multi_c3(torch_cuda, sizes, owned):
     """Config C3's shape (1000 backends, M = 655373: hist + scan + group over all batches), ragged
-    batches including an empty one, in-place MAC swap over owned windows."""
+    batches including an empty one, in-place MAC swap: only the frame's bytes rewritten, or
+    (owned=True, NBG_OWNED_WINDOWS, the mode bench.py times) whole 64-B windows."""
     from netbricks_amd import Maglev
 
     torch = torch_cuda
@@ -74,7 +76,7 @@ def test_desc_multi_c3(torch_cuda, sizes):
     lut = orc.lut_build(NAMES1000, 655373)
     tr = _traces(sizes, seed=3000 + len(sizes))
     dbs = [_dev_batch(torch, *t) for t in tr]
-    res = mg.group_by_desc_multi(dbs)
+    res = mg.group_by_desc_multi(dbs, owned_windows=owned)
     torch.cuda.synchronize()
     mg.check()
     _check_maglev(torch, mg, tr, res, dbs, lut, 1000)
@@ -131,11 +133,13 @@ def test_desc_multi_defer_group_other_stream(torch_cuda):
     mg.close()
 
 
+@pytest.mark.parametrize("owned", [False, True])
 @pytest.mark.parametrize("sizes", [[1 << 20, 1000, 262144], [1, 2, 3, 4, 5, 6, 7, 70000],
                                    [65536 + 7 * i for i in range(16)]])
-def test_chain_multi_vs_oracle(torch_cuda, sizes):
+def test_chain_multi_vs_oracle(torch_cuda, sizes, owned):
     """Config C5's chain over several IMIX batches in one launch: gate, backend, perm, counts of every
-    batch as the oracle gives them for that batch alone; packet bytes unchanged."""
+    batch as the oracle gives them for that batch alone; packet bytes unchanged (with and without
+    NBG_OWNED_WINDOWS, the mode bench.py times)."""
     from netbricks_amd import Lpm, Maglev, chain_lpm_maglev_multi
 
     torch = torch_cuda
@@ -153,7 +157,7 @@ def test_chain_multi_vs_oracle(torch_cuda, sizes):
         for k in range(4):
             buf[off.astype(np.int64) + 26 + k] = b[:, k]
     dbs = [_dev_batch(torch, *t) for t in tr]
-    res = chain_lpm_maglev_multi(mg, lpm, dbs)
+    res = chain_lpm_maglev_multi(mg, lpm, dbs, owned_windows=owned)
     torch.cuda.synchronize()
     mg.check()
     rejected = False

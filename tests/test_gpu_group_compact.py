@@ -1,6 +1,6 @@
 """The compact group kernel (group_direct_kernel: wave-segment ranks and direct perm stores, 28 KB of
 LDS at 1001 bins) that the library takes for many bins while a persistent ring runs on the device.
-NBG_GROUP_COMPACT=1 forces it for every grouping; each case is bit-exact against the C oracle's
+nbg_debug_set_group_compact(1) forces it for every grouping; each case is bit-exact against the C oracle's
 per-group FIFO order (operators/group_by.rs:46-51): few and many bins, partitions of one and of many
 4096-packet chunks, rows summed in the group kernel and from scan_kernel, multi-batch launches, and
 counts only."""
@@ -13,8 +13,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def compact(monkeypatch):
-    monkeypatch.setenv("NBG_GROUP_COMPACT", "1")  # read by the library at every group launch
+def compact():
+    from netbricks_amd._lib import lib
+
+    assert lib.nbg_debug_set_group_compact(1) == 0  # every grouping takes the compact kernel
+    yield
+    assert lib.nbg_debug_set_group_compact(-1) == 0  # back to the library's rule
 
 
 def _names(k):

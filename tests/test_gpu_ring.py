@@ -629,3 +629,85 @@ def test_ring_stop_while_producers_blocked(torch_cuda, swap):
         ring2.wait(ring2.post(dd, n, out))
     np.testing.assert_array_equal(_got(torch, out), _expect(buf, n, lut, False)[0])
     mg.close()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_ring_group_many_backends(torch_cuda, compact):
+    """Ring grouping above 128 bins (200 backends: partition rows from hist_kernel's packed 16-bit rows
+    in the XCD-aware partition order, the 10-bit group kernel; compact=True forces the compact
+    group_direct_kernel the library takes for many bins beside a ring), for single tickets
+    (nbg_ring_group) and a burst (nbg_ring_group_burst), with partition counts that are multiples of 8
+    (131,072 packets: 32 partitions) and not (300,000: 74; 5,000: 2; 1); bit-exact against the oracle's
+    per-group FIFO order (operators/group_by.rs:46-51)."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+    from netbricks_amd._lib import lib
+
+    names = [f"be{i}" for i in range(200)]
+    lut = orc.lut_build(names, 65537)
+    mg = nb.Maglev(names, 65537)
+    sizes = [131072, 300000, 5000, 1, 131072, 300000, 5000, 262144]
+    bufs = [nb.make_trace(n, 0, seed=2100 + i)[0] for i, n in enumerate(sizes)]
+    d = [torch.from_numpy(b.copy()).cuda() for b in bufs]
+    outs = [torch.empty(n, dtype=torch.uint16, device="cuda") for n in sizes]
+    perms = [torch.empty(n, dtype=torch.uint32, device="cuda") for n in sizes]
+    counts = [torch.full((201,), 7, dtype=torch.uint32, device="cuda") for _ in sizes]
+    sides = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    assert lib.nbg_debug_set_group_compact(1 if compact else -1) == 0
+    try:
+        with mg.ring(swap_macs=True) as ring:
+            for i in range(4):  # single tickets, grouped right after their posts
+                t = ring.post(d[i], sizes[i], outs[i])
+                ring.group(t, perms[i], counts[i], stream=sides[i % 2])
+            first = None
+            for i in range(4, 8):  # one burst of four
+                t = ring.post(d[i], sizes[i], outs[i])
+                first = t if first is None else first
+            ring.group_burst(first, perms[4:8], counts[4:8], stream=sides[0])
+            ring.wait(len(sizes) - 1)
+            for st in sides:
+                st.synchronize()
+    finally:
+        assert lib.nbg_debug_set_group_compact(-1) == 0
+    for i, n in enumerate(sizes):
+        be, ref = _expect(bufs[i], n, lut, True)
+        exp_perm, exp_cnt = orc.group(be, 200)
+        np.testing.assert_array_equal(_got(torch, outs[i]), be, err_msg=f"batch {i} ({n}) backend")
+        np.testing.assert_array_equal(_np32(torch, perms[i]), exp_perm, err_msg=f"batch {i} ({n}) perm")
+        np.testing.assert_array_equal(_np32(torch, counts[i]), exp_cnt, err_msg=f"batch {i} ({n}) counts")
+        np.testing.assert_array_equal(d[i].cpu().numpy(), ref, err_msg=f"batch {i} bytes")
+    mg.close()
+
+
+def test_ring_stop_twice_and_restart(torch_cuda):
+    """nbg_ring_stop is idempotent: a second stop of the same ring returns the first stop's result and
+    touches neither the handle nor its spare ring (no double free at destroy); the handle then starts
+    a new ring (reusing the stopped one's buffers) that classifies bit-exact, and closes cleanly."""
+    torch = torch_cuda
+    import netbricks_amd as nb
+    from netbricks_amd._lib import lib
+
+    lut = orc.lut_build(NAMES65, 65537)
+    mg = nb.Maglev(NAMES65, 65537)
+    n = 70000
+    buf = nb.make_trace(n, 0, seed=2300)[0]
+    d = torch.from_numpy(buf.copy()).cuda()
+    out = torch.empty(n, dtype=torch.uint16, device="cuda")
+    torch.cuda.synchronize()
+    ring = mg.ring()
+    raw = ring._r
+    ring.wait(ring.post(d, n, out))
+    ring.stop()
+    assert lib.nbg_ring_stop(raw) == 0
+    assert lib.nbg_ring_stop(raw) == 0
+    be, _ = _expect(buf, n, lut, False)
+    np.testing.assert_array_equal(_got(torch, out), be)
+    out2 = torch.empty(n, dtype=torch.uint16, device="cuda")
+    with mg.ring(swap_macs=True) as ring2:
+        ring2.wait(ring2.post(d, n, out2))
+    be2, ref = _expect(buf, n, lut, True)
+    np.testing.assert_array_equal(_got(torch, out2), be2)
+    np.testing.assert_array_equal(d.cpu().numpy(), ref)
+    mg.check()
+    mg.close()
