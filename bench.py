@@ -61,7 +61,8 @@ FRAME = 60
 N_BATCHES = 8           # rotating batches; one step = one rotation (BATCHES_PER_STEP launches)
 BATCHES_PER_STEP = N_BATCHES
 C4_SHARD = BATCH // 8   # config C4: a 1M batch in 8 contiguous shards, one per GPU
-IMIX_BATCHES = 2        # C3 / C5: 2 distinct 1M IMIX batches (2 x 374 MB > the MALL)
+IMIX_BATCHES = 2        # C3 / C5 one call per batch: at least 2 distinct 1M IMIX batches (2 x 374 MB > the MALL),
+                        # one per stream (an in-place swap never runs on a buffer another stream's call holds)
 # batches per launch of the multi-batch variants and their streams (distinct batch groups in
 # flight); the environment overrides are for sweeps (tools/runs/gpu_multi_sweep.sh)
 MULTI_K = int(os.environ.get("NBG_BENCH_MULTI_K", "4"))
@@ -530,7 +531,20 @@ def e2e_block(timeout_s: int = 240):
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     if not lines:
         return {"error": "e2e_bench printed no JSON line"}
-    return json.loads(lines[-1])
+    res = json.loads(lines[-1])
+    # the drop-in operator path (nb_maglev --loop: test/maglev's operator chain with the pipelined GPU
+    # group_by at the reference's 1024-slot queues and 992-packet batches), 1 / 4 / 16 pipelines
+    cmd = ["timeout", "-k", "5", str(timeout_s), sys.executable, os.path.join(ROOT, "tools", "dropin_bench.py")]
+    r = subprocess.run(cmd, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        res["dropin"] = {"error": f"dropin_bench rc={r.returncode}: {r.stderr[-300:]}"}
+    else:
+        d = json.loads(lines[-1])
+        res["dropin"] = d
+        if isinstance(res.get("compact"), dict):
+            res["compact"]["dropin"] = d["dropin"]
+    return res
 
 
 # ---------------------------------------------------------------------------------------------
@@ -1454,7 +1468,7 @@ def run_rank(args) -> None:
             return imix
         routes = json.load(open(os.path.join(ROOT, "tests", "golden", "lpm_routes.json")))
         bufs, offs, lens = [], [], []
-        for b in range(IMIX_BATCHES):
+        for b in range(max(IMIX_BATCHES, S)):
             buf, off, ln = nb.make_trace(BATCH, 1, seed=1000 + b)
             bufs.append(torch.from_numpy(buf).to(dev))
             offs.append(torch.from_numpy(off.view(np.int32)).to(dev).view(torch.uint32))
@@ -1470,7 +1484,9 @@ def run_rank(args) -> None:
 
     def imix_issue(cfg, g, j, stream=None, defer=False, lut_lds=False):
         x = imix
-        k = g % IMIX_BATCHES
+        # stream j's own input: calls in flight on different streams never share a buffer (C3 swaps in
+        # place), and calls on one stream run in order
+        k = j
         st = sts[j] if stream is None else stream
         if cfg == "c3":
             x["swaps"][k] += 1
@@ -1602,16 +1618,17 @@ def run_rank(args) -> None:
                     r = x["c3"][j].group_by(x["bufs"][i], BATCH, offsets=x["offs"][i], lens=x["lens"][i],
                                             owned_windows=True, swap_macs=False, bounds_check=False, stream=sts[j])
                     ref = (r.backend, r.perm, r.counts)
-                    exp = mac_swapped(x["pristine"][i], x["offs"][i]) if x["swaps"][i] % 2 else x["pristine"][i]
                 else:
                     r = nb.chain_lpm_maglev(mgs[j], x["lpm"], x["bufs"][i], BATCH, offsets=x["offs"][i],
                                             lens=x["lens"][i], owned_windows=True, bounds_check=False, stream=sts[j])
                     ref = (r.backend, r.perm, r.counts, r.gate)
-                    exp = x["pristine"][i]
+                # the inputs are shared by the C3 and C5 passes: C3's calls swapped them in place
+                exp = mac_swapped(x["pristine"][i], x["offs"][i]) if x["swaps"][i] % 2 else x["pristine"][i]
                 sync_all()
-                same = all(torch.equal(a[:b.numel()], b) for a, b in zip(o, ref))
-                if not same or not torch.equal(x["bufs"][i], exp):
-                    bad.append(i)
+                if not all(torch.equal(a[:b.numel()], b) for a, b in zip(o, ref)):
+                    bad.append((i, "outputs"))
+                elif not torch.equal(x["bufs"][i], exp):
+                    bad.append((i, "bytes"))
         return {"ok": not bad, "batches": k * ms, "bad_batches": bad[:8]}
 
     def imix_multi_variant(cfg, steps, warmup, k=IMIX_MULTI_K, ms=IMIX_MULTI_STREAMS):

@@ -346,12 +346,19 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
  * not waited for completes that batch first.  Everything a submit names (mbufs, lens, outputs)
  * must stay valid until its wait returns (or the slot is reused).  Replaces a sequence of
  * GroupByProducer::execute calls over host mbufs (operators/group_by.rs:43-55).
+ * A batch of at most 2,048 packets takes the direct path: one kernel launch reads the staged windows
+ * (or, zero-copy, the offsets and frames) out of host memory and stores its results there, with no
+ * DMA copy either way; larger batches are copied H2D / D2H around the kernels.
  */
 #define NBG_HOST_SLOTS 3
 int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                            uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out,
                            uint64_t* ticket);
 int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket);
+/* Non-blocking: *done = 1 when batch `ticket`'s kernels and copies have finished (its host_wait then
+ * returns without waiting on the GPU), 0 otherwise.  A producer that keeps several batches in flight
+ * polls the oldest between its scheduler's other tasks instead of blocking in host_wait. */
+int nbg_maglev_host_query(nbg_maglev* h, uint64_t ticket, int* done);
 
 /*
  * Zero-copy host path: register a host memory region (a DPDK mempool's hugepage memory, as

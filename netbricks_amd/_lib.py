@@ -98,6 +98,7 @@ SIGNATURES = {
     "nbg_maglev_classify_host": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P]),
     "nbg_maglev_host_submit": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_uint32, _P, _P, _P, C.POINTER(C.c_uint64)]),
     "nbg_maglev_host_wait": (C.c_int, [_P, C.c_uint64]),
+    "nbg_maglev_host_query": (C.c_int, [_P, C.c_uint64, C.POINTER(C.c_int)]),
     "nbg_host_register": (C.c_int, [_P, C.c_uint64, C.c_int, C.POINTER(_P)]),
     "nbg_host_unregister": (C.c_int, [_P, C.c_int]),
     "nbg_lpm_create": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P)]),

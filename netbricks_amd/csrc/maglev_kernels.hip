@@ -2168,7 +2168,7 @@ __device__ __forceinline__ uint32_t small_classify(const ClassifyArgs& a, uint32
 }
 
 template <int LUTM, bool F4, int BITS>
-__global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupArgs g) {
+__device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArgs& g) {
   extern __shared__ __align__(16) uint32_t sm[];
   const uint32_t nbins = a.nb + 1, nbp = (nbins + 3) & ~3u;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
@@ -2261,6 +2261,20 @@ __global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupAr
   lds_sync();
   if (g.perm)
     for (uint32_t p = tid; p < a.n_pkts; p += blockDim.x) g.perm[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
+}
+
+// done (nullable): a completion word in pinned host memory (nbg_maglev_host_submit's direct path), set
+// to done_val once every output of the batch is visible to the host: each thread's stores are
+// released at system scope, then, behind the block barrier, one vector store of the word.  The host
+// polls it with plain loads instead of querying an event through the runtime.
+template <int LUTM, bool F4, int BITS>
+__global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupArgs g, uint32_t* done, uint32_t done_val) {
+  small_body<LUTM, F4, BITS>(a, g);
+  if (done) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---- many backends (more than kMaxGroupBins - 1, up to 32767) ------------------------------------
@@ -3326,7 +3340,8 @@ uint32_t lut_tiles(uint64_t m) { return static_cast<uint32_t>((m + kTileEntries 
 
 size_t small_lds(uint32_t nb) { return (kSmallW * (((nb + 1) + 3) & ~3u)) * 4u + kSmallMax * 4u; }
 
-int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream) {
+int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream, uint32_t* done,
+                 uint32_t done_val) {
   const bool b7 = a.nb + 1 <= 128;
   auto fn = wide_lut ? (a.m == 65537u ? (b7 ? small_kernel<kGlobalU16, true, 7> : small_kernel<kGlobalU16, true, 10>)
                                       : (b7 ? small_kernel<kGlobalU16, false, 7> : small_kernel<kGlobalU16, false, 10>))
@@ -3338,7 +3353,7 @@ int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void*
                           static_cast<int>(lds)) != hipSuccess)
     return set_error(NBG_EIO, "small: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
   const uint32_t waves = (a.n_pkts + 255u) / 256u;  // 1..16: a wave per 256 packets
-  hipLaunchKernelGGL(fn, dim3(1), dim3(64 * waves), lds, static_cast<hipStream_t>(stream), a, g);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(64 * waves), lds, static_cast<hipStream_t>(stream), a, g, done, done_val);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "small launch: %s", hipGetErrorString(e));
   return NBG_OK;

@@ -129,6 +129,20 @@ struct nbg_maglev {
     uint16_t* d_backend = nullptr;
     uint32_t* d_perm = nullptr;
     uint32_t* d_counts = nullptr;
+    // device addresses of the pinned buffers above (mapped, fine-grained): a small batch is classified
+    // straight out of h_win / h_len with its results stored straight into h_backend / h_perm /
+    // h_counts / h_mac — one launch, no copy (host_submit's direct path)
+    uint8_t* dh_win = nullptr;
+    uint16_t* dh_len = nullptr;
+    uint8_t* dh_mac = nullptr;
+    uint16_t* dh_backend = nullptr;
+    uint32_t* dh_perm = nullptr;
+    uint32_t* dh_counts = nullptr;
+    // the direct path's completion word (pinned, fine-grained, its own line): the small kernel stores
+    // the batch's ticket there once its outputs are visible; polled with plain loads
+    uint32_t* h_flag = nullptr;
+    uint32_t* dh_flag = nullptr;
+    bool direct = false;        // the slot's batch took the direct path (completion = h_flag)
     hipEvent_t done = nullptr;  // after the slot's D2H copies (on the handle's host stream)
     bool busy = false;
     uint64_t ticket = 0;
@@ -292,11 +306,17 @@ void free_slot_buffers(nbg_maglev::HostSlot& t) {
   t.h_win = t.h_mac = t.d_win = t.d_mac = nullptr;
   t.h_len = t.d_len = t.h_backend = t.d_backend = nullptr;
   t.h_perm = t.h_counts = t.d_perm = t.d_counts = nullptr;
+  t.dh_win = t.dh_mac = nullptr;
+  t.dh_len = t.dh_backend = nullptr;
+  t.dh_perm = t.dh_counts = nullptr;
   t.cap = 0;
 }
 
 void free_host_path(nbg_maglev* h) {
+  if (h->host_compute) (void)hipStreamSynchronize(h->host_compute);  // direct batches record no event
   for (auto& t : h->slots) {
+    if (t.h_flag) (void)hipHostFree(t.h_flag);
+    t.h_flag = t.dh_flag = nullptr;
     if (t.busy && t.done) (void)hipEventSynchronize(t.done);
     t.busy = false;
     free_slot_buffers(t);
@@ -653,10 +673,12 @@ int classify_lag(nbg_maglev* h, ClassifyArgs& a, bool fuse, uint32_t n_parts, ui
 }
 
 // One classify (+ grouping) launch; `lpm` non-null runs the chained test/lpm stage first.
+// small_done (the host path's direct batches): the small kernel's completion word and value; the call
+// fails unless the batch takes the small kernel
 int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len, uint32_t stride,
                     uint16_t fixed_len, uint64_t n_pkts, uint32_t flags, uint16_t* d_backend, uint32_t* d_perm,
                     uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
-                    uint16_t* d_gate, void* stream) {
+                    uint16_t* d_gate, void* stream, uint32_t* small_done = nullptr, uint32_t small_done_val = 0) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
   if (h->ring) return set_error(NBG_EBUSY, "classify: the handle's persistent ring is running (nbg_ring_stop first)");
   if (h->pending && !h->pending_lag)
@@ -793,11 +815,12 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
                    stream_lds(h->nb, !a.swap ? 0 : (a.mac_out ? 2 : 1), true) <= 160u * 1024u;
   const bool fuse = lag && h->pending_lag && h->pending_lg.n_parts <= static_cast<uint32_t>(h->cus);
   if (h->pending_lag && !fuse && (rc = flush_lag(h, static_cast<hipStream_t>(stream)))) return rc;
+  if (small_done && !small) return set_error(NBG_EINVAL, "classify: a completion word needs the small kernel");
   if (small) {
     GroupArgs g{};
     g.perm = d_perm;
     g.counts = d_counts ? d_counts : (d_perm ? h->d_counts : nullptr);
-    return launch_small(a, g, h->wide, stream);
+    return launch_small(a, g, h->wide, stream, small_done, small_done_val);
   }
   const bool tiled = (flags & NBG_LUT_TILED) && h->wide && !lpm;
   if (tiled) {
@@ -2206,17 +2229,32 @@ uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
 
 int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
   if (!t.done) NBG_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+  if (!t.h_flag) {
+    NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_flag), 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *reinterpret_cast<volatile uint32_t*>(t.h_flag) = 0;
+    NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_flag), t.h_flag, 0));
+  }
   if (n <= t.cap) return NBG_OK;
   free_slot_buffers(t);
   const uint64_t cap = std::max<uint64_t>(n, 4096);
   const size_t nbins = h->nb + 1;
   const size_t win_bytes = cap * 80 + 64;  // any window stride, + the last packet's 4th chunk
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_win), win_bytes, hipHostMallocDefault));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_len), cap * 2, hipHostMallocDefault));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_mac), cap * 12, hipHostMallocDefault));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_backend), cap * 2, hipHostMallocDefault));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_perm), cap * 4, hipHostMallocDefault));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_counts), nbins * 4, hipHostMallocDefault));
+  // mapped and fine-grained: the direct path's kernel reads and writes them over PCIe (no stale
+  // lines in the GPU's caches between the slot's batches; the copies of the large-batch path do not
+  // care)
+  constexpr unsigned kPin = hipHostMallocMapped | hipHostMallocCoherent;
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_win), win_bytes, kPin));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_len), cap * 2, kPin));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_mac), cap * 12, kPin));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_backend), cap * 2, kPin));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_perm), cap * 4, kPin));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_counts), nbins * 4, kPin));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_win), t.h_win, 0));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_len), t.h_len, 0));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_mac), t.h_mac, 0));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_backend), t.h_backend, 0));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_perm), t.h_perm, 0));
+  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_counts), t.h_counts, 0));
   NBG_HIP(hipMalloc(&t.d_win, win_bytes));
   NBG_HIP(hipMalloc(&t.d_len, cap * 2));
   NBG_HIP(hipMalloc(&t.d_mac, cap * 12));
@@ -2232,10 +2270,39 @@ int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
 
 // Complete the batch held by slot t: wait for its D2H, hand the results to the caller's buffers
 // and write the swapped MACs into the mbufs (the egress rewrite of MacHeader::swap_addresses).
+// The direct batch in slot t has finished: its completion word holds its ticket.
+bool flag_set(const nbg_maglev::HostSlot& t) {
+  return __atomic_load_n(t.h_flag, __ATOMIC_ACQUIRE) == static_cast<uint32_t>(t.ticket);
+}
+
+// Wait for a direct batch's completion word: spin, then yield; the stream is queried now and then, so
+// a kernel that failed (its word never set) is reported instead of waited for.
+int wait_flag(nbg_maglev* h, const nbg_maglev::HostSlot& t) {
+  for (uint32_t spin = 0; !flag_set(t); ++spin) {
+    if (spin < 2048) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    std::this_thread::yield();
+    if ((spin & 255u) == 0) {
+      const hipError_t e = hipStreamQuery(h->host_compute);
+      if (e != hipSuccess && e != hipErrorNotReady) return set_error(NBG_EIO, "host_wait: %s", hipGetErrorString(e));
+      if (e == hipSuccess && !flag_set(t))
+        return set_error(NBG_EIO, "host_wait: the batch's kernel ended without its completion word");
+    }
+  }
+  return NBG_OK;
+}
+
 int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
   if (!t.busy) return NBG_OK;
   t.busy = false;
-  NBG_HIP(hipEventSynchronize(t.done));
+  if (t.direct) {
+    const int rc = wait_flag(h, t);
+    if (rc) return rc;
+  } else {
+    NBG_HIP(hipEventSynchronize(t.done));
+  }
   const uint64_t n = t.n;
   if (t.backend_out) std::memcpy(t.backend_out, t.h_backend, n * 2);
   if (t.perm_out) std::memcpy(t.perm_out, t.h_perm, n * 4);
@@ -2274,6 +2341,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   int rc = slot_complete(h, t);  // the slot's previous batch, if its wait has not come yet
   if (rc) return rc;
   if ((rc = slot_reserve(h, t, n))) return rc;
+  t.direct = false;
   const bool swap = flags & NBG_SWAP_MACS;
   t.pkt_ptrs = pkt_ptrs;
   t.lens = lens;
@@ -2309,9 +2377,22 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     if (inside.load()) {
       hipStream_t hs = h->host_compute;
       t.swap = false;  // the kernel rewrites the frames itself
+      const bool group = perm_out || counts_out;
+      const uint32_t zflags = (flags & ~(NBG_DEFER_GROUP | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL;
+      if (use_small(n, h->nb + 1, zflags, reg.dev)) {
+        // direct: the one small-kernel launch reads the offsets and lengths out of pinned memory and
+        // stores its results there (no copy on either side)
+        rc = classify_common(h, reg.dev, reinterpret_cast<const uint32_t*>(t.dh_win), t.dh_len, 0, 0, n, zflags,
+                             t.dh_backend, perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr,
+                             nullptr, 0, nullptr, hs, t.dh_flag, static_cast<uint32_t>(tk));
+        if (rc) return rc;
+        t.direct = true;
+        t.busy = true;
+        *ticket = tk;
+        return NBG_OK;
+      }
       NBG_HIP(hipMemcpyAsync(t.d_win, h_off, n * 4, hipMemcpyHostToDevice, hs));
       NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
-      const bool group = perm_out || counts_out;
       rc = nbg_maglev_classify_device_ex(h, reg.dev, reinterpret_cast<const uint32_t*>(t.d_win), t.d_len, 0, 0, n,
                                          (flags & ~(NBG_DEFER_GROUP | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL, t.d_backend,
                                          perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr, nullptr, hs);
@@ -2334,11 +2415,25 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   // not landed (zero windows, sporadically, with many streams in the process).  The host gathers
   // the next batch while this one runs.
   hipStream_t hs = h->host_compute;
+  const bool group = perm_out || counts_out;
+  const uint32_t sflags = (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS;
+  if (use_small(n, h->nb + 1, sflags, t.dh_win)) {
+    // direct: a batch of at most 2,048 packets (NetBricks' own bursts are 32) is classified and
+    // grouped by one small-kernel launch that reads the staged windows out of pinned memory and
+    // stores backend / perm / counts / MAC records there.  The copies' fixed costs (a few us each
+    // on the DMA engines, four to six per batch) were the whole cost of a small batch
+    rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
+                         group ? t.dh_counts : nullptr, swap ? t.dh_mac : nullptr, nullptr, 0, nullptr, hs, t.dh_flag,
+                         static_cast<uint32_t>(tk));
+    if (rc) return rc;
+    t.direct = true;
+    t.busy = true;
+    *ticket = tk;
+    return NBG_OK;
+  }
   NBG_HIP(hipMemcpyAsync(t.d_win, t.h_win, n * win, hipMemcpyHostToDevice, hs));
   NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
-  const bool group = perm_out || counts_out;
-  rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n,
-                                     (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS, t.d_backend,
+  rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n, sflags, t.d_backend,
                                      perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr,
                                      swap ? t.d_mac : nullptr, hs);
   if (rc) return rc;
@@ -2395,6 +2490,30 @@ int nbg_maglev_host_wait(nbg_maglev* h, uint64_t ticket) {
   if (t.ticket != ticket) return NBG_OK;  // its slot was reused: the batch was completed then
   DeviceGuard g(h->device);
   return slot_complete(h, t);
+}
+
+int nbg_maglev_host_query(nbg_maglev* h, uint64_t ticket, int* done) {
+  if (!h || !done) return set_error(NBG_EINVAL, "host_query: null argument");
+  if (ticket == 0 || ticket >= h->next_ticket) return set_error(NBG_EINVAL, "host_query: unknown ticket %llu",
+                                                                (unsigned long long)ticket);
+  auto& t = h->slots[ticket % NBG_HOST_SLOTS];
+  if (t.ticket != ticket || !t.busy) {  // completed by its wait, or by the submit that reused its slot
+    *done = 1;
+    return NBG_OK;
+  }
+  if (t.direct) {  // a plain load of the completion word: no runtime call
+    *done = flag_set(t) ? 1 : 0;
+    return NBG_OK;
+  }
+  DeviceGuard g(h->device);
+  const hipError_t e = hipEventQuery(t.done);
+  if (e == hipErrorNotReady) {
+    *done = 0;
+    return NBG_OK;
+  }
+  if (e != hipSuccess) return set_error(NBG_EIO, "host_query: %s", hipGetErrorString(e));
+  *done = 1;
+  return NBG_OK;
 }
 
 int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,

@@ -279,7 +279,9 @@ bool group_compact(uint32_t nbins, bool ring_running);
 int launch_group_wide(const GroupArgs& a, void* stream);  // nb + 1 > kMaxGroupBins
 // One launch for a batch of at most small_max() packets and at most kMaxGroupBins bins: classify
 // and (when g.perm / g.counts) group.  The batch base must be 16-B aligned.
-int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream);
+// done (nullable): completion word the kernel sets to done_val once its outputs are visible to the host
+int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream, uint32_t* done = nullptr,
+                 uint32_t done_val = 0);
 uint32_t small_max();
 int launch_classify_idx(const ClassifyArgs& a, int grid, void* stream);  // kIdx classify (tile per wave)
 int launch_tiled_lookup(const TileArgs& a, void* stream);

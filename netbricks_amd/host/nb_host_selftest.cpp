@@ -157,6 +157,34 @@ int main(int argc, char** argv) {
       else EXPECT(st.dropped > 0 && delivered + st.dropped == total);
     }
   }
+  {
+    // Backpressure: a batch of 1500 packets of one group stops at the full 1024-slot queue (1023
+    // in), resumes where it stopped once the consumer drained a burst, and ends with every packet
+    // delivered once, in order, nothing dropped.
+    std::vector<nb::MBuf> m(1500);
+    std::vector<nb::MBuf*> batch;
+    std::vector<uint32_t> perm(m.size());
+    for (size_t i = 0; i < m.size(); ++i) {
+      m[i].storage.assign(64, 0);
+      m[i].port_seq = i;
+      batch.push_back(&m[i]);
+      perm[i] = static_cast<uint32_t>(i);
+    }
+    const uint32_t counts[2] = {1500, 0};
+    std::vector<std::shared_ptr<nb::MpscQueue>> qs = {std::make_shared<nb::MpscQueue>(nb::kQueueSlots)};
+    nb::EnqueueStats st;
+    nb::EnqueueCursor cur;
+    EXPECT(!nb::enqueue_grouped_from(batch.data(), perm.data(), counts, qs, st, cur, true));
+    EXPECT(qs[0]->size() == 1023 && cur.k == 1023 && st.stalls == 1 && st.dropped == 0);
+    nb::MBuf* out[32];
+    uint64_t next = 0, rounds = 0;
+    bool done = false, in_order = true;
+    while (next < 1500 && rounds++ < 1000) {
+      if (!done) done = nb::enqueue_grouped_from(batch.data(), perm.data(), counts, qs, st, cur, true);
+      for (uint32_t n = qs[0]->dequeue(out, 32), i = 0; i < n; ++i) in_order &= out[i]->port_seq == next++;
+    }
+    EXPECT(done && in_order && next == 1500 && st.dropped == 0);
+  }
   if (argc > 2) {  // pcap round trip: argv[1] in, argv[2] out
     auto recs = nb::read_pcap(argv[1]);
     EXPECT(!recs.empty());

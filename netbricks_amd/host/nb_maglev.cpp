@@ -2,30 +2,169 @@
 // path, driven from a pcap port (the eth_pcap PMD of the reference's example tests).
 //
 //   nb_maglev --rx in.pcap --tx out.pcap [--backends N | --names a,b,c] [--table 65537]
-//             [--batch 992] [--order order.txt] [--zero-copy 1] [--drop-on-full 1]
+//             [--batch 992] [--depth 3] [--order order.txt] [--zero-copy 1] [--drop-on-full 1]
+//   nb_maglev --rx in.pcap --loop TOTAL [--pipelines P] [...]      (throughput run)
 //
 // Default backends are the reference's ["Larry", "Curly", "Moe"] (main.rs:36).  Prints one
 // JSON line with rx/tx/dropped counts and the per-group packet counts; --order writes the rx
 // index of every transmitted frame (one per line) for order checks.  --zero-copy 1 registers the
 // port's mempool (nbg_host_register), so the GPU reads and rewrites the frames in place over PCIe.
 // The group queues have the reference's 1024 slots; --batch is capped at 992 (whole bursts, at most
-// 1023).  By default the producer waits while a queue could not take a whole batch; --drop-on-full 1
-// pulls regardless and drops on a full queue, as the reference's producer does (group_by.rs:50).
+// 1023).  --depth batches are on the GPU at once (1..3, nbg_maglev_host_submit's slots).  By default
+// the producer pulls a batch only while every queue could take a whole one, and a classified batch's
+// enqueue waits at a full queue (backpressure: nothing is dropped); --drop-on-full 1 pulls whenever
+// the pipeline has room and drops on a full queue, as the reference's producer does (group_by.rs:50).
+//
+// --loop TOTAL: each of P pipelines (--pipelines, default 1) runs on a thread of its own, pinned to
+// one of the process's CPUs, with its own replay port (LoopPort: the capture's frames in a 64k-mbuf
+// pool, received until TOTAL packets, freed by send — the reference's VirtualPort), its own
+// scheduler, its own Maglev handle and stream: the reference's one pipeline per RX queue and core
+// (scheduler/context.rs:55-69,241-255).  The JSON line then gives each pipeline's Mpps (rx packets
+// over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
+// slowest pipeline's time).
+#include <pthread.h>
+#include <sched.h>
+
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "operators.hpp"
 #include "pcap_port.hpp"
 
+namespace {
+
+struct LoopResult {
+  nb::ProducerProfile prof;
+  double seconds = 0, producer_seconds = 0;
+  uint64_t rx = 0, tx = 0, dropped = 0, would_panic = 0, batches = 0, stalls = 0;
+  std::string error;
+};
+
+void pin_to(int k) {
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
+  int seen = 0;
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &allowed)) continue;
+    if (seen++ == k % CPU_COUNT(&allowed)) {
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(c, &one);
+      pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+      return;
+    }
+  }
+}
+
+int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
+             uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines) {
+  const auto recs = nb::read_pcap(rx);
+  std::vector<LoopResult> res(pipelines);
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false};
+  std::vector<std::thread> th;
+  for (int p = 0; p < pipelines; ++p)
+    th.emplace_back([&, p] {
+      LoopResult& r = res[p];
+      bool counted = false;
+      try {
+        pin_to(p);
+        auto port = std::make_shared<nb::LoopPort>(recs, total);
+        auto pool = port->mempool();
+        uint8_t* dev = nullptr;
+        if (zero_copy) nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
+        nb::StandaloneScheduler sched;
+        sched.set_timed(true);
+        auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch,
+                               drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure, depth);
+        ++ready;
+        counted = true;
+        while (!go.load()) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int idle = 0; idle < 2 * static_cast<int>(names.size() + 2);) {
+          const uint64_t before = port->tx_total() + pipe.groups->processed();
+          sched.execute_round();
+          const bool progress = port->tx_total() + pipe.groups->processed() != before;
+          idle = (port->rx_done() && pipe.groups->in_flight() == 0 && !progress) ? idle + 1 : 0;
+        }
+        r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        r.producer_seconds = sched.task_seconds(0);
+        r.rx = port->rx_total();
+        r.tx = port->tx_total();
+        r.dropped = pipe.groups->dropped();
+        r.would_panic = pipe.groups->would_panic();
+        r.batches = pipe.groups->batches();
+        r.stalls = pipe.groups->stalls();
+        r.prof = pipe.groups->profile();
+        if (zero_copy) nb::check(nbg_host_unregister(pool.first, 0), "nbg_host_unregister");
+      } catch (const std::exception& e) {
+        r.error = e.what();
+        if (!counted) ++ready;
+      }
+    });
+  while (ready.load() < pipelines) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  go = true;
+  for (auto& t : th) t.join();
+  double tmax = 0;
+  nb::ProducerProfile pr;  // summed over pipelines
+  uint64_t rx_all = 0, tx_all = 0, dropped = 0, panic = 0, batches = 0, stalls = 0;
+  std::string per, prod, err;
+  for (auto& r : res) {
+    if (!r.error.empty()) err = r.error;
+    tmax = std::max(tmax, r.seconds);
+    rx_all += r.rx;
+    tx_all += r.tx;
+    dropped += r.dropped;
+    panic += r.would_panic;
+    batches += r.batches;
+    stalls += r.stalls;
+    pr.pull += r.prof.pull;
+    pr.submit += r.prof.submit;
+    pr.query += r.prof.query;
+    pr.wait += r.prof.wait;
+    pr.enqueue += r.prof.enqueue;
+    pr.queries += r.prof.queries;
+    char b[64];
+    std::snprintf(b, sizeof b, "%s%.2f", per.empty() ? "" : ", ", r.seconds > 0 ? r.rx / r.seconds / 1e6 : 0.0);
+    per += b;
+    std::snprintf(b, sizeof b, "%s%.4f", prod.empty() ? "" : ", ", r.producer_seconds);
+    prod += b;
+  }
+  if (!err.empty()) {
+    std::fprintf(stderr, "nb_maglev: %s\n", err.c_str());
+    return 1;
+  }
+  std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
+              "\"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
+              "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
+              "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
+              "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
+              pipelines, names.size(), nb::cap_batch(batch), depth, zero_copy ? "true" : "false",
+              drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
+              static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
+              static_cast<unsigned long long>(dropped), static_cast<unsigned long long>(panic),
+              static_cast<unsigned long long>(batches), static_cast<unsigned long long>(stalls), tmax, tmax > 0 ? rx_all / tmax / 1e6 : 0.0, per.c_str(),
+              prod.c_str(), 1e6 * pr.pull / std::max<uint64_t>(batches, 1), 1e6 * pr.submit / std::max<uint64_t>(batches, 1),
+              1e6 * pr.query / std::max<uint64_t>(batches, 1), static_cast<double>(pr.queries) / std::max<uint64_t>(batches, 1),
+              1e6 * pr.wait / std::max<uint64_t>(batches, 1), 1e6 * pr.enqueue / std::max<uint64_t>(batches, 1));
+  return tx_all + dropped + panic == rx_all ? 0 : 1;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
   std::string rx, tx, order;
   std::vector<std::string> names = {"Larry", "Curly", "Moe"};
-  uint64_t table = 65537;
-  uint32_t batch = nb::kMaxGpuBatch;
+  uint64_t table = 65537, loop = 0;
+  uint32_t batch = nb::kMaxGpuBatch, depth = nb::kMaxDepth;
+  int pipelines = 1;
   bool zero_copy = false, drop_on_full = false;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -34,6 +173,9 @@ int main(int argc, char** argv) {
     else if (k == "--order") order = v;
     else if (k == "--table") table = std::strtoull(v.c_str(), nullptr, 10);
     else if (k == "--batch") batch = static_cast<uint32_t>(std::strtoul(v.c_str(), nullptr, 10));
+    else if (k == "--depth") depth = static_cast<uint32_t>(std::strtoul(v.c_str(), nullptr, 10));
+    else if (k == "--loop") loop = std::strtoull(v.c_str(), nullptr, 10);
+    else if (k == "--pipelines") pipelines = std::atoi(v.c_str());
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -48,11 +190,12 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  if (rx.empty()) {
+  if (rx.empty() || pipelines < 1 || pipelines > 64) {
     std::fprintf(stderr, "usage: nb_maglev --rx in.pcap [--tx out.pcap] [--backends N|--names a,b] ...\n");
     return 2;
   }
   try {
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {
@@ -62,14 +205,14 @@ int main(int argc, char** argv) {
     nb::StandaloneScheduler sched;
     sched.set_timed(true);
     auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch,
-                           drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure);
-    // run until the capture is consumed and every group queue has drained
+                           drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure, depth);
+    // run until the capture is consumed, no batch is on the GPU and every group queue has drained
     const auto t0 = std::chrono::steady_clock::now();
     for (int idle = 0; idle < 2 * static_cast<int>(names.size() + 2);) {
       const uint64_t before = pipe.tx->sent + pipe.groups->processed();
       sched.execute_round();
       const bool progress = pipe.tx->sent + pipe.groups->processed() != before;
-      idle = (port->rx_done() && !progress) ? idle + 1 : 0;
+      idle = (port->rx_done() && pipe.groups->in_flight() == 0 && !progress) ? idle + 1 : 0;
     }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!tx.empty()) port->write_tx(tx);
@@ -80,12 +223,13 @@ int main(int argc, char** argv) {
     }
     if (zero_copy && pool.second) nb::check(nbg_host_unregister(pool.first, 0), "nbg_host_unregister");
     std::printf("{\"rx\": %zu, \"tx\": %llu, \"dropped\": %llu, \"would_panic\": %llu, \"backends\": %zu, "
-                "\"zero_copy\": %s, \"max_batch\": %u, \"drop_on_full\": %s, \"seconds\": %.6f, \"mpps\": %.2f, "
-                "\"group_by_seconds\": %.6f, \"merge_send_seconds\": %.6f}\n",
+                "\"zero_copy\": %s, \"max_batch\": %u, \"depth\": %u, \"drop_on_full\": %s, \"seconds\": %.6f, "
+                "\"mpps\": %.2f, \"group_by_seconds\": %.6f, \"merge_send_seconds\": %.6f}\n",
                 port->rx_total(), static_cast<unsigned long long>(pipe.tx->sent),
                 static_cast<unsigned long long>(pipe.groups->dropped()),
                 static_cast<unsigned long long>(pipe.groups->would_panic()), names.size(), zero_copy ? "true" : "false",
-                pipe.groups->max_batch(), drop_on_full ? "true" : "false", secs, secs > 0 ? port->rx_total() / secs / 1e6 : 0.0, sched.task_seconds(0), sched.task_seconds(1));
+                pipe.groups->max_batch(), pipe.groups->depth(), drop_on_full ? "true" : "false", secs,
+                secs > 0 ? port->rx_total() / secs / 1e6 : 0.0, sched.task_seconds(0), sched.task_seconds(1));
   } catch (const nb::NbError& e) {
     std::fprintf(stderr, "nb_maglev: %s\n", e.what());
     return e.code == NBG_ENODEV ? 3 : 1;

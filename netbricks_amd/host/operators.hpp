@@ -14,9 +14,10 @@
 // The per-packet closures of test/maglev (nf.rs:94-106) cannot cross an FFI boundary per
 // packet, so the transform and group functions of this path are *descriptors* (MacSwap,
 // MaglevGroup) that the GPU group_by recognises: its producer task accumulates received
-// bursts into one batch, runs parse + swap + flow hash + LUT lookup + stable grouping in one
-// nbg_maglev_classify_host call, and enqueues the mbufs into the per-group FIFOs in arrival
-// order — exactly what GroupByProducer::execute (group_by.rs:43-55) does packet by packet.
+// bursts into one batch, submits parse + swap + flow hash + LUT lookup + stable grouping as one
+// nbg_maglev_host_submit (up to NBG_HOST_SLOTS batches in flight), and enqueues each finished
+// batch's mbufs into the per-group FIFOs in arrival order — exactly what GroupByProducer::execute
+// (group_by.rs:43-55) does packet by packet.
 #pragma once
 
 #include <algorithm>
@@ -222,23 +223,42 @@ struct RestoreHeader : Batch {
 // it) is freed, never enqueued; every other packet gets save_header_and_offset and then
 // enqueue_one into its group's queue, where a full queue loses it (mpsc_mbuf_queue.rs:91-115).
 struct EnqueueStats {
-  uint64_t dropped = 0, would_panic = 0;
+  uint64_t dropped = 0, would_panic = 0, stalls = 0;
 };
-inline void enqueue_grouped(MBuf* const* batch, const uint32_t* perm, const uint32_t* counts,
-                            std::vector<std::shared_ptr<MpscQueue>>& queues, EnqueueStats& st) {
+// Where the enqueue of a classified batch stands: group g, its j-th packet, perm position k.
+struct EnqueueCursor {
+  size_t g = 0, k = 0;
+  uint32_t j = 0;
+};
+// Enqueue from `c` on.  stall = false: a full queue loses the packet (the reference), and the batch
+// always completes.  stall = true (backpressure): the enqueue stops at the first packet whose queue is
+// full and returns false; the next call resumes there (per-group FIFO order holds: nothing behind the
+// stopped packet is enqueued before it).
+inline bool enqueue_grouped_from(MBuf* const* batch, const uint32_t* perm, const uint32_t* counts,
+                                 std::vector<std::shared_ptr<MpscQueue>>& queues, EnqueueStats& st, EnqueueCursor& c,
+                                 bool stall) {
   const size_t ct = queues.size();
-  size_t k = 0;
-  for (size_t g = 0; g <= ct; ++g) {
-    for (uint32_t j = 0; j < counts[g]; ++j) {
-      MBuf* m = batch[perm[k++]];
-      if (g == ct) {  // mbuf_free (native/zcsi/zcsi.rs:44): the pcap port owns the storage here
+  for (; c.g <= ct; ++c.g, c.j = 0) {
+    for (; c.j < counts[c.g]; ++c.j, ++c.k) {
+      MBuf* m = batch[perm[c.k]];
+      if (c.g == ct) {  // mbuf_free (native/zcsi/zcsi.rs:44): the port owns the storage here
         ++st.would_panic;
         continue;
       }
+      if (stall && queues[c.g]->free_slots() == 0) {
+        ++st.stalls;
+        return false;
+      }
       save_header_and_offset(m);
-      if (!queues[g]->enqueue_one(m)) ++st.dropped;
+      if (!queues[c.g]->enqueue_one(m)) ++st.dropped;
     }
   }
+  return true;
+}
+inline void enqueue_grouped(MBuf* const* batch, const uint32_t* perm, const uint32_t* counts,
+                            std::vector<std::shared_ptr<MpscQueue>>& queues, EnqueueStats& st) {
+  EnqueueCursor c;
+  enqueue_grouped_from(batch, perm, counts, queues, st, c, false);
 }
 
 // The Maglev group function of test/maglev (nf.rs:101-106): lut[flow_hash % M].
@@ -269,12 +289,15 @@ class MaglevGroup {
 constexpr uint32_t kQueueSlots = 1024;
 constexpr uint32_t kMaxGpuBatch = kQueueSlots - 1;
 
-// When the producer pulls the next batch from its port.
-//   kBackpressure (default; a deliberate deviation): only when every group queue has room for a
-//     whole batch, so no packet is ever dropped — packets wait in the port (the NIC's RX ring), as
-//     they do in DPDK when a pipeline falls behind.
-//   kDropOnFull (the reference): always; a packet whose queue is full is lost (GroupByProducer
-//     ignores enqueue_one's result, group_by.rs:50; enqueue_sp refuses it, mpsc_mbuf_queue.rs:91-115).
+// When the producer pulls the next batch from its port, and what a full group queue does.
+//   kBackpressure (default; a deliberate deviation): a batch is pulled only when every group queue has
+//     room for a whole batch, and the enqueue of a classified batch waits at a full queue (resumed by
+//     the producer's next execution, after the consumers ran) instead of dropping: no packet is ever
+//     lost, and per-group FIFO order holds.  Packets wait in the port (the NIC's RX ring) and in the
+//     producer's in-flight batches, as they do in DPDK when a pipeline falls behind.
+//   kDropOnFull (the reference): a batch is pulled whenever the pipeline has a free slot; a packet
+//     whose queue is full is lost (GroupByProducer ignores enqueue_one's result, group_by.rs:50;
+//     enqueue_sp refuses it, mpsc_mbuf_queue.rs:91-115).
 enum class Admission { kBackpressure, kDropOnFull };
 
 // Packets per GPU batch: at most kMaxGpuBatch, whole 32-packet bursts (receive_batch.rs:26).
@@ -287,25 +310,41 @@ inline bool admit_batch(const std::vector<std::shared_ptr<MpscQueue>>& queues, u
   return true;
 }
 
+// Where a GPU producer's time goes (seconds over the run): pulling RX bursts into a batch, the submit
+// (gather + launch), completion polls, the wait (results + MAC write-back), the per-group enqueue.
+struct ProducerProfile {
+  double pull = 0, submit = 0, query = 0, wait = 0, enqueue = 0;
+  uint64_t queries = 0;
+};
+
+// Batches a producer keeps in flight on the GPU (nbg_maglev_host_submit's staging slots).
+constexpr uint32_t kMaxDepth = NBG_HOST_SLOTS;
+
 // GroupBy (group_by.rs:15-113) with the GPU producer: ct queues, get_group(i) for i < ct.  Packets
 // the reference would panic on (the would-panic sentinel group) are freed by the producer and
 // counted (would_panic()); everything else keeps the reference semantics.  max_batch is capped at
 // kMaxGpuBatch (1023; 992 = 31 whole bursts) so that the reference's 1024-slot queues can always
-// take a batch.
+// take a batch.  The producer is pipelined: up to `depth` batches are on the GPU at once
+// (nbg_maglev_host_submit), each delivered to the queues — in submit order, so per-group FIFO order
+// holds across batches — by the first execute() that finds it complete (nbg_maglev_host_query); the
+// scheduler's other tasks (the consumers) run while a batch is on the GPU or waits at a full queue.
 class GroupBy {
  public:
   GroupBy(ParsedMacBatch parent, uint32_t groups, MaglevGroup fn, StandaloneScheduler& sched,
-          uint32_t max_batch = kMaxGpuBatch, Admission admission = Admission::kBackpressure)
+          uint32_t max_batch = kMaxGpuBatch, Admission admission = Admission::kBackpressure,
+          uint32_t depth = kMaxDepth)
       : groups_(groups) {
     if (groups != fn.backends()) throw std::invalid_argument("group_by: groups != Maglev backends");
     if (max_batch == 0) throw std::invalid_argument("group_by: max_batch must be >= 1");
+    if (depth == 0 || depth > kMaxDepth) throw std::invalid_argument("group_by: depth must be 1..NBG_HOST_SLOTS");
     max_batch = cap_batch(max_batch);
     for (uint32_t i = 0; i < groups; ++i) queues_.push_back(std::make_shared<MpscQueue>(kQueueSlots));
-    producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch, admission);
+    producer_ = std::make_shared<Producer>(std::move(parent), std::move(fn), queues_, max_batch, admission, depth);
     task_ = sched.add_task(producer_);
   }
   uint32_t len() const { return groups_; }
   uint32_t max_batch() const { return producer_->max_batch; }
+  uint32_t depth() const { return producer_->depth; }
 
   // get_group(i): RestoreHeader over a ReceiveBatch of the group's MPSC consumer (group_by.rs:102-112).
   std::shared_ptr<RestoreHeader> get_group(uint32_t i) {
@@ -319,54 +358,118 @@ class GroupBy {
     return std::make_shared<RestoreHeader>(std::make_shared<ReceiveBatch>(c));
   }
   uint64_t dropped() const { return producer_->stats.dropped; }
+  uint64_t stalls() const { return producer_->stats.stalls; }
   uint64_t would_panic() const { return producer_->stats.would_panic; }
-  uint64_t processed() const { return producer_->processed; }
+  uint64_t processed() const { return producer_->processed; }  // packets delivered to the queues
+  uint64_t in_flight() const { return producer_->in_flight_pkts; }
+  uint64_t batches() const { return producer_->batches; }
+  const ProducerProfile& profile() const { return producer_->prof; }
 
  private:
+  struct InFlight {
+    std::vector<MBuf*> batch;
+    std::vector<uint8_t*> ptrs;
+    std::vector<uint16_t> lens, backend;
+    std::vector<uint32_t> perm, counts;
+    uint64_t ticket = 0;
+    bool waited = false;  // results and MAC rewrite landed (host_wait returned)
+    EnqueueCursor cur;    // how far its enqueue got
+  };
+
   struct Producer : Executable {
     Producer(ParsedMacBatch p, MaglevGroup f, std::vector<std::shared_ptr<MpscQueue>> q, uint32_t max_batch,
-             Admission admission)
-        : parent(std::move(p)), fn(std::move(f)), queues(std::move(q)), max_batch(max_batch), admission(admission) {}
-    // GroupByProducer::execute (group_by.rs:43-55) for a whole batch: pull bursts until the
-    // batch is full or the port is idle, classify on the GPU, enqueue in per-group FIFO order.
+             Admission admission, uint32_t depth)
+        : parent(std::move(p)), fn(std::move(f)), queues(std::move(q)), max_batch(max_batch), admission(admission),
+          depth(depth), slots(depth) {
+      for (auto& b : slots) {
+        b.batch.reserve(max_batch);
+        b.ptrs.resize(max_batch);
+        b.lens.resize(max_batch);
+        b.backend.resize(max_batch);
+        b.perm.resize(max_batch);
+        b.counts.resize(queues.size() + 1);
+      }
+    }
+    // GroupByProducer::execute (group_by.rs:43-55) for whole batches: deliver every batch the GPU has
+    // finished (oldest first), then pull bursts until a new batch is full or the port is idle and
+    // submit it, if the pipeline has a free slot and the queues admit it.
     void execute() override {
-      if (!admit_batch(queues, max_batch, admission)) return;
-      std::vector<MBuf*> batch;
+      while (n_in_flight) {
+        InFlight& b = slots[head];
+        if (!b.waited) {
+          int done = 0;
+          const auto t0 = Clock::now();
+          check(nbg_maglev_host_query(fn.handle(), b.ticket, &done), "nbg_maglev_host_query");
+          prof.query += since(t0);
+          ++prof.queries;
+          if (!done) break;
+        }
+        if (!deliver(b)) break;  // a full queue (backpressure): resumed at the next execution
+      }
+      if (n_in_flight == depth || !admit_batch(queues, max_batch, admission)) return;
+      const auto t0 = Clock::now();
+      InFlight& b = slots[(head + n_in_flight) % depth];
+      b.batch.clear();
       for (;;) {  // whole bursts only: max_batch is a multiple of kBurst
         parent.parent->act();
-        auto& b = parent.parent->pkts;
-        batch.insert(batch.end(), b.begin(), b.end());
-        const bool idle = b.size() < kBurst;
+        auto& r = parent.parent->pkts;
+        b.batch.insert(b.batch.end(), r.begin(), r.end());
+        const bool idle = r.size() < kBurst;
         parent.parent->done();
-        if (idle || batch.size() + kBurst > max_batch) break;
+        if (idle || b.batch.size() + kBurst > max_batch) break;
       }
-      if (batch.empty()) return;
-      const size_t n = batch.size();
-      ptrs.resize(n);
-      lens.resize(n);
-      backend.resize(n);
-      perm.resize(n);
-      counts.resize(queues.size() + 1);
+      if (b.batch.empty()) return;
+      const size_t n = b.batch.size();
       for (size_t i = 0; i < n; ++i) {
-        ptrs[i] = batch[i]->data();
-        lens[i] = batch[i]->data_len;
+        b.ptrs[i] = b.batch[i]->data();
+        b.lens[i] = b.batch[i]->data_len;
       }
-      check(nbg_maglev_classify_host(fn.handle(), ptrs.data(), lens.data(), n, parent.swap ? NBG_SWAP_MACS : 0u,
-                                     backend.data(), perm.data(), counts.data()),
-            "nbg_maglev_classify_host");
-      enqueue_grouped(batch.data(), perm.data(), counts.data(), queues, stats);
-      processed += n;
+      const auto t1 = Clock::now();
+      prof.pull += std::chrono::duration<double>(t1 - t0).count();
+      check(nbg_maglev_host_submit(fn.handle(), b.ptrs.data(), b.lens.data(), n, parent.swap ? NBG_SWAP_MACS : 0u,
+                                   b.backend.data(), b.perm.data(), b.counts.data(), &b.ticket),
+            "nbg_maglev_host_submit");
+      b.waited = false;
+      b.cur = EnqueueCursor{};
+      prof.submit += since(t1);
+      ++n_in_flight;
+      in_flight_pkts += n;
+      ++batches;
+    }
+    // The enqueue half: results and the MAC rewrite land (host_wait), then the per-group FIFOs.
+    // false: stopped at a full queue (backpressure); the batch stays at the head
+    bool deliver(InFlight& b) {
+      if (!b.waited) {
+        const auto t0 = Clock::now();
+        check(nbg_maglev_host_wait(fn.handle(), b.ticket), "nbg_maglev_host_wait");
+        prof.wait += since(t0);
+        b.waited = true;
+      }
+      const auto t1 = Clock::now();
+      const bool all = enqueue_grouped_from(b.batch.data(), b.perm.data(), b.counts.data(), queues, stats, b.cur,
+                                            admission == Admission::kBackpressure);
+      prof.enqueue += since(t1);
+      if (!all) return false;
+      processed += b.batch.size();
+      in_flight_pkts -= b.batch.size();
+      head = (head + 1) % depth;
+      --n_in_flight;
+      return true;
     }
     ParsedMacBatch parent;
     MaglevGroup fn;
     std::vector<std::shared_ptr<MpscQueue>> queues;
     uint32_t max_batch;
     Admission admission;
-    std::vector<uint8_t*> ptrs;
-    std::vector<uint16_t> lens, backend;
-    std::vector<uint32_t> perm, counts;
+    uint32_t depth;
+    std::vector<InFlight> slots;  // a ring of `depth` batches: [head, head + n_in_flight) are on the GPU
+    uint32_t head = 0, n_in_flight = 0;
+    uint64_t in_flight_pkts = 0;
     EnqueueStats stats;
-    uint64_t processed = 0;
+    uint64_t processed = 0, batches = 0;
+    ProducerProfile prof;
+    using Clock = std::chrono::steady_clock;
+    static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
   };
 
   uint32_t groups_;
@@ -406,11 +509,11 @@ struct MaglevPipeline {
 inline MaglevPipeline maglev(std::shared_ptr<Batch> parent, StandaloneScheduler& s,
                              const std::vector<std::string>& backends, std::shared_ptr<PacketTx> port,
                              uint64_t lut_size = 65537, uint32_t max_batch = kMaxGpuBatch,
-                             Admission admission = Admission::kBackpressure) {
+                             Admission admission = Admission::kBackpressure, uint32_t depth = kMaxDepth) {
   const uint32_t ct = static_cast<uint32_t>(backends.size());
   MaglevGroup lut(backends, lut_size);  // Maglev::new(backends, 65537), nf.rs:90
   auto groups = std::make_shared<GroupBy>(transform(parse_mac(std::move(parent)), MacSwap{}), ct, lut, s,
-                                          max_batch, admission);
+                                          max_batch, admission, depth);
   std::vector<std::shared_ptr<Batch>> outs;
   for (uint32_t i = 0; i < ct; ++i) outs.push_back(groups->get_group(i));  // nf.rs:109
   auto tx = std::make_shared<MergeSend>(outs, std::move(port));

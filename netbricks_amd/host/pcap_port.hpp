@@ -132,4 +132,64 @@ class PcapPort : public PacketRx, public PacketTx {
   std::vector<size_t> tx_index_;
 };
 
+// A replay port for throughput runs: the reference's VirtualPort (interface/port/virt_port.rs:27-52:
+// recv hands out mbufs, send frees them) over a capture's frames.  The frames are copied into one
+// mempool of at least min_pool mbufs (the capture repeated; 2-KiB data rooms, as DPDK's); recv hands
+// out free mbufs in pool order until `total` packets were received, send returns them to the pool
+// (the free list is FIFO, so a frame is received again only after it was sent).
+class LoopPort : public PacketRx, public PacketTx {
+ public:
+  LoopPort(const std::vector<PcapRecord>& recs, uint64_t total, size_t min_pool = 65536, uint32_t data_room = 2048)
+      : total_(total) {
+    if (recs.empty()) throw std::invalid_argument("LoopPort: empty capture");
+    room_ = data_room;
+    for (auto& r : recs) room_ = std::max<size_t>(room_, (r.data.size() + 63) & ~size_t{63});
+    const size_t n = (std::max(min_pool, recs.size()) + recs.size() - 1) / recs.size() * recs.size();
+    mem_.assign(n * room_ + 4096, 0);
+    base_ = mem_.data() + ((4096 - reinterpret_cast<uintptr_t>(mem_.data()) % 4096) % 4096);
+    pool_.resize(n);
+    free_.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      const auto& r = recs[i % recs.size()];
+      MBuf& m = pool_[i];
+      m.room = base_ + i * room_;
+      std::memcpy(m.room, r.data.data(), r.data.size());
+      m.data_len = static_cast<uint16_t>(r.data.size());
+      m.port_seq = i;
+      free_[i] = &m;
+    }
+    tail_ = n;
+  }
+  std::pair<uint8_t*, size_t> mempool() { return {base_, pool_.size() * room_}; }
+  uint32_t recv(MBuf** pkts, uint32_t cap) override {
+    uint32_t n = 0;
+    while (n < cap && received_ < total_ && head_ != tail_) {
+      pkts[n++] = free_[head_++ % free_.size()];
+      ++received_;
+    }
+    return n;
+  }
+  uint32_t send(MBuf** pkts, uint32_t n) override {  // rte_eth_tx_burst + the NIC freeing the mbufs
+    for (uint32_t i = 0; i < n; ++i) {
+      MBuf::write_metadata_slot(pkts[i], kHeaderSlot, 0);
+      free_[tail_++ % free_.size()] = pkts[i];
+    }
+    sent_ += n;
+    return n;
+  }
+  bool rx_done() const { return received_ >= total_; }
+  uint64_t rx_total() const { return received_; }
+  uint64_t tx_total() const { return sent_; }
+  size_t pool_size() const { return pool_.size(); }
+
+ private:
+  uint64_t total_, received_ = 0, sent_ = 0;
+  std::vector<uint8_t> mem_;
+  uint8_t* base_ = nullptr;
+  size_t room_ = 2048;
+  std::vector<MBuf> pool_;
+  std::vector<MBuf*> free_;  // ring: [head_, tail_) are free
+  uint64_t head_ = 0, tail_ = 0;
+};
+
 }  // namespace nb

@@ -72,16 +72,17 @@ def _check_owned(name: str, pkts, offsets, n_pkts: int, stream=None) -> None:
 
     import torch
 
-    if torch.cuda.is_current_stream_capturing():
-        return  # no reduction inside a graph capture: the caller's descriptors are taken as they are
-    if n_pkts and offsets is not None:
-        ctx = (torch.cuda.stream(torch.cuda.ExternalStream(stream, device=pkts.device)) if stream
-               else contextlib.nullcontext())
-        with ctx:
-            top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
-        if top + 64 > pkts.numel():
-            raise ValueError(f"{name}: the 64-B owned window at offset {top} runs past the end of pkts "
-                             f"({pkts.numel()} B); pass owned_windows=False for frames without a 64-B data room")
+    if not n_pkts or offsets is None:
+        return
+    ctx = (torch.cuda.stream(torch.cuda.ExternalStream(stream, device=pkts.device)) if stream
+           else contextlib.nullcontext())
+    with ctx:
+        if torch.cuda.is_current_stream_capturing():
+            return  # no reduction inside a graph capture: the caller's descriptors are taken as they are
+        top = int((offsets[:n_pkts].view(torch.int32).to(torch.int64) & 0xFFFFFFFF).max().item())
+    if top + 64 > pkts.numel():
+        raise ValueError(f"{name}: the 64-B owned window at offset {top} runs past the end of pkts "
+                         f"({pkts.numel()} B); pass owned_windows=False for frames without a 64-B data room")
 
 
 def build_lut(backends: Sequence[str], lut_size: int = 65537) -> np.ndarray:
@@ -385,6 +386,12 @@ class Maglev:
         """Start this handle's persistent RX ring (nbg_ring_start): one classify kernel on `stream`
         (default: a new torch stream) that takes batches as they are posted until stop()."""
         return Ring(self, stride=stride, frame_len=frame_len, swap_macs=swap_macs, idle_ms=idle_ms, stream=stream)
+
+    def host_query(self, ticket: int) -> bool:
+        """nbg_maglev_host_query: True once batch `ticket` has finished on the GPU (non-blocking)."""
+        done = C.c_int(0)
+        check(lib.nbg_maglev_host_query(self._h, ticket, C.byref(done)), "nbg_maglev_host_query")
+        return bool(done.value)
 
     def host_wait(self, ticket: int) -> None:
         check(lib.nbg_maglev_host_wait(self._h, ticket), "nbg_maglev_host_wait")

@@ -550,6 +550,37 @@ def test_host_pipeline_submit_wait(torch_cuda, mg65):
             assert pool[i * 2048:i * 2048 + l].tobytes() == exp[0][o:o + l].tobytes(), i
 
 
+@pytest.mark.parametrize("kind", [48, 64, 80])
+def test_host_pipeline_direct_small_batches(torch_cuda, mg65, kind):
+    """Batches of at most 2,048 frames take host_submit's direct path (the small kernel reads the
+    staged windows out of pinned memory and stores backend / perm / counts / MAC records there): every
+    window stride with runts, IHL options and non-IPv4 frames, three batches in flight, completion
+    polled with nbg_maglev_host_query before each wait; bit-exact vs the oracle."""
+    lut = orc.lut_build(NAMES65, 65537)
+    frames_all = _host_case(kind, 40 + kind)
+    batches = []
+    for lo, hi in ((0, 2048), (2048, 2048 + 992), (3040, 3072)):
+        frames = frames_all[lo:hi]
+        pool, ptrs, lens = _mbuf_pool(frames)
+        out = dict(backend=np.empty(len(frames), np.uint16), perm=np.empty(len(frames), np.uint32),
+                   counts=np.empty(66, np.uint32))
+        batches.append((frames, pool, ptrs, lens, out, mg65.host_submit(ptrs, lens, **out)))
+    for *_, t in batches:
+        for _ in range(100000):
+            if mg65.host_query(t):
+                break
+        assert mg65.host_query(t)
+        mg65.host_wait(t)
+    for frames, pool, ptrs, lens, out, _ in batches:
+        pbuf, poff, pln = _pack([bytearray(f) for f in frames], 64)
+        exp = _oracle(pbuf, len(frames), lut, 65, offs=poff, lens=pln)
+        np.testing.assert_array_equal(out["backend"], exp[1])
+        np.testing.assert_array_equal(out["perm"], exp[2])
+        np.testing.assert_array_equal(out["counts"], exp[3])
+        for i, (o, l) in enumerate(zip(poff.tolist(), pln.tolist())):
+            assert pool[i * 2048:i * 2048 + l].tobytes() == exp[0][o:o + l].tobytes(), i
+
+
 def test_host_pipeline_large_batch(torch_cuda, mg65):
     """A 300k-packet host batch (the parallel gather and write-back) through submit/wait."""
     from netbricks_amd import make_trace

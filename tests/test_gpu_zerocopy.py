@@ -81,14 +81,16 @@ def test_region_rejects_closed_and_bad_arrays(torch_cuda):
     mg.close()
 
 
-def test_host_submit_takes_zero_copy_for_registered_pool(torch_cuda):
+@pytest.mark.parametrize("n", [20000, 992, 1])
+def test_host_submit_takes_zero_copy_for_registered_pool(torch_cuda, n):
     """nbg_maglev_host_submit over mbufs inside a registered region: the GPU rewrites the frames
     itself (the swap is in host memory once the device is idle, before host_wait), results
-    bit-exact; the same batch from an unregistered pool takes the gather path (swap at wait)."""
+    bit-exact; the same batch from an unregistered pool takes the gather path (swap at wait).
+    Batches of at most 2,048 packets take the direct path (offsets, lengths and results in pinned
+    memory, one kernel launch, no copy)."""
     import netbricks_amd as nb
 
     torch = torch_cuda
-    n = 20000
     pool, offs, lens = _pool(n, seed=11)
     ref = pool.copy()
     be = orc.classify(ref, n, orc.lut_build(NAMES, 65537), offs=offs, lens=lens)

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Throughput of the drop-in operator path (north_star: test/maglev's ReceiveBatch -> parse ->
+transform -> group_by surface): nb_maglev --loop, the C++ mirror of test/maglev (operators.hpp) with
+the pipelined GPU group_by producer, at the reference's own queue limit (1024-slot group queues,
+992-packet batches = 31 RX bursts, framework/src/queues/mpsc_mbuf_queue.rs:261-265,
+framework/src/operators/group_by.rs:43-55).
+
+1, 4 and 16 pipelines, one thread + Maglev handle + stream each (one pipeline per RX queue and core,
+scheduler/context.rs:55-69,241-255), each replaying a C1-style capture (10k 64-B UDP frames, 65
+backends / 65537) through a LoopPort (the reference's VirtualPort: recv hands out mbufs, send frees
+them).  Producer and consumer (merge + send) tasks share each pipeline's thread, as in the reference.
+
+This process never initialises the GPU: it writes the capture (host trace generator) and runs
+nb_maglev as child processes.  Prints one JSON line.
+"""
+import argparse
+import json
+import os
+import struct
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+NB = os.path.join(ROOT, "netbricks_amd", "host", "nb_maglev")
+
+
+def write_c1_pcap(path, n=10000, seed=2024):
+    import netbricks_amd as nb  # host-only: the trace generator needs no GPU
+
+    buf, off, ln = nb.make_trace(n, 0, seed=seed)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+        for i, (o, l) in enumerate(zip(off.tolist(), ln.tolist())):
+            f.write(struct.pack("<IIII", i, 0, l, l))
+            f.write(buf[o:o + l].tobytes())
+
+
+def run(pcap, pipelines, total, batch=992, depth=3, zero_copy=False, drop_on_full=False, timeout=120):
+    args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
+            "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
+            "--drop-on-full", "1" if drop_on_full else "0"]
+    r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True)
+    if r.returncode != 0:
+        return {"error": f"rc={r.returncode}: {r.stderr[-300:]}"}
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--total", type=int, default=20_000_000, help="packets received per pipeline")
+    ap.add_argument("--pipelines", default="1,4,16")
+    ap.add_argument("--extra", action="store_true", help="also depth 1, 496-packet batches, zero-copy, drop-on-full")
+    ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
+    args = ap.parse_args()
+    if args.write_pcap:
+        write_c1_pcap(args.write_pcap)
+        return
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        pcap = os.path.join(d, "c1.pcap")
+        write_c1_pcap(pcap)
+        runs = [(f"p{p}", dict(pipelines=int(p))) for p in args.pipelines.split(",")]
+        if args.extra:
+            top = max(int(p) for p in args.pipelines.split(","))
+            runs += [(f"p{top}_depth1", dict(pipelines=top, depth=1)),
+                     (f"p{top}_b496", dict(pipelines=top, batch=496)),
+                     (f"p{top}_b320", dict(pipelines=top, batch=320)),
+                     (f"p{top}_zero_copy", dict(pipelines=top, zero_copy=True)),
+                     (f"p{top}_drop_on_full", dict(pipelines=top, drop_on_full=True)),
+                     ("p1_depth1", dict(pipelines=1, depth=1))]
+        for name, kw in runs:
+            r = run(pcap, total=args.total, **kw)
+            out[name] = r
+            print(f"{name}: {r.get('aggregate_mpps', r.get('error'))}", file=sys.stderr, flush=True)
+    rows = []
+    for name, r in out.items():
+        if name.startswith("p") and name[1:].isdigit() and "aggregate_mpps" in r:
+            per = r["per_pipeline_mpps"]
+            rows.append({"pipelines": r["pipelines"], "per_pipeline_mpps": round(sum(per) / len(per), 2),
+                         "aggregate_mpps": r["aggregate_mpps"]})
+    print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024,
+                      "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, LoopPort replay"}))
+
+
+if __name__ == "__main__":
+    main()
