@@ -153,8 +153,8 @@ int nbg_maglev_classify_device(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d
 /* As nbg_maglev_classify_device, plus d_mac_out (nullable, n_pkts x 12 B): with NBG_SWAP_MACS
  * the swapped MAC pair of packet i (its new bytes 0..11) is written to d_mac_out + 12*i and
  * the packet bytes are left untouched — the egress rewrite record a host-mbuf pipeline
- * applies before TX (what nbg_maglev_classify_host does).  Packets shorter than 14 B get no
- * record (their 12 bytes are left as they were). */
+ * applies before TX.  Packets shorter than 14 B get no record (their 12 bytes are left as they
+ * were). */
 int nbg_maglev_classify_device_ex(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len,
                                   uint32_t stride, uint16_t fixed_len, uint64_t n_pkts, uint32_t flags,
                                   uint16_t* d_backend, uint32_t* d_perm, uint32_t* d_counts, uint8_t* d_mac_out,
@@ -327,20 +327,21 @@ int nbg_maglev_check(nbg_maglev* h);
 /*
  * Host-resident batch (the PCIe path): packet i is the mbuf data at pkt_ptrs[i]
  * with lens[i] bytes (MBuf::data_address / data_len, native/zcsi/mbuf.rs:34-49).
- * Header windows are gathered into pinned staging, copied H2D, classified on the
- * GPU, and the results (plus the swapped MAC bytes when NBG_SWAP_MACS) copied back
- * and written into the mbufs.  perm_out / counts_out are nullable.  Synchronous.
- * Replaces one GroupByProducer::execute over a batch of host mbufs.
+ * Header windows are gathered into pinned staging (with NBG_SWAP_MACS the MACs of every
+ * frame of >= 14 B are swapped in the mbuf as its line is gathered: the flow hash reads
+ * none of those 12 bytes), classified on the GPU, and the results copied back.
+ * perm_out / counts_out are nullable.  Synchronous.  Replaces one GroupByProducer::execute
+ * over a batch of host mbufs.
  */
 int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                              uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out);
 
 /*
  * The same, pipelined: nbg_maglev_host_submit gathers the batch's header windows into one of the
- * handle's NBG_HOST_SLOTS pinned staging slots (host worker threads), queues the H2D copy, the
- * kernels and the D2H copy, and returns a ticket without waiting; nbg_maglev_host_wait(ticket)
- * waits for that batch, stores its results in the buffers given to the submit and writes the
- * swapped MACs into its mbufs.  So a producer gathers batch i+1 while batch i crosses PCIe and
+ * handle's NBG_HOST_SLOTS pinned staging slots (host worker threads; the MAC swap is applied to
+ * the mbufs on the way), queues the H2D copy, the kernels and the D2H copy, and returns a ticket
+ * without waiting; nbg_maglev_host_wait(ticket) waits for that batch and stores its results in the
+ * buffers given to the submit.  So a producer gathers batch i+1 while batch i crosses PCIe and
  * runs.  Windows are 48 B when every frame longer than 48 B has IHL <= 7 (64 or 80 B otherwise).
  * Batches of one handle are classified in submit order.  A submit into a slot whose batch was
  * not waited for completes that batch first.  Everything a submit names (mbufs, lens, outputs)

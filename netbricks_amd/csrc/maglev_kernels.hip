@@ -2130,7 +2130,11 @@ __global__ __launch_bounds__(kLookupNT) void tile_lookup_kernel(TileArgs a) {
 // (receive_batch.rs:26), where two launches and their gaps were the whole cost of a call.  Wave w
 // owns packets [256w, 256w + 256) in four 64-packet rounds.  Per packet: the chunks 0..2 of its
 // 64-B window are loaded as three 16-B vectors when the frame allows (aligned, >= 48 B), and it
-// takes the fast path (IHL 5) or the byte-wise path.  Then each round ranks its lanes among the
+// takes the fast path (IHL 5) or the byte-wise path.  The loads are coalesced: in a round, load k
+// of lane l fetches chunk (64k + l) % 3 of packet (64k + l) / 3, so three neighbouring lanes read one
+// packet's 48 contiguous bytes in one instruction (one request per line, where a lane per packet
+// touched every line three times, once per instruction: the host path's direct batches read their
+// windows over PCIe, uncached); an LDS pass hands each lane its packet's three chunks.  Then each round ranks its lanes among the
 // same bin (readlane match) into per-wave counters, one block scan over (bin, wave) in bin-major
 // order gives every wave's start per bin, and perm is scattered: per-group FIFO order as the
 // reference's producer (group_by.rs:46-51).
@@ -2185,7 +2189,7 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
   // loads of every round first (unconditional, clamped), then every round's classification (its
   // LUT gathers in flight together), then the ranking
   uint32_t off[4], len[4], bin[4];
-  uint4 c[4][3];
+  uint4 v[4][3];
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
     const uint32_t p = min(wave * 256u + r * 64u + lane, a.n_pkts - 1u);
@@ -2194,18 +2198,32 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
   }
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
-    const uint8_t* pk = a.pkts + off[r];
-    const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && len[r] >= 48u;
-    const uint8_t* src = vec ? pk : a.pkts;  // the batch base is 16-B aligned by the host check
 #pragma unroll
-    for (uint32_t k = 0; k < 3; ++k) c[r][k] = *reinterpret_cast<const uint4*>(src + 16u * k);
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t q = 64u * k + lane, pi = q / 3u, part = q - 3u * pi;
+      const uint32_t o = __shfl(off[r], static_cast<int>(pi)), l = __shfl(len[r], static_cast<int>(pi));
+      const uint8_t* pk = a.pkts + o;
+      const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && l >= 48u;
+      // the batch base is 16-B aligned by the host check; its 48 B are read for packets off the path
+      v[r][k] = *reinterpret_cast<const uint4*>((vec ? pk : a.pkts) + 16u * part);
+    }
   }
+  uint4* tp = reinterpret_cast<uint4*>(bin16 + kSmallMax) + wave * 192u;  // [192] chunks of one round
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) tp[64u * k + lane] = v[r][k];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations run in issue order
+    uint4 c[3];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) c[k] = tp[3u * lane + k];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // the next round's writes after these reads
     const uint32_t p = wave * 256u + r * 64u + lane;
     bin[r] = 0xffffffffu;
     if (r < rounds && p < a.n_pkts) {
-      bin[r] = small_classify<LUTM, F4>(a, p, off[r], len[r], c[r]);
+      bin[r] = small_classify<LUTM, F4>(a, p, off[r], len[r], c);
       a.backend[p] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
     }
   }
@@ -3338,7 +3356,10 @@ int launch_tiled_lookup(const TileArgs& a, void* stream) {
 
 uint32_t lut_tiles(uint64_t m) { return static_cast<uint32_t>((m + kTileEntries - 1) / kTileEntries); }
 
-size_t small_lds(uint32_t nb) { return (kSmallW * (((nb + 1) + 3) & ~3u)) * 4u + kSmallMax * 4u; }
+// counters [kSmallW][nbp], rank16 / bin16 [kSmallMax], then a 3-KB load transpose area per wave
+size_t small_lds(uint32_t nb, uint32_t waves) {
+  return (kSmallW * (((nb + 1) + 3) & ~3u)) * 4u + kSmallMax * 4u + waves * 192u * 16u;
+}
 
 int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void* stream, uint32_t* done,
                  uint32_t done_val) {
@@ -3347,12 +3368,12 @@ int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void*
                                       : (b7 ? small_kernel<kGlobalU16, false, 7> : small_kernel<kGlobalU16, false, 10>))
                      : (a.m == 65537u ? (b7 ? small_kernel<kGlobalU8, true, 7> : small_kernel<kGlobalU8, true, 10>)
                                       : (b7 ? small_kernel<kGlobalU8, false, 7> : small_kernel<kGlobalU8, false, 10>));
-  const size_t lds = small_lds(a.nb);
+  const uint32_t waves = (a.n_pkts + 255u) / 256u;  // 1..16: a wave per 256 packets
+  const size_t lds = small_lds(a.nb, waves);
   if (lds > 64 * 1024 &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                           static_cast<int>(lds)) != hipSuccess)
     return set_error(NBG_EIO, "small: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
-  const uint32_t waves = (a.n_pkts + 255u) / 256u;  // 1..16: a wave per 256 packets
   hipLaunchKernelGGL(fn, dim3(1), dim3(64 * waves), lds, static_cast<hipStream_t>(stream), a, g, done, done_val);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(NBG_EIO, "small launch: %s", hipGetErrorString(e));

@@ -119,22 +119,19 @@ struct nbg_maglev {
     uint64_t cap = 0;          // packets the buffers hold
     uint8_t* h_win = nullptr;  // pinned: windows (cap * 80 B + 64 B of slack for the last chunk load)
     uint16_t* h_len = nullptr;
-    uint8_t* h_mac = nullptr;  // pinned: 12-B swapped-MAC records
     uint16_t* h_backend = nullptr;
     uint32_t* h_perm = nullptr;
     uint32_t* h_counts = nullptr;
     uint8_t* d_win = nullptr;
     uint16_t* d_len = nullptr;
-    uint8_t* d_mac = nullptr;
     uint16_t* d_backend = nullptr;
     uint32_t* d_perm = nullptr;
     uint32_t* d_counts = nullptr;
     // device addresses of the pinned buffers above (mapped, fine-grained): a small batch is classified
     // straight out of h_win / h_len with its results stored straight into h_backend / h_perm /
-    // h_counts / h_mac — one launch, no copy (host_submit's direct path)
+    // h_counts — one launch, no copy (host_submit's direct path)
     uint8_t* dh_win = nullptr;
     uint16_t* dh_len = nullptr;
-    uint8_t* dh_mac = nullptr;
     uint16_t* dh_backend = nullptr;
     uint32_t* dh_perm = nullptr;
     uint32_t* dh_counts = nullptr;
@@ -146,11 +143,8 @@ struct nbg_maglev {
     hipEvent_t done = nullptr;  // after the slot's D2H copies (on the handle's host stream)
     bool busy = false;
     uint64_t ticket = 0;
-    // the submitted batch (the caller keeps these valid until its wait)
-    uint8_t* const* pkt_ptrs = nullptr;
-    const uint16_t* lens = nullptr;
+    // the submitted batch's outputs (the caller keeps them valid until its wait)
     uint64_t n = 0;
-    bool swap = false;
     uint16_t* backend_out = nullptr;
     uint32_t* perm_out = nullptr;
     uint32_t* counts_out = nullptr;
@@ -293,20 +287,18 @@ void free_scratch(nbg_maglev* h) {
 void free_slot_buffers(nbg_maglev::HostSlot& t) {
   (void)hipHostFree(t.h_win);
   (void)hipHostFree(t.h_len);
-  (void)hipHostFree(t.h_mac);
   (void)hipHostFree(t.h_backend);
   (void)hipHostFree(t.h_perm);
   (void)hipHostFree(t.h_counts);
   (void)hipFree(t.d_win);
   (void)hipFree(t.d_len);
-  (void)hipFree(t.d_mac);
   (void)hipFree(t.d_backend);
   (void)hipFree(t.d_perm);
   (void)hipFree(t.d_counts);
-  t.h_win = t.h_mac = t.d_win = t.d_mac = nullptr;
+  t.h_win = t.d_win = nullptr;
   t.h_len = t.d_len = t.h_backend = t.d_backend = nullptr;
   t.h_perm = t.h_counts = t.d_perm = t.d_counts = nullptr;
-  t.dh_win = t.dh_mac = nullptr;
+  t.dh_win = nullptr;
   t.dh_len = t.dh_backend = nullptr;
   t.dh_perm = t.dh_counts = nullptr;
   t.cap = 0;
@@ -415,7 +407,7 @@ bool use_small(uint64_t n_pkts, uint32_t nbins, uint32_t flags, const uint8_t* d
          (reinterpret_cast<uintptr_t>(d_pkts) & 15u) == 0;
 }
 
-// Persistent host worker pool for the host path's gather and MAC write-back (bound by host
+// Persistent host worker pool for the host path's gather and MAC swap (bound by host
 // memory latency over scattered mbufs, not bandwidth): up to 16 threads (the GPU box's CPU share), started on first use and
 // kept for the life of the process (no thread start per batch).  One job at a time.
 class HostPool {
@@ -2205,19 +2197,29 @@ namespace {
 // the staged copy, so one pass over the (scattered) mbufs both gathers and sizes; frames shorter
 // than the stride are staged whole and take the kernel's byte-wise path.  Software prefetch runs
 // kAhead frames ahead: the gather is bound by host memory latency, one cache line per mbuf.
+// swap: apply MacHeader::swap_addresses (headers/mac.rs:140-145) to every frame of >= 14 B while its
+// line is in cache (the staged copy keeps the bytes as received; the flow hash reads none of the 12
+// swapped bytes), so no second pass over the mbufs writes the swap back after the GPU.
 uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint8_t* h_win,
-                     uint16_t* h_len) {
+                     uint16_t* h_len, bool swap) {
   constexpr uint64_t kAhead = 16;
   std::atomic<uint32_t> need{48};
   parallel_for(n, [&](uint64_t b, uint64_t e) {
     uint32_t m = 48;
     for (uint64_t i = b; i < e; ++i) {
-      if (i + kAhead < e) __builtin_prefetch(pkt_ptrs[i + kAhead], 0, 0);
+      if (i + kAhead < e) __builtin_prefetch(pkt_ptrs[i + kAhead], 1, 0);  // read, then (swap) written
       const uint32_t l = lens[i], c = std::min<uint32_t>(l, win);
       uint8_t* w = h_win + i * win;
-      std::memcpy(w, pkt_ptrs[i], c);
+      uint8_t* f = pkt_ptrs[i];
+      std::memcpy(w, f, c);
       h_len[i] = static_cast<uint16_t>(l);
       if (l > 48) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (w[14] & 0xfu) * 4 + 4));
+      if (swap && l >= 14) {
+        uint8_t dst[6];
+        std::memcpy(dst, f, 6);
+        std::memmove(f, f + 6, 6);
+        std::memcpy(f + 6, dst, 6);
+      }
     }
     uint32_t cur = need.load();
     while (m > cur && !need.compare_exchange_weak(cur, m)) {
@@ -2243,21 +2245,24 @@ int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
   // lines in the GPU's caches between the slot's batches; the copies of the large-batch path do not
   // care)
   constexpr unsigned kPin = hipHostMallocMapped | hipHostMallocCoherent;
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_win), win_bytes, kPin));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_len), cap * 2, kPin));
-  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_mac), cap * 12, kPin));
+  // NBG_HOST_IN_COARSE=1 (measurement): the staged windows and lengths coarse-grained, so the direct
+  // kernel's reads go through the L2 (the dispatch's acquire invalidates it)
+  static const unsigned kPinIn = [] {
+    const char* e = std::getenv("NBG_HOST_IN_COARSE");
+    return e && std::atoi(e) == 1 ? unsigned{hipHostMallocMapped | hipHostMallocNonCoherent} : kPin;
+  }();
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_win), win_bytes, kPinIn));
+  NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_len), cap * 2, kPinIn));
   NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_backend), cap * 2, kPin));
   NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_perm), cap * 4, kPin));
   NBG_HIP(hipHostMalloc(reinterpret_cast<void**>(&t.h_counts), nbins * 4, kPin));
   NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_win), t.h_win, 0));
   NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_len), t.h_len, 0));
-  NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_mac), t.h_mac, 0));
   NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_backend), t.h_backend, 0));
   NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_perm), t.h_perm, 0));
   NBG_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.dh_counts), t.h_counts, 0));
   NBG_HIP(hipMalloc(&t.d_win, win_bytes));
   NBG_HIP(hipMalloc(&t.d_len, cap * 2));
-  NBG_HIP(hipMalloc(&t.d_mac, cap * 12));
   NBG_HIP(hipMalloc(&t.d_backend, cap * 2));
   NBG_HIP(hipMalloc(&t.d_perm, cap * 4));
   NBG_HIP(hipMalloc(&t.d_counts, nbins * 4));
@@ -2268,8 +2273,6 @@ int slot_reserve(nbg_maglev* h, nbg_maglev::HostSlot& t, uint64_t n) {
   return NBG_OK;
 }
 
-// Complete the batch held by slot t: wait for its D2H, hand the results to the caller's buffers
-// and write the swapped MACs into the mbufs (the egress rewrite of MacHeader::swap_addresses).
 // The direct batch in slot t has finished: its completion word holds its ticket.
 bool flag_set(const nbg_maglev::HostSlot& t) {
   return __atomic_load_n(t.h_flag, __ATOMIC_ACQUIRE) == static_cast<uint32_t>(t.ticket);
@@ -2294,6 +2297,8 @@ int wait_flag(nbg_maglev* h, const nbg_maglev::HostSlot& t) {
   return NBG_OK;
 }
 
+// Complete the batch held by slot t: wait for it (completion word or D2H copies) and hand the results
+// to the caller's buffers (the MAC swap was applied at submit: in the gather, or by the zero-copy kernel).
 int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
   if (!t.busy) return NBG_OK;
   t.busy = false;
@@ -2307,17 +2312,6 @@ int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
   if (t.backend_out) std::memcpy(t.backend_out, t.h_backend, n * 2);
   if (t.perm_out) std::memcpy(t.perm_out, t.h_perm, n * 4);
   if (t.counts_out) std::memcpy(t.counts_out, t.h_counts, (h->nb + 1) * 4);
-  if (t.swap) {
-    const uint8_t* h_mac = t.h_mac;
-    uint8_t* const* pkt_ptrs = t.pkt_ptrs;
-    const uint16_t* lens = t.lens;
-    parallel_for(n, [=](uint64_t b, uint64_t e) {
-      for (uint64_t i = b; i < e; ++i) {
-        if (i + 16 < e) __builtin_prefetch(pkt_ptrs[i + 16], 1, 0);
-        if (lens[i] >= 14) std::memcpy(pkt_ptrs[i], h_mac + i * 12, 12);
-      }
-    });
-  }
   return NBG_OK;
 }
 
@@ -2343,10 +2337,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   if ((rc = slot_reserve(h, t, n))) return rc;
   t.direct = false;
   const bool swap = flags & NBG_SWAP_MACS;
-  t.pkt_ptrs = pkt_ptrs;
-  t.lens = lens;
   t.n = n;
-  t.swap = swap;
   t.backend_out = backend_out;
   t.perm_out = perm_out;
   t.counts_out = counts_out;
@@ -2376,7 +2367,6 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     });
     if (inside.load()) {
       hipStream_t hs = h->host_compute;
-      t.swap = false;  // the kernel rewrites the frames itself
       const bool group = perm_out || counts_out;
       const uint32_t zflags = (flags & ~(NBG_DEFER_GROUP | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL;
       if (use_small(n, h->nb + 1, zflags, reg.dev)) {
@@ -2406,9 +2396,10 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
       return NBG_OK;
     }
   }
-  // gather at 48-B windows; a batch with longer IP headers is staged again at the stride it needs
-  uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len);
-  if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len);
+  // gather at 48-B windows, swapping the MACs in the mbufs on the way; a batch with longer IP headers
+  // is staged again (without swapping) at the stride it needs
+  uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len, swap);
+  if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len, false);
   // copies and kernels in submit order on the handle's one host stream (the kernels share the
   // handle's grouping scratch).  No cross-stream event: with the copies on a stream of their own
   // and an event wait on the compute stream, kernels were seen reading windows whose H2D copy had
@@ -2416,14 +2407,15 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   // the next batch while this one runs.
   hipStream_t hs = h->host_compute;
   const bool group = perm_out || counts_out;
-  const uint32_t sflags = (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS;
+  const uint32_t sflags =
+      (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG | NBG_SWAP_MACS)) | NBG_OWNED_WINDOWS;
   if (use_small(n, h->nb + 1, sflags, t.dh_win)) {
     // direct: a batch of at most 2,048 packets (NetBricks' own bursts are 32) is classified and
     // grouped by one small-kernel launch that reads the staged windows out of pinned memory and
-    // stores backend / perm / counts / MAC records there.  The copies' fixed costs (a few us each
-    // on the DMA engines, four to six per batch) were the whole cost of a small batch
+    // stores backend / perm / counts there.  The copies' fixed costs (a few us each on the DMA
+    // engines, four to six per batch) were the whole cost of a small batch
     rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
-                         group ? t.dh_counts : nullptr, swap ? t.dh_mac : nullptr, nullptr, 0, nullptr, hs, t.dh_flag,
+                         group ? t.dh_counts : nullptr, nullptr, nullptr, 0, nullptr, hs, t.dh_flag,
                          static_cast<uint32_t>(tk));
     if (rc) return rc;
     t.direct = true;
@@ -2434,13 +2426,11 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   NBG_HIP(hipMemcpyAsync(t.d_win, t.h_win, n * win, hipMemcpyHostToDevice, hs));
   NBG_HIP(hipMemcpyAsync(t.d_len, t.h_len, n * 2, hipMemcpyHostToDevice, hs));
   rc = nbg_maglev_classify_device_ex(h, t.d_win, nullptr, t.d_len, win, 0, n, sflags, t.d_backend,
-                                     perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr,
-                                     swap ? t.d_mac : nullptr, hs);
+                                     perm_out ? t.d_perm : nullptr, group ? t.d_counts : nullptr, nullptr, hs);
   if (rc) return rc;
   NBG_HIP(hipMemcpyAsync(t.h_backend, t.d_backend, n * 2, hipMemcpyDeviceToHost, hs));
   if (perm_out) NBG_HIP(hipMemcpyAsync(t.h_perm, t.d_perm, n * 4, hipMemcpyDeviceToHost, hs));
   if (counts_out) NBG_HIP(hipMemcpyAsync(t.h_counts, t.d_counts, (h->nb + 1) * 4, hipMemcpyDeviceToHost, hs));
-  if (swap) NBG_HIP(hipMemcpyAsync(t.h_mac, t.d_mac, n * 12, hipMemcpyDeviceToHost, hs));
   NBG_HIP(hipEventRecord(t.done, hs));
   t.busy = true;
   *ticket = tk;

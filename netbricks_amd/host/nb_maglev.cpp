@@ -3,7 +3,7 @@
 //
 //   nb_maglev --rx in.pcap --tx out.pcap [--backends N | --names a,b,c] [--table 65537]
 //             [--batch 992] [--depth 3] [--order order.txt] [--zero-copy 1] [--drop-on-full 1]
-//   nb_maglev --rx in.pcap --loop TOTAL [--pipelines P] [...]      (throughput run)
+//   nb_maglev --rx in.pcap --loop TOTAL [--pipelines P] [--hw-queues Q] [...]      (throughput run)
 //
 // Default backends are the reference's ["Larry", "Curly", "Moe"] (main.rs:36).  Prints one
 // JSON line with rx/tx/dropped counts and the per-group packet counts; --order writes the rx
@@ -17,7 +17,8 @@
 //
 // --loop TOTAL: each of P pipelines (--pipelines, default 1) runs on a thread of its own, pinned to
 // one of the process's CPUs, with its own replay port (LoopPort: the capture's frames in a 64k-mbuf
-// pool, received until TOTAL packets, freed by send — the reference's VirtualPort), its own
+// pool of 2-KiB data rooms in transparent huge pages, as DPDK's mempools are in hugepages; --hugepages 0
+// for 4-KiB pages; received until TOTAL packets, freed by send — the reference's VirtualPort), its own
 // scheduler, its own Maglev handle and stream: the reference's one pipeline per RX queue and core
 // (scheduler/context.rs:55-69,241-255).  The JSON line then gives each pipeline's Mpps (rx packets
 // over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
@@ -42,6 +43,7 @@ namespace {
 struct LoopResult {
   nb::ProducerProfile prof;
   double seconds = 0, producer_seconds = 0;
+  bool huge = false;
   uint64_t rx = 0, tx = 0, dropped = 0, would_panic = 0, batches = 0, stalls = 0;
   std::string error;
 };
@@ -63,7 +65,7 @@ void pin_to(int k) {
 }
 
 int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
-             uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines) {
+             uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge) {
   const auto recs = nb::read_pcap(rx);
   std::vector<LoopResult> res(pipelines);
   std::atomic<int> ready{0};
@@ -75,7 +77,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
       bool counted = false;
       try {
         pin_to(p);
-        auto port = std::make_shared<nb::LoopPort>(recs, total);
+        auto port = std::make_shared<nb::LoopPort>(recs, total, 65536, 2048, huge);
         auto pool = port->mempool();
         uint8_t* dev = nullptr;
         if (zero_copy) nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
@@ -96,6 +98,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
         r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         r.producer_seconds = sched.task_seconds(0);
         r.rx = port->rx_total();
+        r.huge = port->huge_pages();
         r.tx = port->tx_total();
         r.dropped = pipe.groups->dropped();
         r.would_panic = pipe.groups->would_panic();
@@ -115,8 +118,10 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
   nb::ProducerProfile pr;  // summed over pipelines
   uint64_t rx_all = 0, tx_all = 0, dropped = 0, panic = 0, batches = 0, stalls = 0;
   std::string per, prod, err;
+  bool huge_all = true;
   for (auto& r : res) {
     if (!r.error.empty()) err = r.error;
+    huge_all = huge_all && r.huge;
     tmax = std::max(tmax, r.seconds);
     rx_all += r.rx;
     tx_all += r.tx;
@@ -141,12 +146,13 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
     return 1;
   }
   std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
-              "\"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
               "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
               "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
               "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
               "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
-              pipelines, names.size(), nb::cap_batch(batch), depth, zero_copy ? "true" : "false",
+              pipelines, names.size(), nb::cap_batch(batch), depth, huge_all ? "true" : "false",
+              std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "", zero_copy ? "true" : "false",
               drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
               static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
               static_cast<unsigned long long>(dropped), static_cast<unsigned long long>(panic),
@@ -164,8 +170,8 @@ int main(int argc, char** argv) {
   std::vector<std::string> names = {"Larry", "Curly", "Moe"};
   uint64_t table = 65537, loop = 0;
   uint32_t batch = nb::kMaxGpuBatch, depth = nb::kMaxDepth;
-  int pipelines = 1;
-  bool zero_copy = false, drop_on_full = false;
+  int pipelines = 1, hw_queues = 0;
+  bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
     if (k == "--rx") rx = v;
@@ -176,6 +182,8 @@ int main(int argc, char** argv) {
     else if (k == "--depth") depth = static_cast<uint32_t>(std::strtoul(v.c_str(), nullptr, 10));
     else if (k == "--loop") loop = std::strtoull(v.c_str(), nullptr, 10);
     else if (k == "--pipelines") pipelines = std::atoi(v.c_str());
+    else if (k == "--hw-queues") hw_queues = std::atoi(v.c_str());
+    else if (k == "--hugepages") huge = std::atoi(v.c_str()) != 0;
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -190,12 +198,23 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
+  if (hw_queues < 0 || hw_queues > 32) {
+    std::fprintf(stderr, "--hw-queues: 0 (default: the pipeline count, at least 4) .. 32\n");
+    return 2;
+  }
   if (rx.empty() || pipelines < 1 || pipelines > 64) {
     std::fprintf(stderr, "usage: nb_maglev --rx in.pcap [--tx out.pcap] [--backends N|--names a,b] ...\n");
     return 2;
   }
+  // HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default), and kernels
+  // of streams that share a queue run one after another: each pipeline's stream gets a queue of its
+  // own (set before the first HIP call; an explicit environment setting is kept)
+  if (!std::getenv("GPU_MAX_HW_QUEUES")) {
+    const int q = hw_queues ? hw_queues : std::min(32, std::max(4, pipelines));
+    setenv("GPU_MAX_HW_QUEUES", std::to_string(q).c_str(), 1);
+  }
   try {
-    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines);
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {

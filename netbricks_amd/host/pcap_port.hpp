@@ -3,6 +3,8 @@
 // out the capture's frames in bursts; send() appends frames to the output capture.
 #pragma once
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -139,14 +141,22 @@ class PcapPort : public PacketRx, public PacketTx {
 // (the free list is FIFO, so a frame is received again only after it was sent).
 class LoopPort : public PacketRx, public PacketTx {
  public:
-  LoopPort(const std::vector<PcapRecord>& recs, uint64_t total, size_t min_pool = 65536, uint32_t data_room = 2048)
+  // huge: the mempool in 2-MiB transparent huge pages, as a DPDK mempool lives in hugepages (for the
+  // GPU's reads of a registered pool, and the host's, one TLB entry per 2 MiB instead of per 4 KiB)
+  LoopPort(const std::vector<PcapRecord>& recs, uint64_t total, size_t min_pool = 65536, uint32_t data_room = 2048,
+           bool huge = true)
       : total_(total) {
     if (recs.empty()) throw std::invalid_argument("LoopPort: empty capture");
     room_ = data_room;
     for (auto& r : recs) room_ = std::max<size_t>(room_, (r.data.size() + 63) & ~size_t{63});
     const size_t n = (std::max(min_pool, recs.size()) + recs.size() - 1) / recs.size() * recs.size();
-    mem_.assign(n * room_ + 4096, 0);
-    base_ = mem_.data() + ((4096 - reinterpret_cast<uintptr_t>(mem_.data()) % 4096) % 4096);
+    constexpr size_t kHuge = 2u << 20;
+    map_bytes_ = (n * room_ + 2 * kHuge - 1) / kHuge * kHuge;
+    void* m = mmap(nullptr, map_bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) throw std::runtime_error("LoopPort: mmap of the mempool failed");
+    map_ = static_cast<uint8_t*>(m);
+    base_ = map_ + (kHuge - reinterpret_cast<uintptr_t>(map_) % kHuge) % kHuge;  // 2-MiB aligned
+    if (huge) huge_ = madvise(base_, static_cast<size_t>(map_ + map_bytes_ - base_) / kHuge * kHuge, MADV_HUGEPAGE) == 0;
     pool_.resize(n);
     free_.resize(n);
     for (size_t i = 0; i < n; ++i) {
@@ -160,7 +170,13 @@ class LoopPort : public PacketRx, public PacketTx {
     }
     tail_ = n;
   }
+  ~LoopPort() override {
+    if (map_) munmap(map_, map_bytes_);
+  }
+  LoopPort(const LoopPort&) = delete;
+  LoopPort& operator=(const LoopPort&) = delete;
   std::pair<uint8_t*, size_t> mempool() { return {base_, pool_.size() * room_}; }
+  bool huge_pages() const { return huge_; }
   uint32_t recv(MBuf** pkts, uint32_t cap) override {
     uint32_t n = 0;
     while (n < cap && received_ < total_ && head_ != tail_) {
@@ -184,7 +200,9 @@ class LoopPort : public PacketRx, public PacketTx {
 
  private:
   uint64_t total_, received_ = 0, sent_ = 0;
-  std::vector<uint8_t> mem_;
+  uint8_t* map_ = nullptr;
+  size_t map_bytes_ = 0;
+  bool huge_ = false;
   uint8_t* base_ = nullptr;
   size_t room_ = 2048;
   std::vector<MBuf> pool_;

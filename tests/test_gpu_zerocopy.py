@@ -85,9 +85,10 @@ def test_region_rejects_closed_and_bad_arrays(torch_cuda):
 def test_host_submit_takes_zero_copy_for_registered_pool(torch_cuda, n):
     """nbg_maglev_host_submit over mbufs inside a registered region: the GPU rewrites the frames
     itself (the swap is in host memory once the device is idle, before host_wait), results
-    bit-exact; the same batch from an unregistered pool takes the gather path (swap at wait).
-    Batches of at most 2,048 packets take the direct path (offsets, lengths and results in pinned
-    memory, one kernel launch, no copy)."""
+    bit-exact; the same batch from an unregistered pool takes the gather path, which swaps the MACs
+    in the mbufs as it stages them (also before host_wait).  Batches of at most 2,048 packets take
+    the direct path (offsets or windows, lengths and results in pinned memory, one kernel launch,
+    no copy)."""
     import netbricks_amd as nb
 
     torch = torch_cuda
@@ -109,7 +110,7 @@ def test_host_submit_takes_zero_copy_for_registered_pool(torch_cuda, n):
         np.testing.assert_array_equal(out_pm, perm)
         np.testing.assert_array_equal(out_ct, counts)
         np.testing.assert_array_equal(work, ref)
-        assert swapped_before_wait == registered
+        assert swapped_before_wait
         if reg is not None:
             reg.close()
     mg.close()

@@ -37,11 +37,14 @@ def write_c1_pcap(path, n=10000, seed=2024):
             f.write(buf[o:o + l].tobytes())
 
 
-def run(pcap, pipelines, total, batch=992, depth=3, zero_copy=False, drop_on_full=False, timeout=120):
+def run(pcap, pipelines, total, batch=992, depth=3, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
+        env=None, timeout=120):
     args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
-            "--drop-on-full", "1" if drop_on_full else "0"]
-    r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True)
+            "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
+            "--hugepages", "1" if huge else "0"]
+    r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True,
+                       env=dict(os.environ, **(env or {})))
     if r.returncode != 0:
         return {"error": f"rc={r.returncode}: {r.stderr[-300:]}"}
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -51,7 +54,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--total", type=int, default=20_000_000, help="packets received per pipeline")
     ap.add_argument("--pipelines", default="1,4,16")
-    ap.add_argument("--extra", action="store_true", help="also depth 1, 496-packet batches, zero-copy, drop-on-full")
+    ap.add_argument("--extra", action="store_true",
+                    help="also zero-copy, 4-KiB pages, 4 hardware queues, depth 1, 496-packet batches, drop-on-full")
     ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
     args = ap.parse_args()
     if args.write_pcap:
@@ -64,10 +68,14 @@ def main():
         runs = [(f"p{p}", dict(pipelines=int(p))) for p in args.pipelines.split(",")]
         if args.extra:
             top = max(int(p) for p in args.pipelines.split(","))
-            runs += [(f"p{top}_depth1", dict(pipelines=top, depth=1)),
+            runs += [(f"p{top}_zero_copy", dict(pipelines=top, zero_copy=True)),
+                     ("p4_zero_copy", dict(pipelines=4, zero_copy=True)),
+                     ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
+                     (f"p{top}_4k_pages", dict(pipelines=top, huge=False)),
+                     (f"p{top}_zero_copy_4k_pages", dict(pipelines=top, zero_copy=True, huge=False)),
+                     (f"p{top}_hwq4", dict(pipelines=top, hw_queues=4)),
+                     (f"p{top}_depth1", dict(pipelines=top, depth=1)),
                      (f"p{top}_b496", dict(pipelines=top, batch=496)),
-                     (f"p{top}_b320", dict(pipelines=top, batch=320)),
-                     (f"p{top}_zero_copy", dict(pipelines=top, zero_copy=True)),
                      (f"p{top}_drop_on_full", dict(pipelines=top, drop_on_full=True)),
                      ("p1_depth1", dict(pipelines=1, depth=1))]
         for name, kw in runs:
@@ -78,8 +86,11 @@ def main():
     for name, r in out.items():
         if name.startswith("p") and name[1:].isdigit() and "aggregate_mpps" in r:
             per = r["per_pipeline_mpps"]
+            # the producer task alone (the GPU group_by: pull, submit, wait, enqueue), the part of the
+            # pipeline bench.py's cpu_baseline restates (the reference's producer loop, no consumer)
+            prod = sum(r["rx_per_pipeline"] / s for s in r["producer_seconds"] if s > 0)
             rows.append({"pipelines": r["pipelines"], "per_pipeline_mpps": round(sum(per) / len(per), 2),
-                         "aggregate_mpps": r["aggregate_mpps"]})
+                         "aggregate_mpps": r["aggregate_mpps"], "producer_only_mpps": round(prod / 1e6, 1)})
     print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024,
                       "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, LoopPort replay"}))
 
