@@ -351,7 +351,7 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
  * (or, zero-copy, the offsets and frames) out of host memory and stores its results there, with no
  * DMA copy either way; larger batches are copied H2D / D2H around the kernels.
  */
-#define NBG_HOST_SLOTS 3
+#define NBG_HOST_SLOTS 4
 int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                            uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out,
                            uint64_t* ticket);
@@ -375,6 +375,27 @@ int nbg_maglev_host_query(nbg_maglev* h, uint64_t ticket, int* done);
  */
 int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base);
 int nbg_host_unregister(void* base, int device);
+
+/*
+ * Host-batch server: one persistent kernel per GPU that takes the direct (<= 2,048-packet) batches of
+ * nbg_maglev_host_submit / nbg_maglev_classify_host from every handle attached to it, so a batch costs
+ * no kernel launch (one launch per 992-packet batch bounds a multi-pipeline drop-in producer by the
+ * GPU's dispatch rate).  Each of `blocks` (0 = 32; at most half the CUs) resident
+ * 1024-thread blocks takes the next posted batch from a descriptor ring in pinned host memory,
+ * classifies and groups it exactly as the small kernel would, and sets the batch's completion word;
+ * results are identical.  Producer threads post concurrently (the calls stay per handle).
+ * nbg_maglev_set_host_ring(h, r) attaches a handle (r = NULL detaches; batches already posted
+ * complete as before); a batch is launched as before when its handle has no server or the server
+ * ended.  The kernel runs on a private stream of the highest priority and ends at
+ * nbg_host_ring_stop (every posted batch completes first; NBG_EBUSY while handles are attached), or by
+ * itself after idle_ms without a post (0 = 2000 ms; later batches are then launched).  One server per
+ * device, not beside a persistent RX ring (nbg_ring_start and nbg_host_ring_start refuse each other
+ * with NBG_EBUSY).  nbg_maglev_destroy detaches its handle after its batches completed.
+ */
+typedef struct nbg_host_ring nbg_host_ring;
+int nbg_host_ring_start(int device, uint32_t blocks, uint32_t idle_ms, nbg_host_ring** out);
+int nbg_host_ring_stop(nbg_host_ring* r);
+int nbg_maglev_set_host_ring(nbg_maglev* h, nbg_host_ring* r);
 
 
 /* ---- chained NF: test/lpm -> test/maglev (BASELINE config C5) ------------- */

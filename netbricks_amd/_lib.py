@@ -31,7 +31,7 @@ NBG_DEFER_GROUP = 0x10
 NBG_LUT_TILED = 0x20
 NBG_STREAM_DESC = 0x40
 NBG_GROUP_LAG = 0x80
-NBG_HOST_SLOTS = 3
+NBG_HOST_SLOTS = 4
 NBG_MAX_MULTI = 16
 NBG_RING_SLOTS = 64
 NBG_RING_MAX_QUEUES = 16
@@ -101,6 +101,9 @@ SIGNATURES = {
     "nbg_maglev_host_query": (C.c_int, [_P, C.c_uint64, C.POINTER(C.c_int)]),
     "nbg_host_register": (C.c_int, [_P, C.c_uint64, C.c_int, C.POINTER(_P)]),
     "nbg_host_unregister": (C.c_int, [_P, C.c_int]),
+    "nbg_host_ring_start": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
+    "nbg_host_ring_stop": (C.c_int, [_P]),
+    "nbg_maglev_set_host_ring": (C.c_int, [_P, _P]),
     "nbg_lpm_create": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.POINTER(_P)]),
     "nbg_lpm_destroy": (None, [_P]),
     "nbg_lpm_lookup_device": (C.c_int, [_P, _P, C.c_uint64, _P, _P]),

@@ -2295,6 +2295,74 @@ __global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupAr
   }
 }
 
+// ---- host-batch server (nbg_host_ring_*) ---------------------------------------------------------
+// One launch per GPU serves every producer thread's small host batches (nbg_maglev_host_submit's
+// direct path) without a kernel launch per batch: the GPU's dispatch rate, ~200k launches/s per GPU
+// measured with 16 producer threads, capped the drop-in path at ~200 Mpps at the
+// reference's 992-packet batches.  Each 1024-thread block: claim the next ticket (device atomic), wait
+// for its descriptor in pinned host memory (thread 0 polls seq with s_sleep; exits on the host's stop,
+// or after idle_ticks without any post), copy it to LDS, acknowledge it, run the small kernel's body
+// on it, set the batch's completion word.  Every posted ticket is claimed by some block before any
+// block can exit on a stop (tickets are claimed in order and a block exits only at an unposted one).
+__global__ __launch_bounds__(kSmallNT) void host_ring_kernel(HostRingArgs r) {
+  __shared__ __align__(16) uint32_t s_desc[kHostRingDescBytes / 4];
+  __shared__ uint32_t s_ticket, s_go;
+  const uint32_t tid = threadIdx.x;
+  for (;;) {
+    if (tid == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(r.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t* seq = reinterpret_cast<const uint32_t*>(r.desc + static_cast<size_t>(t & (r.slots - 1u)) *
+                                                                           kHostRingDescBytes);
+      uint64_t t_act = wall_clock64();
+      uint32_t seen = __hip_atomic_load(&r.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t go = 0;
+      for (uint32_t nap = 1;; nap = min(2u * nap, 8u)) {
+        if (__hip_atomic_load(seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == t + 1u) {
+          go = 1;
+          break;
+        }
+        if (__hip_atomic_load(&r.ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        const uint32_t p = __hip_atomic_load(&r.ctl->posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (p != seen) {
+          seen = p;
+          t_act = wall_clock64();
+        } else if (static_cast<uint64_t>(wall_clock64()) - t_act > r.idle_ticks) {
+          __hip_atomic_store(&r.ctl->ended, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(4);
+      }
+      s_ticket = t;
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) break;
+    const uint32_t t = s_ticket;
+    uint32_t* d = reinterpret_cast<uint32_t*>(r.desc + static_cast<size_t>(t & (r.slots - 1u)) * kHostRingDescBytes);
+    if (tid < sizeof(HostRingDesc) / 4)
+      s_desc[tid] = __hip_atomic_load(d + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(d + 1, t + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // ack: reusable
+    const HostRingDesc& hd = *reinterpret_cast<const HostRingDesc*>(s_desc);
+    const ClassifyArgs a = hd.a;
+    const GroupArgs g = hd.g;
+    switch (hd.variant & 7u) {
+      case 0: small_body<kGlobalU8, false, 7>(a, g); break;
+      case 1: small_body<kGlobalU16, false, 7>(a, g); break;
+      case 2: small_body<kGlobalU8, true, 7>(a, g); break;
+      case 3: small_body<kGlobalU16, true, 7>(a, g); break;
+      case 4: small_body<kGlobalU8, false, 10>(a, g); break;
+      case 5: small_body<kGlobalU16, false, 10>(a, g); break;
+      case 6: small_body<kGlobalU8, true, 10>(a, g); break;
+      default: small_body<kGlobalU16, true, 10>(a, g); break;
+    }
+    __threadfence_system();  // this thread's outputs are visible to the host
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(hd.done, hd.done_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();  // s_desc and the small body's LDS are reused by the next batch
+  }
+}
+
 // ---- many backends (more than kMaxGroupBins - 1, up to 32767) ------------------------------------
 // The multisplit group kernel keeps a counter row per wave and bin in LDS, which does not scale to
 // 32768 bins.  Past 1023 backends the per-partition histograms (hist_kernel) and their prefix over
@@ -3381,6 +3449,22 @@ int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void*
 }
 
 uint32_t small_max() { return kSmallMax; }
+
+// host_ring_kernel's dispatch over the small kernel's instantiations (as launch_small picks them)
+uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb) {
+  return (wide_lut ? 1u : 0u) | (m == 65537u ? 2u : 0u) | (nb + 1 > 128 ? 4u : 0u);
+}
+
+int launch_host_ring(const HostRingArgs& r, uint32_t blocks, void* stream) {
+  const size_t lds = small_lds(kMaxGroupBins - 1, kSmallW);  // any handle's batch: up to 1023 backends
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(host_ring_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          static_cast<int>(lds)) != hipSuccess)
+    return set_error(NBG_EIO, "host ring: LDS attribute: %s", hipGetErrorString(hipGetLastError()));
+  hipLaunchKernelGGL(host_ring_kernel, dim3(blocks), dim3(kSmallNT), lds, static_cast<hipStream_t>(stream), r);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(NBG_EIO, "host ring launch: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
 
 int launch_group_wide(const GroupArgs& a, void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);

@@ -140,6 +140,10 @@ struct nbg_maglev {
     uint32_t* h_flag = nullptr;
     uint32_t* dh_flag = nullptr;
     bool direct = false;        // the slot's batch took the direct path (completion = h_flag)
+    hipStream_t watch = nullptr;  // the direct batch's kernel runs on it (its end without the flag is a failure)
+    bool on_ring = false;         // posted to the host-batch server: ra / rg relaunch it if the server ended first
+    ClassifyArgs ra{};
+    GroupArgs rg{};
     hipEvent_t done = nullptr;  // after the slot's D2H copies (on the handle's host stream)
     bool busy = false;
     uint64_t ticket = 0;
@@ -152,6 +156,22 @@ struct nbg_maglev {
   HostSlot slots[NBG_HOST_SLOTS];
   hipStream_t host_compute = nullptr;  // the classify and group kernels of every slot, in submit order
   uint64_t next_ticket = 1;
+  nbg_host_ring* hring = nullptr;      // direct batches go to this host-batch server instead of a launch
+};
+
+// The host-batch server of one device (nbg_host_ring_start): a persistent kernel fed descriptors.
+struct nbg_host_ring {
+  int device = 0;
+  uint32_t blocks = 0, slots = 0, idle_ms = 0;
+  hipStream_t stream = nullptr;     // private, highest priority (a hardware queue no ordinary stream shares)
+  uint8_t* host = nullptr;          // pinned, mapped, fine-grained: HostRingCtl | slots x kHostRingDescBytes
+  HostRingCtl* ctl = nullptr;
+  uint8_t* desc = nullptr;
+  uint32_t* claim = nullptr;        // device
+  std::atomic<uint64_t> next{0};    // tickets handed out (producer threads post concurrently)
+  std::atomic<uint32_t> attached{0};
+  std::atomic<bool> stopping{false};
+  bool leaked = false;
 };
 
 namespace {
@@ -192,6 +212,10 @@ int check_device(int device) {
 // The running persistent ring of each device (one per GPU: its kernel holds every CU's LDS).
 std::mutex g_dev_ring_mu;
 std::vector<nbg_ring*> g_dev_ring;
+std::vector<nbg_host_ring*> g_dev_hring;  // host-batch servers (nbg_host_ring_start), under g_dev_ring_mu
+// a stopped server's private stream, kept for the device's next server: a batch's completion wait may
+// still query it after the stop (never a destroyed stream)
+std::vector<hipStream_t> g_hring_stream;
 
 bool device_ring_running(int device) {
   std::lock_guard<std::mutex> g(g_dev_ring_mu);
@@ -304,8 +328,17 @@ void free_slot_buffers(nbg_maglev::HostSlot& t) {
   t.cap = 0;
 }
 
+bool flag_set(const nbg_maglev::HostSlot& t);
+int wait_flag(nbg_maglev* h, nbg_maglev::HostSlot& t);
+
 void free_host_path(nbg_maglev* h) {
-  if (h->host_compute) (void)hipStreamSynchronize(h->host_compute);  // direct batches record no event
+  if (h->host_compute) (void)hipStreamSynchronize(h->host_compute);  // direct launches record no event
+  for (auto& t : h->slots)
+    if (t.busy && t.direct) (void)wait_flag(h, t);  // a host-ring batch reads the LUT and writes the slot
+  if (h->hring) {
+    h->hring->attached.fetch_sub(1);
+    h->hring = nullptr;
+  }
   for (auto& t : h->slots) {
     if (t.h_flag) (void)hipHostFree(t.h_flag);
     t.h_flag = t.dh_flag = nullptr;
@@ -1876,6 +1909,8 @@ int nbg_ring_start(nbg_maglev* h, uint32_t stride, uint16_t fixed_len, uint32_t 
   if (h->cus < 2) return set_error(NBG_EINVAL, "ring_start: needs a CU for the relay beside the classify blocks");
   // one ring per GPU: a second one's blocks could never all become resident beside the first
   std::lock_guard<std::mutex> dev_lock(g_dev_ring_mu);
+  if (static_cast<size_t>(h->device) < g_dev_hring.size() && g_dev_hring[h->device])
+    return set_error(NBG_EBUSY, "ring_start: device %d runs a host-batch server (nbg_host_ring_stop first)", h->device);
   if (static_cast<size_t>(h->device) < g_dev_ring.size() && g_dev_ring[h->device])
     return set_error(NBG_EBUSY,
                      "ring_start: device %d already runs a persistent ring (one per GPU; RX queues share it through "
@@ -2202,7 +2237,7 @@ namespace {
 // swapped bytes), so no second pass over the mbufs writes the swap back after the GPU.
 uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint8_t* h_win,
                      uint16_t* h_len, bool swap) {
-  constexpr uint64_t kAhead = 16;
+  constexpr uint64_t kAhead = 16;  // 32 and 64 measured no faster (profiles/r06_dropin_tune.json)
   std::atomic<uint32_t> need{48};
   parallel_for(n, [&](uint64_t b, uint64_t e) {
     uint32_t m = 48;
@@ -2279,8 +2314,9 @@ bool flag_set(const nbg_maglev::HostSlot& t) {
 }
 
 // Wait for a direct batch's completion word: spin, then yield; the stream is queried now and then, so
-// a kernel that failed (its word never set) is reported instead of waited for.
-int wait_flag(nbg_maglev* h, const nbg_maglev::HostSlot& t) {
+// a kernel that failed (its word never set) is reported instead of waited for.  A batch posted to a
+// host-batch server whose kernel ended before taking it (its idle exit racing the post) is launched.
+int wait_flag(nbg_maglev* h, nbg_maglev::HostSlot& t) {
   for (uint32_t spin = 0; !flag_set(t); ++spin) {
     if (spin < 2048) {
       __builtin_ia32_pause();
@@ -2288,10 +2324,16 @@ int wait_flag(nbg_maglev* h, const nbg_maglev::HostSlot& t) {
     }
     std::this_thread::yield();
     if ((spin & 255u) == 0) {
-      const hipError_t e = hipStreamQuery(h->host_compute);
+      const hipError_t e = hipStreamQuery(t.watch);
       if (e != hipSuccess && e != hipErrorNotReady) return set_error(NBG_EIO, "host_wait: %s", hipGetErrorString(e));
-      if (e == hipSuccess && !flag_set(t))
-        return set_error(NBG_EIO, "host_wait: the batch's kernel ended without its completion word");
+      if (e == hipSuccess && !flag_set(t)) {
+        if (!t.on_ring) return set_error(NBG_EIO, "host_wait: the batch's kernel ended without its completion word");
+        t.on_ring = false;  // no block of the ended server touches it: launch it
+        t.watch = h->host_compute;
+        DeviceGuard g(h->device);
+        const int rc = launch_small(t.ra, t.rg, h->wide, h->host_compute, t.dh_flag, static_cast<uint32_t>(t.ticket));
+        if (rc) return rc;
+      }
     }
   }
   return NBG_OK;
@@ -2315,6 +2357,60 @@ int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
   return NBG_OK;
 }
 
+
+// The arguments the small kernel would be launched with for a host batch (classify_common's small
+// path): packets at pkts (+ off[i], or i * stride), lengths len[], outputs in pinned host memory.
+void small_args(const nbg_maglev* h, uint8_t* pkts, const uint32_t* off, const uint16_t* len, uint32_t stride,
+                uint64_t n, uint32_t flags, uint16_t* backend, uint32_t* perm, uint32_t* counts, ClassifyArgs& a,
+                GroupArgs& g) {
+  a = ClassifyArgs{};
+  a.pkts = pkts;
+  a.off = off;
+  a.len = len;
+  a.stride = stride;
+  a.n_pkts = static_cast<uint32_t>(n);
+  a.tiles_per_wave = 1;
+  a.lut = h->d_lut;
+  a.m = static_cast<uint32_t>(h->m);
+  a.mu = ~0ull / h->m + ((~0ull % h->m) + 1 == h->m ? 1 : 0);  // floor(2^64 / m)
+  a.nb = h->nb;
+  a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
+  a.win_owned = (!off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
+  a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
+  a.backend = backend;
+  g = GroupArgs{};
+  g.perm = perm;
+  g.counts = counts;
+}
+
+// Post a direct batch to the handle's host-batch server; false when the server has ended or stops
+// (the caller launches the small kernel instead).  Producer threads post concurrently: tickets come
+// from one atomic counter, a slot is reused once a block acknowledged its previous descriptor.
+bool host_ring_post(nbg_host_ring* r, const ClassifyArgs& a, const GroupArgs& g, uint32_t variant, uint32_t* done,
+                    uint32_t done_val) {
+  if (r->stopping.load() || __atomic_load_n(&r->ctl->ended, __ATOMIC_ACQUIRE)) return false;
+  const uint64_t t = r->next.fetch_add(1);
+  auto* d = reinterpret_cast<HostRingDesc*>(r->desc + (t & (r->slots - 1)) * kHostRingDescBytes);
+  if (t >= r->slots) {
+    const uint32_t want = static_cast<uint32_t>(t - r->slots + 1);
+    for (uint32_t spin = 0; __atomic_load_n(&d->ack, __ATOMIC_ACQUIRE) != want; ++spin) {
+      if (spin < 4096) {
+        __builtin_ia32_pause();
+      } else {
+        std::this_thread::yield();  // the slots' batches are in flight: a block takes one every few us
+      }
+    }
+  }
+  d->variant = variant;
+  d->done_val = done_val;
+  d->done = done;
+  d->a = a;
+  d->g = g;
+  __atomic_store_n(&d->seq, static_cast<uint32_t>(t + 1), __ATOMIC_RELEASE);
+  __atomic_store_n(&r->ctl->posted, static_cast<uint32_t>(t + 1), __ATOMIC_RELEASE);
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2336,6 +2432,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   if (rc) return rc;
   if ((rc = slot_reserve(h, t, n))) return rc;
   t.direct = false;
+  t.on_ring = false;
   const bool swap = flags & NBG_SWAP_MACS;
   t.n = n;
   t.backend_out = backend_out;
@@ -2370,12 +2467,25 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
       const bool group = perm_out || counts_out;
       const uint32_t zflags = (flags & ~(NBG_DEFER_GROUP | NBG_GROUP_LAG)) | NBG_OWNED_WINDOWS | NBG_WB_PARTIAL;
       if (use_small(n, h->nb + 1, zflags, reg.dev)) {
-        // direct: the one small-kernel launch reads the offsets and lengths out of pinned memory and
-        // stores its results there (no copy on either side)
-        rc = classify_common(h, reg.dev, reinterpret_cast<const uint32_t*>(t.dh_win), t.dh_len, 0, 0, n, zflags,
-                             t.dh_backend, perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr,
-                             nullptr, 0, nullptr, hs, t.dh_flag, static_cast<uint32_t>(tk));
-        if (rc) return rc;
+        // direct: the one small-kernel launch (or the host-batch server) reads the offsets and lengths
+        // out of pinned memory and stores its results there (no copy on either side)
+        ClassifyArgs a;
+        GroupArgs ga;
+        small_args(h, reg.dev, reinterpret_cast<const uint32_t*>(t.dh_win), t.dh_len, 0, n, zflags, t.dh_backend,
+                   perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, a, ga);
+        t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb), t.dh_flag,
+                                               static_cast<uint32_t>(tk));
+        if (t.on_ring) {
+          t.watch = h->hring->stream;
+          t.ra = a;
+          t.rg = ga;
+        } else {
+          rc = classify_common(h, reg.dev, reinterpret_cast<const uint32_t*>(t.dh_win), t.dh_len, 0, 0, n, zflags,
+                               t.dh_backend, perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr,
+                               nullptr, 0, nullptr, hs, t.dh_flag, static_cast<uint32_t>(tk));
+          if (rc) return rc;
+          t.watch = hs;
+        }
         t.direct = true;
         t.busy = true;
         *ticket = tk;
@@ -2414,10 +2524,23 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     // grouped by one small-kernel launch that reads the staged windows out of pinned memory and
     // stores backend / perm / counts there.  The copies' fixed costs (a few us each on the DMA
     // engines, four to six per batch) were the whole cost of a small batch
-    rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
-                         group ? t.dh_counts : nullptr, nullptr, nullptr, 0, nullptr, hs, t.dh_flag,
-                         static_cast<uint32_t>(tk));
-    if (rc) return rc;
+    ClassifyArgs a;
+    GroupArgs ga;
+    small_args(h, t.dh_win, nullptr, t.dh_len, win, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
+               group ? t.dh_counts : nullptr, a, ga);
+    t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb), t.dh_flag,
+                                           static_cast<uint32_t>(tk));
+    if (t.on_ring) {
+      t.watch = h->hring->stream;
+      t.ra = a;
+      t.rg = ga;
+    } else {
+      rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend,
+                           perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr, nullptr, 0, nullptr,
+                           hs, t.dh_flag, static_cast<uint32_t>(tk));
+      if (rc) return rc;
+      t.watch = hs;
+    }
     t.direct = true;
     t.busy = true;
     *ticket = tk;
@@ -2469,6 +2592,125 @@ int nbg_host_unregister(void* base, int device) {
       }
   }
   NBG_HIP(hipHostUnregister(base));
+  return NBG_OK;
+}
+
+int nbg_host_ring_start(int device, uint32_t blocks, uint32_t idle_ms, nbg_host_ring** out) {
+  if (!out) return set_error(NBG_EINVAL, "host_ring_start: null argument");
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  int cus = 0;
+  NBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+  if (blocks == 0) blocks = 32;
+  if (blocks > static_cast<uint32_t>(cus) / 2)
+    return set_error(NBG_EINVAL, "host_ring_start: %u blocks (one per CU, at most half of the %d CUs)", blocks, cus);
+  // one resident server per device, and not beside a persistent RX ring (whose blocks need every CU)
+  std::lock_guard<std::mutex> dev_lock(g_dev_ring_mu);
+  if (static_cast<size_t>(device) < g_dev_ring.size() && g_dev_ring[device])
+    return set_error(NBG_EBUSY, "host_ring_start: device %d runs a persistent RX ring", device);
+  if (static_cast<size_t>(device) < g_dev_hring.size() && g_dev_hring[device])
+    return set_error(NBG_EBUSY, "host_ring_start: device %d already runs a host-batch server", device);
+  auto* r = new (std::nothrow) nbg_host_ring;
+  if (!r) return set_error(NBG_ENOMEM, "host_ring_start: out of memory");
+  r->device = device;
+  r->blocks = blocks;
+  r->slots = 256;
+  r->idle_ms = idle_ms ? idle_ms : 2000u;
+  auto fail = [&](int code, const char* what) {
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    if (r->host) (void)hipHostFree(r->host);
+    if (r->claim) (void)hipFree(r->claim);
+    delete r;
+    return set_error(code, "host_ring_start: %s", what);
+  };
+  if (static_cast<size_t>(device) < g_hring_stream.size() && g_hring_stream[device]) {
+    r->stream = g_hring_stream[device];
+    g_hring_stream[device] = nullptr;
+  } else {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&r->stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+      r->stream = nullptr;
+      return fail(NBG_EIO, "private stream");
+    }
+  }
+  const size_t hbytes = 64 + static_cast<size_t>(r->slots) * kHostRingDescBytes;
+  if (hipHostMalloc(reinterpret_cast<void**>(&r->host), hbytes, hipHostMallocMapped | hipHostMallocCoherent) !=
+      hipSuccess) {
+    r->host = nullptr;
+    return fail(NBG_ENOMEM, "pinned descriptor ring");
+  }
+  std::memset(r->host, 0, hbytes);
+  r->ctl = reinterpret_cast<HostRingCtl*>(r->host);
+  r->desc = r->host + 64;
+  if (hipMalloc(&r->claim, 64) != hipSuccess) {
+    r->claim = nullptr;
+    return fail(NBG_ENOMEM, "claim counter");
+  }
+  uint8_t* hdev = nullptr;
+  if (hipMemsetAsync(r->claim, 0, 64, r->stream) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), r->host, 0) != hipSuccess)
+    return fail(NBG_EIO, "setup");
+  HostRingArgs a{};
+  a.ctl = reinterpret_cast<HostRingCtl*>(hdev);
+  a.desc = hdev + 64;
+  a.claim = r->claim;
+  a.slots = r->slots;
+  a.idle_ticks = static_cast<uint64_t>(r->idle_ms) * 100000u;  // 100 MHz
+  if ((rc = launch_host_ring(a, blocks, r->stream))) {
+    (void)hipStreamSynchronize(r->stream);
+    return fail(rc, nbg_last_error());
+  }
+  if (static_cast<size_t>(device) >= g_dev_hring.size()) g_dev_hring.resize(device + 1, nullptr);
+  g_dev_hring[device] = r;
+  *out = r;
+  return NBG_OK;
+}
+
+int nbg_host_ring_stop(nbg_host_ring* r) {
+  if (!r) return set_error(NBG_EINVAL, "host_ring_stop: null server");
+  if (r->leaked) return set_error(NBG_EBUSY, "host_ring_stop: its kernel did not end at an earlier stop (leaked)");
+  if (r->attached.load())
+    return set_error(NBG_EBUSY, "host_ring_stop: %u handles still use it (nbg_maglev_set_host_ring(h, NULL) first)",
+                     r->attached.load());
+  DeviceGuard g(r->device);
+  r->stopping = true;
+  __atomic_store_n(&r->ctl->stop, 1u, __ATOMIC_RELEASE);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (hipStreamQuery(r->stream) == hipErrorNotReady) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(r->idle_ms + 5000u)) {
+      r->leaked = true;  // never free what a running kernel may touch
+      return set_error(NBG_EBUSY, "host_ring_stop: the kernel did not end (its memory is leaked)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  const hipError_t e = hipStreamQuery(r->stream);
+  {
+    std::lock_guard<std::mutex> dev_lock(g_dev_ring_mu);
+    if (static_cast<size_t>(r->device) < g_dev_hring.size() && g_dev_hring[r->device] == r)
+      g_dev_hring[r->device] = nullptr;
+    if (static_cast<size_t>(r->device) >= g_hring_stream.size()) g_hring_stream.resize(r->device + 1, nullptr);
+    if (!g_hring_stream[r->device]) g_hring_stream[r->device] = r->stream;
+    else (void)hipStreamDestroy(r->stream);
+  }
+  (void)hipHostFree(r->host);
+  (void)hipFree(r->claim);
+  delete r;
+  if (e != hipSuccess) return set_error(NBG_EIO, "host_ring_stop: %s", hipGetErrorString(e));
+  return NBG_OK;
+}
+
+int nbg_maglev_set_host_ring(nbg_maglev* h, nbg_host_ring* r) {
+  if (!h) return set_error(NBG_EINVAL, "set_host_ring: null handle");
+  if (r && r->device != h->device) return set_error(NBG_EINVAL, "set_host_ring: the server runs on another device");
+  if (r && (r->stopping.load() || r->leaked)) return set_error(NBG_EINVAL, "set_host_ring: the server was stopped");
+  if (h->hring == r) return NBG_OK;
+  // batches already posted to the old server complete through their completion words as before
+  if (h->hring) h->hring->attached.fetch_sub(1);
+  h->hring = r;
+  if (r) r->attached.fetch_add(1);
   return NBG_OK;
 }
 

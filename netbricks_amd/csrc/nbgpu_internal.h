@@ -235,6 +235,41 @@ struct GroupMulti {
 // summing the partition histograms straight from L2.
 enum GroupScan { kScanKernel = 0, kScanDirect = 2 };
 
+// The host-batch server (nbg_host_ring_*): a persistent kernel whose blocks each take the next posted
+// small host batch (the direct path of nbg_maglev_host_submit) from a descriptor ring in pinned host
+// memory, so a batch costs no kernel launch.  Descriptors are written by producer threads: the
+// arguments the small kernel would have been launched with, then seq = ticket + 1 (release); a block
+// copies them, stores ack = ticket + 1 (the slot may be reused), classifies + groups, and sets the
+// batch's completion word.
+struct HostRingDesc {
+  uint32_t seq;       // ticket + 1 once posted
+  uint32_t ack;       // ticket + 1 once a block has copied the descriptor
+  uint32_t variant;   // small-kernel instantiation: bit 0 u16 LUT, bit 1 M = 65537, bit 2 more than 128 bins
+  uint32_t done_val;  // stored into *done when the batch's outputs are visible
+  uint32_t* done;     // the batch's completion word (pinned host memory)
+  uint64_t pad0;
+  ClassifyArgs a;
+  GroupArgs g;
+};
+constexpr uint32_t kHostRingDescBytes = 512;  // one slot (a whole number of lines)
+static_assert(sizeof(HostRingDesc) <= kHostRingDescBytes, "host ring slot");
+struct HostRingCtl {   // pinned host memory, the first line
+  uint32_t stop;       // host: exit once every posted batch is done
+  uint32_t ended;      // device: 1 = exited after idle_ticks without a post
+  uint32_t posted;     // host: batches posted (mod 2^32), so idle blocks see activity
+  uint32_t pad[13];
+};
+struct HostRingArgs {
+  HostRingCtl* ctl;         // host (device address)
+  uint8_t* desc;            // host [slots] x kHostRingDescBytes (device address)
+  uint32_t* claim;          // device: next ticket to claim
+  uint32_t slots;           // power of two
+  uint64_t idle_ticks;      // 100 MHz wall clock
+};
+int launch_host_ring(const HostRingArgs& r, uint32_t blocks, void* stream);
+uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb);
+
+
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.
 int launch_classify(const ClassifyArgs& a, bool wide_lut, bool lds_lut, int grid, void* stream);
 // Streaming classify (lean fixed slots, u8 LUT of <= 65537 entries staged in LDS): one block per

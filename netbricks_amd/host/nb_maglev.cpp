@@ -3,14 +3,14 @@
 //
 //   nb_maglev --rx in.pcap --tx out.pcap [--backends N | --names a,b,c] [--table 65537]
 //             [--batch 992] [--depth 3] [--order order.txt] [--zero-copy 1] [--drop-on-full 1]
-//   nb_maglev --rx in.pcap --loop TOTAL [--pipelines P] [--hw-queues Q] [...]      (throughput run)
+//   nb_maglev --rx in.pcap --loop TOTAL [--pipelines P] [--hw-queues Q] [--host-ring B] [...]  (throughput run)
 //
 // Default backends are the reference's ["Larry", "Curly", "Moe"] (main.rs:36).  Prints one
 // JSON line with rx/tx/dropped counts and the per-group packet counts; --order writes the rx
 // index of every transmitted frame (one per line) for order checks.  --zero-copy 1 registers the
 // port's mempool (nbg_host_register), so the GPU reads and rewrites the frames in place over PCIe.
 // The group queues have the reference's 1024 slots; --batch is capped at 992 (whole bursts, at most
-// 1023).  --depth batches are on the GPU at once (1..3, nbg_maglev_host_submit's slots).  By default
+// 1023).  --depth batches are on the GPU at once (1..NBG_HOST_SLOTS = 4, nbg_maglev_host_submit's slots).  By default
 // the producer pulls a batch only while every queue could take a whole one, and a classified batch's
 // enqueue waits at a full queue (backpressure: nothing is dropped); --drop-on-full 1 pulls whenever
 // the pipeline has room and drops on a full queue, as the reference's producer does (group_by.rs:50).
@@ -22,7 +22,8 @@
 // scheduler, its own Maglev handle and stream: the reference's one pipeline per RX queue and core
 // (scheduler/context.rs:55-69,241-255).  The JSON line then gives each pipeline's Mpps (rx packets
 // over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
-// slowest pipeline's time).
+// slowest pipeline's time).  --host-ring B attaches every pipeline's handle to one host-batch server
+// of B blocks (nbg_host_ring_*: one persistent kernel takes the batches; no kernel launch per batch).
 #include <pthread.h>
 #include <sched.h>
 
@@ -65,7 +66,8 @@ void pin_to(int k) {
 }
 
 int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
-             uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge) {
+             uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge,
+             nbg_host_ring* server) {
   const auto recs = nb::read_pcap(rx);
   std::vector<LoopResult> res(pipelines);
   std::atomic<int> ready{0};
@@ -85,6 +87,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
         sched.set_timed(true);
         auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch,
                                drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure, depth);
+        if (server) nb::check(nbg_maglev_set_host_ring(pipe.groups->handle(), server), "nbg_maglev_set_host_ring");
         ++ready;
         counted = true;
         while (!go.load()) std::this_thread::yield();
@@ -146,12 +149,12 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
     return 1;
   }
   std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
-              "\"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"host_ring\": %s, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
               "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
               "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
               "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
               "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
-              pipelines, names.size(), nb::cap_batch(batch), depth, huge_all ? "true" : "false",
+              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", huge_all ? "true" : "false",
               std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "", zero_copy ? "true" : "false",
               drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
               static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
@@ -170,7 +173,7 @@ int main(int argc, char** argv) {
   std::vector<std::string> names = {"Larry", "Curly", "Moe"};
   uint64_t table = 65537, loop = 0;
   uint32_t batch = nb::kMaxGpuBatch, depth = nb::kMaxDepth;
-  int pipelines = 1, hw_queues = 0;
+  int pipelines = 1, hw_queues = 0, ring_blocks = -1;
   bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -184,6 +187,7 @@ int main(int argc, char** argv) {
     else if (k == "--pipelines") pipelines = std::atoi(v.c_str());
     else if (k == "--hw-queues") hw_queues = std::atoi(v.c_str());
     else if (k == "--hugepages") huge = std::atoi(v.c_str()) != 0;
+    else if (k == "--host-ring") ring_blocks = std::atoi(v.c_str());
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -214,7 +218,18 @@ int main(int argc, char** argv) {
     setenv("GPU_MAX_HW_QUEUES", std::to_string(q).c_str(), 1);
   }
   try {
-    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge);
+    // --host-ring B: every pipeline's direct batches go to one host-batch server of B blocks (0 = the
+    // library's default) instead of a kernel launch each; -1 (default) = no server
+    nbg_host_ring* server = nullptr;
+    if (ring_blocks >= 0)
+      nb::check(nbg_host_ring_start(0, static_cast<uint32_t>(ring_blocks), 5000, &server), "nbg_host_ring_start");
+    struct StopServer {
+      nbg_host_ring* s;
+      ~StopServer() {
+        if (s && nbg_host_ring_stop(s) != NBG_OK) std::fprintf(stderr, "nb_maglev: %s\n", nbg_last_error());
+      }
+    } stop_server{server};
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {
@@ -225,6 +240,7 @@ int main(int argc, char** argv) {
     sched.set_timed(true);
     auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch,
                            drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure, depth);
+    if (server) nb::check(nbg_maglev_set_host_ring(pipe.groups->handle(), server), "nbg_maglev_set_host_ring");
     // run until the capture is consumed, no batch is on the GPU and every group queue has drained
     const auto t0 = std::chrono::steady_clock::now();
     for (int idle = 0; idle < 2 * static_cast<int>(names.size() + 2);) {

@@ -26,6 +26,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <numeric>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -238,8 +239,10 @@ inline bool enqueue_grouped_from(MBuf* const* batch, const uint32_t* perm, const
                                  std::vector<std::shared_ptr<MpscQueue>>& queues, EnqueueStats& st, EnqueueCursor& c,
                                  bool stall) {
   const size_t ct = queues.size();
+  const size_t n = std::accumulate(counts, counts + ct + 1, size_t{0});
   for (; c.g <= ct; ++c.g, c.j = 0) {
     for (; c.j < counts[c.g]; ++c.j, ++c.k) {
+      if (c.k + 8 < n) __builtin_prefetch(batch[perm[c.k + 8]], 1, 0);  // the mbufs come in group order
       MBuf* m = batch[perm[c.k]];
       if (c.g == ct) {  // mbuf_free (native/zcsi/zcsi.rs:44): the port owns the storage here
         ++st.would_panic;
@@ -364,6 +367,7 @@ class GroupBy {
   uint64_t in_flight() const { return producer_->in_flight_pkts; }
   uint64_t batches() const { return producer_->batches; }
   const ProducerProfile& profile() const { return producer_->prof; }
+  nbg_maglev* handle() const { return producer_->fn.handle(); }
 
  private:
   struct InFlight {

@@ -20,7 +20,7 @@ from ._lib import (NBG_DEFER_GROUP, NBG_GROUP_LAG, NBG_HOST_SLOTS, NBG_LUT_LDS, 
                    NBG_SENTINEL, NBG_STREAM_DESC, NbgBatch, NbgDescBatch, NbgRingBatch,
                    NBG_SWAP_MACS, NBG_WB_PARTIAL, check, lib)
 
-__all__ = ["Maglev", "GroupedBatch", "Ring", "RingQueue", "build_lut", "make_trace", "NBG_SENTINEL"]
+__all__ = ["Maglev", "GroupedBatch", "Ring", "RingQueue", "HostRing", "build_lut", "make_trace", "NBG_SENTINEL"]
 
 
 def _ptr(t) -> Optional[int]:
@@ -387,6 +387,11 @@ class Maglev:
         (default: a new torch stream) that takes batches as they are posted until stop()."""
         return Ring(self, stride=stride, frame_len=frame_len, swap_macs=swap_macs, idle_ms=idle_ms, stream=stream)
 
+    def use_host_ring(self, ring: Optional["HostRing"]) -> None:
+        """nbg_maglev_set_host_ring: this handle's direct host batches (<= 2,048 packets) go to the
+        device's host-batch server instead of a kernel launch each (None detaches)."""
+        check(lib.nbg_maglev_set_host_ring(self._h, None if ring is None else ring._r), "nbg_maglev_set_host_ring")
+
     def host_query(self, ticket: int) -> bool:
         """nbg_maglev_host_query: True once batch `ticket` has finished on the GPU (non-blocking)."""
         done = C.c_int(0)
@@ -658,6 +663,32 @@ class RingQueue:
         if self._q is not None:
             q, self._q = self._q, None
             check(lib.nbg_ring_queue_close(q), "nbg_ring_queue_close")
+
+
+class HostRing:
+    """The device's host-batch server (nbg_host_ring_*): one persistent kernel whose blocks classify and
+    group the direct host batches of every attached handle (Maglev.use_host_ring) without a kernel
+    launch per batch.  stop() ends it once every posted batch is done (handles detached first)."""
+
+    def __init__(self, device: int = 0, blocks: int = 0, idle_ms: int = 2000):
+        h = C.c_void_p()
+        check(lib.nbg_host_ring_start(device, blocks, idle_ms, C.byref(h)), "nbg_host_ring_start")
+        self._r = h
+        self.device = device
+
+    def stop(self) -> None:
+        if self._r is not None:
+            r, self._r = self._r, None
+            rc = lib.nbg_host_ring_stop(r)
+            if rc == _lib.NBG_EBUSY and "still use it" in _lib.last_error():
+                self._r = r  # handles attached: nothing was stopped
+            check(rc, "nbg_host_ring_stop")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.stop()
 
 
 class HostRegion:

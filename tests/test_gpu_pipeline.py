@@ -38,10 +38,11 @@ def read_pcap(path):
     return out
 
 
-def run_pipeline(tmp_path, frames, names, batch=992, zero_copy=False, drop_on_full=False, depth=3):
+def run_pipeline(tmp_path, frames, names, batch=992, zero_copy=False, drop_on_full=False, depth=3, server=-1):
     rx, tx, order = tmp_path / "in.pcap", tmp_path / "out.pcap", tmp_path / "order.txt"
     write_pcap(rx, frames)
-    args = [NB, "--rx", str(rx), "--tx", str(tx), "--order", str(order), "--batch", str(batch), "--depth", str(depth)]
+    args = [NB, "--rx", str(rx), "--tx", str(tx), "--order", str(order), "--batch", str(batch), "--depth", str(depth),
+            "--host-ring", str(server)]
     args += ["--zero-copy", "1" if zero_copy else "0", "--drop-on-full", "1" if drop_on_full else "0"]
     args += ["--names", ",".join(names)]
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
@@ -88,9 +89,10 @@ def test_lemmy_pcap_through_pipeline(torch_cuda, tmp_path, zero_copy):
     assert (f'"zero_copy": {"true" if zero_copy else "false"}') in stdout
 
 
-@pytest.mark.parametrize("batch,zero_copy,depth", [(32, False, 3), (4096, False, 3), (4096, True, 3), (320, False, 3),
-                                                 (320, True, 2), (992, False, 1)])
-def test_c1_10k_udp_pcap_65_backends(torch_cuda, tmp_path, batch, zero_copy, depth):
+@pytest.mark.parametrize("batch,zero_copy,depth,server", [(32, False, 3, -1), (4096, False, 4, -1), (4096, True, 4, -1),
+                                                        (320, False, 3, -1), (320, True, 2, -1), (992, False, 1, -1),
+                                                        (992, False, 4, 32), (992, True, 4, 8), (32, False, 4, 2)])
+def test_c1_10k_udp_pcap_65_backends(torch_cuda, tmp_path, batch, zero_copy, depth, server):
     """BASELINE config C1: 65 backends / 65537-slot table, 10k-packet UDP pcap.  The group queues
     keep the reference's 1024 slots; --batch 4096 is capped at 992 packets (whole bursts, <= 1023);
     up to `depth` batches are on the GPU at once, delivered in submit order, and the producer waits
@@ -100,19 +102,21 @@ def test_c1_10k_udp_pcap_65_backends(torch_cuda, tmp_path, batch, zero_copy, dep
     buf, off, ln = make_trace(10000, 0, seed=2024)
     frames = [buf[o:o + l].tobytes() for o, l in zip(off, ln)]
     names = [f"backend-{i}" for i in range(65)]
-    out, idx, stdout = run_pipeline(tmp_path, frames, names, batch=batch, zero_copy=zero_copy, depth=depth)
+    out, idx, stdout = run_pipeline(tmp_path, frames, names, batch=batch, zero_copy=zero_copy, depth=depth,
+                                    server=server)
     check(frames, names, out, idx)
     assert '"dropped": 0' in stdout
     assert f'"max_batch": {min(batch, 992)}' in stdout
     assert f'"depth": {depth}' in stdout
 
 
-@pytest.mark.parametrize("zero_copy,drop_on_full", [(False, False), (True, False), (False, True)])
-def test_loop_pipelines_account_for_every_packet(torch_cuda, tmp_path, zero_copy, drop_on_full):
+@pytest.mark.parametrize("zero_copy,drop_on_full,server", [(False, False, -1), (True, False, -1), (False, True, -1),
+                                                         (False, False, 32), (True, False, 32)])
+def test_loop_pipelines_account_for_every_packet(torch_cuda, tmp_path, zero_copy, drop_on_full, server):
     """nb_maglev --loop (the throughput mode: LoopPort replay ports, one pipeline per thread with its
-    own handle and stream): 3 pipelines x 300k packets of a C1-style capture through 992-packet
-    batches, 3 in flight; every received packet is sent, dropped or would-panic, and nothing is
-    dropped with backpressure."""
+    own handle and stream; with and without the host-batch server): 3 pipelines x 300k packets of a
+    C1-style capture through 992-packet batches, several in flight; every received packet is sent,
+    dropped or would-panic, and nothing is dropped with backpressure."""
     import json
 
     from netbricks_amd import make_trace
@@ -121,7 +125,8 @@ def test_loop_pipelines_account_for_every_packet(torch_cuda, tmp_path, zero_copy
     rx = tmp_path / "c1.pcap"
     write_pcap(rx, [buf[o:o + l].tobytes() for o, l in zip(off, ln)])
     args = [NB, "--rx", str(rx), "--backends", "65", "--batch", "992", "--loop", "300000", "--pipelines", "3",
-            "--zero-copy", "1" if zero_copy else "0", "--drop-on-full", "1" if drop_on_full else "0"]
+            "--zero-copy", "1" if zero_copy else "0", "--drop-on-full", "1" if drop_on_full else "0",
+            "--host-ring", str(server)]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     st = json.loads(r.stdout)

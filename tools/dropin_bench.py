@@ -9,6 +9,8 @@ framework/src/operators/group_by.rs:43-55).
 scheduler/context.rs:55-69,241-255), each replaying a C1-style capture (10k 64-B UDP frames, 65
 backends / 65537) through a LoopPort (the reference's VirtualPort: recv hands out mbufs, send frees
 them).  Producer and consumer (merge + send) tasks share each pipeline's thread, as in the reference.
+Every pipeline's batches go to the device's host-batch server (nbg_host_ring_*, 32 blocks), up to 4
+in flight per pipeline.
 
 This process never initialises the GPU: it writes the capture (host trace generator) and runs
 nb_maglev as child processes.  Prints one JSON line.
@@ -37,12 +39,12 @@ def write_c1_pcap(path, n=10000, seed=2024):
             f.write(buf[o:o + l].tobytes())
 
 
-def run(pcap, pipelines, total, batch=992, depth=3, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
-        env=None, timeout=120):
+def run(pcap, pipelines, total, batch=992, depth=4, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
+        server=-1, env=None, timeout=120):
     args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
             "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
-            "--hugepages", "1" if huge else "0"]
+            "--hugepages", "1" if huge else "0", "--host-ring", str(server)]
     r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True,
                        env=dict(os.environ, **(env or {})))
     if r.returncode != 0:
@@ -55,8 +57,9 @@ def main():
     ap.add_argument("--total", type=int, default=20_000_000, help="packets received per pipeline")
     ap.add_argument("--pipelines", default="1,4,16")
     ap.add_argument("--extra", action="store_true",
-                    help="also zero-copy, 4-KiB pages, 4 hardware queues, depth 1, 496-packet batches, drop-on-full")
+                    help="also zero-copy, depth 3, drop-on-full, 4-KiB pages, and a kernel launch per batch")
     ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
+    ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
     args = ap.parse_args()
     if args.write_pcap:
         write_c1_pcap(args.write_pcap)
@@ -65,19 +68,32 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         pcap = os.path.join(d, "c1.pcap")
         write_c1_pcap(pcap)
-        runs = [(f"p{p}", dict(pipelines=int(p))) for p in args.pipelines.split(",")]
+        # the rows: every pipeline's batches through the device's host-batch server (32 blocks), 4 in
+        # flight per pipeline, staged 48-B windows; then (extra) each choice against its alternative
+        runs = [(f"p{p}", dict(pipelines=int(p), server=32)) for p in args.pipelines.split(",")]
+        if args.tune:
+            runs = [(f"p16_server_ahead{a}", dict(pipelines=16, server=32, env={"NBG_GATHER_AHEAD": str(a)}))
+                    for a in (16, 32, 64)]
+            runs += [("p16_server64", dict(pipelines=16, server=64)), ("p16_server16", dict(pipelines=16, server=16)),
+                     ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
+                     ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
+                     ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
         if args.extra:
             top = max(int(p) for p in args.pipelines.split(","))
-            runs += [(f"p{top}_zero_copy", dict(pipelines=top, zero_copy=True)),
-                     ("p4_zero_copy", dict(pipelines=4, zero_copy=True)),
-                     ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
-                     (f"p{top}_4k_pages", dict(pipelines=top, huge=False)),
-                     (f"p{top}_zero_copy_4k_pages", dict(pipelines=top, zero_copy=True, huge=False)),
-                     (f"p{top}_hwq4", dict(pipelines=top, hw_queues=4)),
-                     (f"p{top}_depth1", dict(pipelines=top, depth=1)),
-                     (f"p{top}_b496", dict(pipelines=top, batch=496)),
-                     (f"p{top}_drop_on_full", dict(pipelines=top, drop_on_full=True)),
-                     ("p1_depth1", dict(pipelines=1, depth=1))]
+            runs += [(f"p{top}_server_zero_copy", dict(pipelines=top, server=32, zero_copy=True)),
+                     ("p1_server_zero_copy", dict(pipelines=1, server=32, zero_copy=True)),
+                     (f"p{top}_server_depth3", dict(pipelines=top, server=32, depth=3)),
+                     (f"p{top}_server_drop_on_full", dict(pipelines=top, server=32, drop_on_full=True)),
+                     (f"p{top}_server_4k_pages", dict(pipelines=top, server=32, huge=False)),
+                     (f"p{top}_launch", dict(pipelines=top)),
+                     ("p4_launch", dict(pipelines=4)),
+                     ("p1_launch", dict(pipelines=1)),
+                     (f"p{top}_launch_zero_copy", dict(pipelines=top, zero_copy=True)),
+                     ("p1_launch_zero_copy", dict(pipelines=1, zero_copy=True)),
+                     (f"p{top}_launch_hwq4", dict(pipelines=top, hw_queues=4)),
+                     (f"p{top}_launch_zero_copy_4k_pages", dict(pipelines=top, zero_copy=True, huge=False)),
+                     (f"p{top}_launch_b496", dict(pipelines=top, batch=496)),
+                     ("p1_launch_depth1", dict(pipelines=1, depth=1))]
         for name, kw in runs:
             r = run(pcap, total=args.total, **kw)
             out[name] = r
@@ -91,8 +107,9 @@ def main():
             prod = sum(r["rx_per_pipeline"] / s for s in r["producer_seconds"] if s > 0)
             rows.append({"pipelines": r["pipelines"], "per_pipeline_mpps": round(sum(per) / len(per), 2),
                          "aggregate_mpps": r["aggregate_mpps"], "producer_only_mpps": round(prod / 1e6, 1)})
-    print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024,
-                      "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, LoopPort replay"}))
+    print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024, "depth": 4,
+                      "server_blocks": 32, "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, "
+                                                      "LoopPort replay (2-KiB mbufs in huge pages)"}))
 
 
 if __name__ == "__main__":
