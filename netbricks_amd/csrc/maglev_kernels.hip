@@ -2196,14 +2196,18 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
     off[r] = a.off ? a.off[p] : p * a.stride;
     len[r] = a.len ? a.len[p] : a.fixed_len;
   }
+  // owned windows (slots of >= 64 B, mbuf data rooms, the host path's staging): the 48 B at every
+  // packet start are readable whatever its length, so the window loads do not wait for len[] (over
+  // PCIe, for the host path's direct batches, one round trip less per batch)
+  const bool owned = a.win_owned != 0;
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
 #pragma unroll
     for (uint32_t k = 0; k < 3; ++k) {
       const uint32_t q = 64u * k + lane, pi = q / 3u, part = q - 3u * pi;
-      const uint32_t o = __shfl(off[r], static_cast<int>(pi)), l = __shfl(len[r], static_cast<int>(pi));
-      const uint8_t* pk = a.pkts + o;
-      const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && l >= 48u;
+      const uint8_t* pk = a.pkts + __shfl(off[r], static_cast<int>(pi));
+      bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0;
+      if (!owned) vec = vec && __shfl(len[r], static_cast<int>(pi)) >= 48u;
       // the batch base is 16-B aligned by the host check; its 48 B are read for packets off the path
       v[r][k] = *reinterpret_cast<const uint4*>((vec ? pk : a.pkts) + 16u * part);
     }
