@@ -2207,7 +2207,12 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
       const uint32_t q = 64u * k + lane, pi = q / 3u, part = q - 3u * pi;
       const uint8_t* pk = a.pkts + __shfl(off[r], static_cast<int>(pi));
       bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0;
-      if (!owned) vec = vec && __shfl(len[r], static_cast<int>(pi)) >= 48u;
+      if (!owned) {
+        // every lane shuffles (not under `vec &&`: a bpermute from a lane the short-circuit
+        // disabled reads 0, and the packet would then take the batch base's window)
+        const uint32_t l = __shfl(len[r], static_cast<int>(pi));
+        vec = vec && l >= 48u;
+      }
       // the batch base is 16-B aligned by the host check; its 48 B are read for packets off the path
       v[r][k] = *reinterpret_cast<const uint4*>((vec ? pk : a.pkts) + 16u * part);
     }
