@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--k", default="4,8")
     ap.add_argument("--calls", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--nohist", action="store_true",
+                    help="also time the launch without grouping (no per-unit histogram in the classify kernel)")
     args = ap.parse_args()
     import torch
 
@@ -77,6 +79,19 @@ def main():
             kt.close()
             for h in hs:
                 h.check()
+            if args.nohist:
+                na = (NbgBatch * k)()
+                for q in range(k):
+                    o = keep[-(ms * k) + q]
+                    na[q] = NbgBatch(bufs[q].data_ptr(), n, o[0].data_ptr(), None, None, None)
+                kt2 = KernelTimer(calls)
+                for i in range(calls):
+                    kt2.start(i, st)
+                    assert lib.nbg_maglev_classify_device_multi(hs[0]._h, na, k, 64, 60, NBG_SWAP_MACS, st) == 0
+                    kt2.stop(i, st)
+                torch.cuda.synchronize()
+                out[f"k{k}_r{rnd}_nohist_classify_us_per_batch"] = round(float(kt2.ms().mean()) * 1e3 / k, 2)
+                kt2.close()
             out[f"k{k}_r{rnd}"] = {"path_us_per_batch": round(el / (calls * k) * 1e6, 2),
                                    "classify_us_per_batch": round(kus / k, 2), "frac": round(n * 78 / (kus / k) / 8e6, 4)}
     print(json.dumps(out), flush=True)

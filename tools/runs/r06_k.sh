@@ -12,3 +12,6 @@ timeout -k 10 200 python3 bench.py --steps 20 --warmup 30 $F > $O/w30.json 2> $O
 timeout -k 10 200 python3 bench.py --steps 20 --warmup 100 $F > $O/w100.json 2> $O/w100.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ktrace -o run -- python3 bench.py --steps 20 --warmup 5 $F > $O/prof.json 2> $O/prof.err
 echo "rc=$?" >> $O/done.txt
+# the multi launch with and without the classify kernel's per-unit histogram (verdict item 5)
+timeout -k 10 200 python3 tools/c2_multik.py --k 4,8 --nohist > $O/multik.json 2> $O/multik.err
+echo "rc2=$?" >> $O/done.txt
