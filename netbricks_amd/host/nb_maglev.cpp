@@ -16,14 +16,17 @@
 // the pipeline has room and drops on a full queue, as the reference's producer does (group_by.rs:50).
 //
 // --loop TOTAL: each of P pipelines (--pipelines, default 1) runs on a thread of its own, pinned to
-// one of the process's CPUs, with its own replay port (LoopPort: the capture's frames in a 64k-mbuf
-// pool of 2-KiB data rooms in transparent huge pages, as DPDK's mempools are in hugepages; --hugepages 0
-// for 4-KiB pages; received until TOTAL packets, freed by send — the reference's VirtualPort), its own
+// one of the process's CPUs, with its own replay port (LoopPort: the capture's frames in a pool of
+// --pool mbufs (default 8,192, rounded up to whole copies of the capture) with 2-KiB data rooms in
+// transparent huge pages, as DPDK's mempools are in hugepages; --hugepages 0 for 4-KiB pages; received
+// until TOTAL packets, freed by send — the reference's VirtualPort), its own
 // scheduler, its own Maglev handle and stream: the reference's one pipeline per RX queue and core
 // (scheduler/context.rs:55-69,241-255).  The JSON line then gives each pipeline's Mpps (rx packets
 // over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
 // slowest pipeline's time).  --host-ring B attaches every pipeline's handle to one host-batch server
 // of B blocks (nbg_host_ring_*: one persistent kernel takes the batches; no kernel launch per batch).
+// The JSON's per-phase profile and producer seconds come from TSC reads around every task execution and
+// producer phase; --profile 0 turns them off (the NF rate without them: within ~2 %).
 #include <pthread.h>
 #include <sched.h>
 
@@ -45,6 +48,7 @@ struct LoopResult {
   nb::ProducerProfile prof;
   double seconds = 0, producer_seconds = 0;
   bool huge = false;
+  size_t pool = 0;
   uint64_t rx = 0, tx = 0, dropped = 0, would_panic = 0, batches = 0, stalls = 0;
   std::string error;
 };
@@ -67,7 +71,7 @@ void pin_to(int k) {
 
 int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
              uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge,
-             nbg_host_ring* server) {
+             nbg_host_ring* server, size_t pool_mbufs, bool profiled) {
   const auto recs = nb::read_pcap(rx);
   std::vector<LoopResult> res(pipelines);
   std::atomic<int> ready{0};
@@ -79,14 +83,15 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
       bool counted = false;
       try {
         pin_to(p);
-        auto port = std::make_shared<nb::LoopPort>(recs, total, 65536, 2048, huge);
+        auto port = std::make_shared<nb::LoopPort>(recs, total, pool_mbufs, 2048, huge);
         auto pool = port->mempool();
         uint8_t* dev = nullptr;
         if (zero_copy) nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
         nb::StandaloneScheduler sched;
-        sched.set_timed(true);
+        sched.set_timed(profiled);
         auto pipe = nb::maglev(std::make_shared<nb::ReceiveBatch>(port), sched, names, port, table, batch,
                                drop_on_full ? nb::Admission::kDropOnFull : nb::Admission::kBackpressure, depth);
+        pipe.groups->set_profiled(profiled);
         if (server) nb::check(nbg_maglev_set_host_ring(pipe.groups->handle(), server), "nbg_maglev_set_host_ring");
         ++ready;
         counted = true;
@@ -102,6 +107,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
         r.producer_seconds = sched.task_seconds(0);
         r.rx = port->rx_total();
         r.huge = port->huge_pages();
+        r.pool = port->pool_size();
         r.tx = port->tx_total();
         r.dropped = pipe.groups->dropped();
         r.would_panic = pipe.groups->would_panic();
@@ -149,12 +155,12 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
     return 1;
   }
   std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
-              "\"host_ring\": %s, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"host_ring\": %s, \"profiled\": %s, \"pool_mbufs\": %zu, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
               "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
               "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
               "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
               "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
-              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", huge_all ? "true" : "false",
+              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", profiled ? "true" : "false", res[0].pool, huge_all ? "true" : "false",
               std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "", zero_copy ? "true" : "false",
               drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
               static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
@@ -174,6 +180,13 @@ int main(int argc, char** argv) {
   uint64_t table = 65537, loop = 0;
   uint32_t batch = nb::kMaxGpuBatch, depth = nb::kMaxDepth;
   int pipelines = 1, hw_queues = 0, ring_blocks = -1;
+  // mbufs per replay port: at least 8,192 (up to 4 x 992 in flight plus the group queues), rounded up
+  // to whole copies of the capture by LoopPort.  The reference's default pool is 2,047 mbufs
+  // (DEFAULT_POOL_SIZE, config/config_reader.rs:8) for a producer that holds no batch in flight; a
+  // pool far larger than needed only spreads the mbufs' lines over more cache (64k mbufs: 297 against
+  // 370 Mpps at 16 pipelines, profiles/r06_dropin_pool.json)
+  size_t pool_mbufs = 8192;
+  bool profiled = true;
   bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -188,6 +201,8 @@ int main(int argc, char** argv) {
     else if (k == "--hw-queues") hw_queues = std::atoi(v.c_str());
     else if (k == "--hugepages") huge = std::atoi(v.c_str()) != 0;
     else if (k == "--host-ring") ring_blocks = std::atoi(v.c_str());
+    else if (k == "--pool") pool_mbufs = std::strtoull(v.c_str(), nullptr, 10);
+    else if (k == "--profile") profiled = std::atoi(v.c_str()) != 0;
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -229,7 +244,7 @@ int main(int argc, char** argv) {
         if (s && nbg_host_ring_stop(s) != NBG_OK) std::fprintf(stderr, "nb_maglev: %s\n", nbg_last_error());
       }
     } stop_server{server};
-    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server);
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server, pool_mbufs, profiled);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {

@@ -29,11 +29,48 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
+
+#if defined(__x86_64__)
+#include <x86intrin.h>
+#endif
 
 #include "../../include/nbgpu.h"
 
 namespace nb {
+
+// ---- timing -------------------------------------------------------------------------------
+// The throughput runs time every scheduler task and producer phase, hundreds of reads per 992-packet
+// batch (a consumer execution moves one burst of one group), so the read itself must be cheap: the
+// invariant TSC on x86-64 (one instruction, ~10-20 ns against ~20-40 for steady_clock::now, measured),
+// converted with a rate calibrated once against steady_clock.
+struct TscClock {
+  using tick = uint64_t;
+  static tick now() {
+#if defined(__x86_64__)
+    return __rdtsc();
+#else
+    return static_cast<tick>(std::chrono::steady_clock::now().time_since_epoch().count());
+#endif
+  }
+  static double seconds_per_tick() {
+    static const double spt = [] {
+#if defined(__x86_64__)
+      const auto c0 = std::chrono::steady_clock::now();
+      const tick t0 = now();
+      std::this_thread::sleep_for(std::chrono::milliseconds(20));
+      const tick t1 = now();
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
+      return s / static_cast<double>(t1 - t0);
+#else
+      return static_cast<double>(std::chrono::steady_clock::period::num) / std::chrono::steady_clock::period::den;
+#endif
+    }();
+    return spt;
+  }
+  static double since(tick t0) { return static_cast<double>(now() - t0) * seconds_per_tick(); }
+};
 
 // ---- packets ----------------------------------------------------------------------------
 // Stand-in for rte_mbuf: data pointer + data_len + the metadata slots NetBricks uses to save the
@@ -140,20 +177,25 @@ class StandaloneScheduler {
       for (auto& t : tasks_) t->execute();
       return;
     }
-    seconds_.resize(tasks_.size());
+    ticks_.resize(tasks_.size());
     for (size_t i = 0; i < tasks_.size(); ++i) {
-      const auto t0 = std::chrono::steady_clock::now();
+      const TscClock::tick t0 = TscClock::now();
       tasks_[i]->execute();
-      seconds_[i] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      ticks_[i] += TscClock::now() - t0;
     }
   }
   // per-task wall time accumulated over execute_round() (for throughput breakdowns; off by default)
-  void set_timed(bool on) { timed_ = on; }
-  double task_seconds(size_t i) const { return i < seconds_.size() ? seconds_[i] : 0.0; }
+  void set_timed(bool on) {
+    if (on) TscClock::seconds_per_tick();  // calibrated before the run, not inside it
+    timed_ = on;
+  }
+  double task_seconds(size_t i) const {
+    return i < ticks_.size() ? static_cast<double>(ticks_[i]) * TscClock::seconds_per_tick() : 0.0;
+  }
 
  private:
   std::vector<std::shared_ptr<Executable>> tasks_;
-  std::vector<double> seconds_;
+  std::vector<TscClock::tick> ticks_;
   bool timed_ = false;
 };
 
@@ -367,6 +409,10 @@ class GroupBy {
   uint64_t in_flight() const { return producer_->in_flight_pkts; }
   uint64_t batches() const { return producer_->batches; }
   const ProducerProfile& profile() const { return producer_->prof; }
+  void set_profiled(bool on) {
+    if (on) TscClock::seconds_per_tick();
+    producer_->timed = on;
+  }
   nbg_maglev* handle() const { return producer_->fn.handle(); }
 
  private:
@@ -402,7 +448,7 @@ class GroupBy {
         InFlight& b = slots[head];
         if (!b.waited) {
           int done = 0;
-          const auto t0 = Clock::now();
+          const Clock::tick t0 = tnow();
           check(nbg_maglev_host_query(fn.handle(), b.ticket, &done), "nbg_maglev_host_query");
           prof.query += since(t0);
           ++prof.queries;
@@ -411,7 +457,7 @@ class GroupBy {
         if (!deliver(b)) break;  // a full queue (backpressure): resumed at the next execution
       }
       if (n_in_flight == depth || !admit_batch(queues, max_batch, admission)) return;
-      const auto t0 = Clock::now();
+      const Clock::tick t0 = tnow();
       InFlight& b = slots[(head + n_in_flight) % depth];
       b.batch.clear();
       for (;;) {  // whole bursts only: max_batch is a multiple of kBurst
@@ -428,8 +474,8 @@ class GroupBy {
         b.ptrs[i] = b.batch[i]->data();
         b.lens[i] = b.batch[i]->data_len;
       }
-      const auto t1 = Clock::now();
-      prof.pull += std::chrono::duration<double>(t1 - t0).count();
+      const Clock::tick t1 = tnow();
+      prof.pull += static_cast<double>(t1 - t0) * TscClock::seconds_per_tick();
       check(nbg_maglev_host_submit(fn.handle(), b.ptrs.data(), b.lens.data(), n, parent.swap ? NBG_SWAP_MACS : 0u,
                                    b.backend.data(), b.perm.data(), b.counts.data(), &b.ticket),
             "nbg_maglev_host_submit");
@@ -444,12 +490,12 @@ class GroupBy {
     // false: stopped at a full queue (backpressure); the batch stays at the head
     bool deliver(InFlight& b) {
       if (!b.waited) {
-        const auto t0 = Clock::now();
+        const Clock::tick t0 = tnow();
         check(nbg_maglev_host_wait(fn.handle(), b.ticket), "nbg_maglev_host_wait");
         prof.wait += since(t0);
         b.waited = true;
       }
-      const auto t1 = Clock::now();
+      const Clock::tick t1 = tnow();
       const bool all = enqueue_grouped_from(b.batch.data(), b.perm.data(), b.counts.data(), queues, stats, b.cur,
                                             admission == Admission::kBackpressure);
       prof.enqueue += since(t1);
@@ -472,8 +518,10 @@ class GroupBy {
     EnqueueStats stats;
     uint64_t processed = 0, batches = 0;
     ProducerProfile prof;
-    using Clock = std::chrono::steady_clock;
-    static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+    bool timed = true;  // the per-phase profile (off: no clock reads at all)
+    using Clock = TscClock;
+    Clock::tick tnow() const { return timed ? Clock::now() : 0; }
+    double since(Clock::tick t) const { return timed ? TscClock::since(t) : 0.0; }
   };
 
   uint32_t groups_;

@@ -40,11 +40,15 @@ def write_c1_pcap(path, n=10000, seed=2024):
 
 
 def run(pcap, pipelines, total, batch=992, depth=4, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
-        server=-1, env=None, timeout=120):
+        server=-1, pool=None, profile=True, env=None, timeout=120):
     args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
             "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
             "--hugepages", "1" if huge else "0", "--host-ring", str(server)]
+    if pool:
+        args += ["--pool", str(pool)]
+    if not profile:
+        args += ["--profile", "0"]
     r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True,
                        env=dict(os.environ, **(env or {})))
     if r.returncode != 0:
@@ -60,6 +64,8 @@ def main():
                     help="also zero-copy, depth 3, drop-on-full, 4-KiB pages, and a kernel launch per batch")
     ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
     ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
+    ap.add_argument("--pool-sweep", action="store_true",
+                    help="only the mempool size A/B (mbufs per pipeline's port) at 1, 4 and 16 pipelines")
     args = ap.parse_args()
     if args.write_pcap:
         write_c1_pcap(args.write_pcap)
@@ -78,6 +84,9 @@ def main():
                      ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
                      ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
                      ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
+        if args.pool_sweep:
+            runs = [(f"p{p}_pool{m}{'' if prof else '_noprof'}", dict(pipelines=p, server=32, pool=m, profile=prof))
+                    for p in (1, 4, 16) for m in (10000, 65536) for prof in (True, False)]
         if args.extra:
             top = max(int(p) for p in args.pipelines.split(","))
             runs += [(f"p{top}_server_zero_copy", dict(pipelines=top, server=32, zero_copy=True)),
