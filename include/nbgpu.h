@@ -377,6 +377,16 @@ int nbg_host_register(void* base, uint64_t bytes, int device, uint8_t** dev_base
 int nbg_host_unregister(void* base, int device);
 
 /*
+ * The host CPUs local to a device (its PCI function's local_cpulist in sysfs, in the kernel's order:
+ * the node's physical cores first, then their SMT siblings), for pinning the producer threads that feed
+ * it, as a DPDK application puts its lcores on the NIC's socket.  Writes up to cap CPU numbers to cpus
+ * and their count to *n (which may exceed cap).  NBG_ENODEV without the device, NBG_EIO when sysfs
+ * does not say.  Replaces no reference interface: NetBricks takes its cores from the configuration
+ * (config/config_reader.rs), the integration picks them from this list.
+ */
+int nbg_device_local_cpus(int device, int32_t* cpus, uint32_t cap, uint32_t* n);
+
+/*
  * Host-batch server: one persistent kernel per GPU that takes the direct (<= 2,048-packet) batches of
  * nbg_maglev_host_submit / nbg_maglev_classify_host from every handle attached to it, so a batch costs
  * no kernel launch (one launch per 992-packet batch bounds a multi-pipeline drop-in producer by the

@@ -101,6 +101,7 @@ SIGNATURES = {
     "nbg_maglev_host_query": (C.c_int, [_P, C.c_uint64, C.POINTER(C.c_int)]),
     "nbg_host_register": (C.c_int, [_P, C.c_uint64, C.c_int, C.POINTER(_P)]),
     "nbg_host_unregister": (C.c_int, [_P, C.c_int]),
+    "nbg_device_local_cpus": (C.c_int, [C.c_int, C.POINTER(C.c_int32), C.c_uint32, C.POINTER(C.c_uint32)]),
     "nbg_host_ring_start": (C.c_int, [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_P)]),
     "nbg_host_ring_stop": (C.c_int, [_P]),
     "nbg_maglev_set_host_ring": (C.c_int, [_P, _P]),

@@ -11,11 +11,13 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <cctype>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -2394,6 +2396,8 @@ bool host_ring_post(nbg_host_ring* r, const ClassifyArgs& a, const GroupArgs& g,
   if (t >= r->slots) {
     const uint32_t want = static_cast<uint32_t>(t - r->slots + 1);
     for (uint32_t spin = 0; __atomic_load_n(&d->ack, __ATOMIC_ACQUIRE) != want; ++spin) {
+      // a server that ended (idle exit racing an earlier post) never acknowledges the slot: launch
+      if (__atomic_load_n(&r->ctl->ended, __ATOMIC_ACQUIRE)) return false;
       if (spin < 4096) {
         __builtin_ia32_pause();
       } else {
@@ -2593,6 +2597,42 @@ int nbg_host_unregister(void* base, int device) {
   }
   NBG_HIP(hipHostUnregister(base));
   return NBG_OK;
+}
+
+int nbg_device_local_cpus(int device, int32_t* cpus, uint32_t cap, uint32_t* n) {
+  if (!n || (!cpus && cap)) return set_error(NBG_EINVAL, "device_local_cpus: null argument");
+  *n = 0;
+  const int rc = check_device(device);
+  if (rc) return rc;
+  char bus[64] = {0};
+  NBG_HIP(hipDeviceGetPCIBusId(bus, static_cast<int>(sizeof bus) - 1, device));
+  for (char* c = bus; *c; ++c) *c = static_cast<char>(std::tolower(static_cast<unsigned char>(*c)));
+  const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
+  FILE* f = std::fopen(path.c_str(), "r");
+  if (!f) return set_error(NBG_EIO, "device_local_cpus: cannot read %s", path.c_str());
+  char line[4096] = {0};
+  const bool got = std::fgets(line, sizeof line, f) != nullptr;
+  std::fclose(f);
+  if (!got) return set_error(NBG_EIO, "device_local_cpus: %s is empty", path.c_str());
+  // "0-63,128-191": ranges and single CPUs, comma separated
+  uint32_t count = 0;
+  for (const char* p = line; *p && *p != '\n';) {
+    char* end = nullptr;
+    const long lo = std::strtol(p, &end, 10);
+    if (end == p || lo < 0) return set_error(NBG_EIO, "device_local_cpus: cannot parse %s", line);
+    long hi = lo;
+    p = end;
+    if (*p == '-') {
+      hi = std::strtol(p + 1, &end, 10);
+      if (end == p + 1 || hi < lo) return set_error(NBG_EIO, "device_local_cpus: cannot parse %s", line);
+      p = end;
+    }
+    for (long c = lo; c <= hi; ++c, ++count)
+      if (count < cap) cpus[count] = static_cast<int32_t>(c);
+    if (*p == ',') ++p;
+  }
+  *n = count;
+  return count ? NBG_OK : set_error(NBG_EIO, "device_local_cpus: %s lists no CPU", path.c_str());
 }
 
 int nbg_host_ring_start(int device, uint32_t blocks, uint32_t idle_ms, nbg_host_ring** out) {

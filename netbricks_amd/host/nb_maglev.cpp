@@ -25,6 +25,8 @@
 // over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
 // slowest pipeline's time).  --host-ring B attaches every pipeline's handle to one host-batch server
 // of B blocks (nbg_host_ring_*: one persistent kernel takes the batches; no kernel launch per batch).
+// Pipeline p runs on the p-th CPU local to the GPU (--local-cpus 0: of all the process may use), the
+// CPUs dealt over their L3 caches first (--spread-l3 0: in the kernel's order).
 // The JSON's per-phase profile and producer seconds come from TSC reads around every task execution and
 // producer phase; --profile 0 turns them off (the NF rate without them: within ~2 %).
 #include <pthread.h>
@@ -53,26 +55,69 @@ struct LoopResult {
   std::string error;
 };
 
-void pin_to(int k) {
+// The CPUs the pipelines are pinned to, in order: the process's allowed CPUs that are local to the GPU
+// (nbg_device_local_cpus: its socket's physical cores first), or every allowed CPU when none is (or
+// local = false).  A producer thread on the GPU's socket keeps its staged windows and the completion
+// words it polls on the GPU's side of the inter-socket link, as DPDK puts lcores on the NIC's socket.
+std::vector<int> pipeline_cpus(bool local) {
+  std::vector<int> out;
   cpu_set_t allowed;
-  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return;
-  int seen = 0;
-  for (int c = 0; c < CPU_SETSIZE; ++c) {
-    if (!CPU_ISSET(c, &allowed)) continue;
-    if (seen++ == k % CPU_COUNT(&allowed)) {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      CPU_SET(c, &one);
-      pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
-      return;
-    }
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return out;
+  if (local) {
+    std::vector<int32_t> near(1024);
+    uint32_t n = 0;
+    if (nbg_device_local_cpus(0, near.data(), static_cast<uint32_t>(near.size()), &n) == NBG_OK)
+      for (uint32_t i = 0; i < std::min<uint32_t>(n, static_cast<uint32_t>(near.size())); ++i)
+        if (near[i] >= 0 && near[i] < CPU_SETSIZE && CPU_ISSET(near[i], &allowed)) out.push_back(near[i]);
   }
+  if (out.empty())
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) out.push_back(c);
+  return out;
+}
+
+// The same CPUs dealt round-robin over their L3 caches (sysfs cache/index3 of each CPU; the order
+// within one L3 kept): 16 pipelines then take two cores on each of eight 8-core CCDs instead of all
+// eight cores of two, so each thread has an L3 share and a CCD link share four times as large.
+std::vector<int> spread_over_l3(const std::vector<int>& cpus) {
+  std::vector<std::string> keys;
+  std::vector<std::vector<int>> groups;
+  for (int c : cpus) {
+    std::string key = "?";
+    const std::string path = "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/shared_cpu_list";
+    if (FILE* f = std::fopen(path.c_str(), "r")) {
+      char line[256] = {0};
+      if (std::fgets(line, sizeof line, f)) key = line;
+      std::fclose(f);
+    }
+    size_t g = 0;
+    while (g < keys.size() && keys[g] != key) ++g;
+    if (g == keys.size()) {
+      keys.push_back(key);
+      groups.emplace_back();
+    }
+    groups[g].push_back(c);
+  }
+  std::vector<int> out;
+  for (size_t i = 0; out.size() < cpus.size(); ++i)
+    for (auto& g : groups)
+      if (i < g.size()) out.push_back(g[i]);
+  return out;
+}
+
+void pin_to(int k, const std::vector<int>& cpus) {
+  if (cpus.empty()) return;
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(cpus[static_cast<size_t>(k) % cpus.size()], &one);
+  pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
 }
 
 int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
              uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge,
-             nbg_host_ring* server, size_t pool_mbufs, bool profiled) {
+             nbg_host_ring* server, size_t pool_mbufs, bool profiled, bool local, bool spread) {
   const auto recs = nb::read_pcap(rx);
+  const std::vector<int> cpus = spread ? spread_over_l3(pipeline_cpus(local)) : pipeline_cpus(local);
   std::vector<LoopResult> res(pipelines);
   std::atomic<int> ready{0};
   std::atomic<bool> go{false};
@@ -82,7 +127,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
       LoopResult& r = res[p];
       bool counted = false;
       try {
-        pin_to(p);
+        pin_to(p, cpus);
         auto port = std::make_shared<nb::LoopPort>(recs, total, pool_mbufs, 2048, huge);
         auto pool = port->mempool();
         uint8_t* dev = nullptr;
@@ -154,13 +199,16 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
     std::fprintf(stderr, "nb_maglev: %s\n", err.c_str());
     return 1;
   }
+  std::string cpu_list;
+  for (int p = 0; p < pipelines && !cpus.empty(); ++p)
+    cpu_list += (p ? "," : "") + std::to_string(cpus[static_cast<size_t>(p) % cpus.size()]);
   std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
-              "\"host_ring\": %s, \"profiled\": %s, \"pool_mbufs\": %zu, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"host_ring\": %s, \"profiled\": %s, \"cpus\": \"%s\", \"pool_mbufs\": %zu, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
               "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
               "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
               "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
               "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
-              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", profiled ? "true" : "false", res[0].pool, huge_all ? "true" : "false",
+              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", profiled ? "true" : "false", cpu_list.c_str(), res[0].pool, huge_all ? "true" : "false",
               std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "", zero_copy ? "true" : "false",
               drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
               static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
@@ -186,7 +234,7 @@ int main(int argc, char** argv) {
   // pool far larger than needed only spreads the mbufs' lines over more cache (64k mbufs: 297 against
   // 370 Mpps at 16 pipelines, profiles/r06_dropin_pool.json)
   size_t pool_mbufs = 8192;
-  bool profiled = true;
+  bool profiled = true, local = true, spread = true;
   bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -203,6 +251,8 @@ int main(int argc, char** argv) {
     else if (k == "--host-ring") ring_blocks = std::atoi(v.c_str());
     else if (k == "--pool") pool_mbufs = std::strtoull(v.c_str(), nullptr, 10);
     else if (k == "--profile") profiled = std::atoi(v.c_str()) != 0;
+    else if (k == "--local-cpus") local = std::atoi(v.c_str()) != 0;
+    else if (k == "--spread-l3") spread = std::atoi(v.c_str()) != 0;
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -244,7 +294,7 @@ int main(int argc, char** argv) {
         if (s && nbg_host_ring_stop(s) != NBG_OK) std::fprintf(stderr, "nb_maglev: %s\n", nbg_last_error());
       }
     } stop_server{server};
-    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server, pool_mbufs, profiled);
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server, pool_mbufs, profiled, local, spread);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {

@@ -298,6 +298,12 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(nb.NbgError) as e:
         nb.Maglev(["a", "b"])
     assert e.value.code == -19
+    import ctypes as C
+
+    from netbricks_amd._lib import lib
+
+    n = C.c_uint32(7)
+    assert lib.nbg_device_local_cpus(0, None, 0, C.byref(n)) == -19 and n.value == 0
 
 
 def test_oracle_is_test_infrastructure_only():

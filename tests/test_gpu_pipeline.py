@@ -134,6 +134,28 @@ def test_loop_pipelines_account_for_every_packet(torch_cuda, tmp_path, zero_copy
     assert st["would_panic"] == 0 and len(st["per_pipeline_mpps"]) == 3 and st["aggregate_mpps"] > 0
     if not drop_on_full:
         assert st["dropped"] == 0 and st["tx"] == 900000
+    # one mempool of 10,000 mbufs per port (the capture, once), threads on CPUs the process may use
+    assert st["pool_mbufs"] == 10000
+    cpus = [int(c) for c in st["cpus"].split(",")]
+    assert len(cpus) == 3 and set(cpus) <= os.sched_getaffinity(0)
+
+
+def test_device_local_cpus(torch_cuda):
+    """nbg_device_local_cpus: the CPUs of the GPU's socket from sysfs (nb_maglev pins its pipelines to
+    them): a non-empty list of distinct CPUs of this machine; a short buffer still reports the count."""
+    import ctypes as C
+
+    from netbricks_amd._lib import lib
+
+    buf = (C.c_int32 * 4096)()
+    n = C.c_uint32()
+    assert lib.nbg_device_local_cpus(0, buf, 4096, C.byref(n)) == 0
+    cpus = list(buf[:n.value])
+    assert 0 < n.value <= os.cpu_count() and len(set(cpus)) == n.value
+    assert all(0 <= c < os.cpu_count() for c in cpus)
+    m = C.c_uint32()
+    assert lib.nbg_device_local_cpus(0, buf, 1, C.byref(m)) == 0 and m.value == n.value and buf[0] == cpus[0]
+    assert lib.nbg_device_local_cpus(99, buf, 4096, C.byref(m)) != 0
 
 
 def test_c1_drop_on_full_keeps_reference_semantics(torch_cuda, tmp_path):

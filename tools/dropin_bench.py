@@ -10,7 +10,8 @@ scheduler/context.rs:55-69,241-255), each replaying a C1-style capture (10k 64-B
 backends / 65537) through a LoopPort (the reference's VirtualPort: recv hands out mbufs, send frees
 them).  Producer and consumer (merge + send) tasks share each pipeline's thread, as in the reference.
 Every pipeline's batches go to the device's host-batch server (nbg_host_ring_*, 32 blocks), up to 4
-in flight per pipeline.
+in flight per pipeline; each pipeline's thread is pinned to a CPU on the GPU's socket and its port's
+mempool holds 10,000 mbufs (nb_maglev's defaults).
 
 This process never initialises the GPU: it writes the capture (host trace generator) and runs
 nb_maglev as child processes.  Prints one JSON line.
@@ -40,7 +41,7 @@ def write_c1_pcap(path, n=10000, seed=2024):
 
 
 def run(pcap, pipelines, total, batch=992, depth=4, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
-        server=-1, pool=None, profile=True, env=None, timeout=120):
+        server=-1, pool=None, profile=True, local_cpus=True, spread=True, env=None, timeout=120):
     args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
             "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
@@ -49,6 +50,10 @@ def run(pcap, pipelines, total, batch=992, depth=4, zero_copy=False, drop_on_ful
         args += ["--pool", str(pool)]
     if not profile:
         args += ["--profile", "0"]
+    if not local_cpus:
+        args += ["--local-cpus", "0"]
+    if not spread:
+        args += ["--spread-l3", "0"]
     r = subprocess.run(["timeout", "-k", "5", str(timeout)] + args, capture_output=True, text=True,
                        env=dict(os.environ, **(env or {})))
     if r.returncode != 0:
@@ -64,6 +69,8 @@ def main():
                     help="also zero-copy, depth 3, drop-on-full, 4-KiB pages, and a kernel launch per batch")
     ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
     ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
+    ap.add_argument("--ab-spread", action="store_true",
+                    help="only the thread placement A/B at 16 pipelines (spread over L3 caches or not), 3 rounds")
     ap.add_argument("--pool-sweep", action="store_true",
                     help="only the mempool size A/B (mbufs per pipeline's port) at 1, 4 and 16 pipelines")
     args = ap.parse_args()
@@ -84,12 +91,19 @@ def main():
                      ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
                      ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
                      ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
+        if args.ab_spread:
+            runs = [(f"p16_{'spread' if sp else 'packed'}_r{k}", dict(pipelines=16, server=32, spread=sp))
+                    for k in range(3) for sp in (True, False)]
+            runs += [(f"p4_{'spread' if sp else 'packed'}", dict(pipelines=4, server=32, spread=sp)) for sp in (True, False)]
         if args.pool_sweep:
             runs = [(f"p{p}_pool{m}{'' if prof else '_noprof'}", dict(pipelines=p, server=32, pool=m, profile=prof))
                     for p in (1, 4, 16) for m in (10000, 65536) for prof in (True, False)]
         if args.extra:
             top = max(int(p) for p in args.pipelines.split(","))
-            runs += [(f"p{top}_server_zero_copy", dict(pipelines=top, server=32, zero_copy=True)),
+            runs += [(f"p{top}_any_cpus", dict(pipelines=top, server=32, local_cpus=False)),
+                     (f"p{top}_packed_cpus", dict(pipelines=top, server=32, spread=False)),
+                     (f"p{top}_pool65536", dict(pipelines=top, server=32, pool=65536)),
+                     (f"p{top}_noprof", dict(pipelines=top, server=32, profile=False)),(f"p{top}_server_zero_copy", dict(pipelines=top, server=32, zero_copy=True)),
                      ("p1_server_zero_copy", dict(pipelines=1, server=32, zero_copy=True)),
                      (f"p{top}_server_depth3", dict(pipelines=top, server=32, depth=3)),
                      (f"p{top}_server_drop_on_full", dict(pipelines=top, server=32, drop_on_full=True)),
@@ -118,7 +132,8 @@ def main():
                          "aggregate_mpps": r["aggregate_mpps"], "producer_only_mpps": round(prod / 1e6, 1)})
     print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024, "depth": 4,
                       "server_blocks": 32, "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, "
-                                                      "LoopPort replay (2-KiB mbufs in huge pages)"}))
+                                                      "LoopPort replay (a pool of 10,000 2-KiB mbufs in huge pages, "
+                                                      "one per frame of the capture); threads on the GPU's socket"}))
 
 
 if __name__ == "__main__":
