@@ -251,6 +251,24 @@ def cpu_inventory():
     return cores, quota, model
 
 
+def spread_cpus(cpus):
+    """The CPUs dealt round-robin over their L3 caches (sysfs cache/index3), the order within one L3
+    kept: the drop-in path's thread placement (nb_maglev's spread_over_l3), two cores per 8-core CCD at
+    16 threads instead of every core of two CCDs."""
+    groups = {}
+    for c in cpus:
+        try:
+            key = open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read().strip()
+        except OSError:
+            key = "?"
+        groups.setdefault(key, []).append(c)
+    out, i = [], 0
+    while len(out) < len(cpus):
+        out += [g[i] for g in groups.values() if i < len(g)]
+        i += 1
+    return out
+
+
 def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
     """The reference's per-core producer loop restated in C (oracle/, kind "port"), timed on this
     host's cores: MAC swap, ipv4_extract_flow, FNV-1a, the FNV-keyed memo map (nf.rs:91,104),
@@ -278,10 +296,22 @@ def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
         return n * reps / s / 1e6, reps, s * threads
 
     single, r1, c1 = measure(BATCH, 1, True, 2.0)
-    allc, ra, ca = measure(n_all, cores, True, target_cpu_s)
+    packed, ra, ca = measure(n_all, cores, True, target_cpu_s)
     nocache, rn, cn = measure(n_all, cores, False, target_cpu_s / 2)
+    # the same threads placed as the drop-in path places its pipelines (dealt over the L3 caches):
+    # the baseline is the faster of the two placements
+    order = spread_cpus(sorted(os.sched_getaffinity(0)))[:cores]
+    arr = (C.c_int * len(order))(*order)
+    L.orc_set_cpu_order(arr, len(order))
+    try:
+        spread, rs, cs = measure(n_all, cores, True, target_cpu_s)
+    finally:
+        L.orc_set_cpu_order(None, 0)
+    allc, ra, ca = (spread, rs, cs) if spread > packed else (packed, ra, ca)
     return {"value": round(allc, 1), "unit": "Mpps", "cores": cores, "kind": "port",
             "single_core_mpps": round(single, 2), "no_cache_mpps": round(nocache, 1),
+            "packed_mpps": round(packed, 1), "spread_l3_mpps": round(spread, 1),
+            "placement": "spread over L3 caches" if spread > packed else "first allowed CPUs",
             "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "cpu_model": model,
             "sample": f"C port of the reference loop (FNV-keyed memo map nf.rs:91,104, 32-pkt bursts, per-group "
                       f"1024-slot rings) over the {len(host_bufs)} C2 batches ({n_all:,} 64-B UDP packets, 65 backends, "

@@ -268,9 +268,24 @@ static inline uint16_t lpm_lookup(const uint16_t *tbl24, const uint16_t *tbl_lon
 #define RING 1024
 #define BURST 32
 
+/* Thread placement of the baseline: thread t on CPU g_cpu_order[t % n] when a caller set an order
+ * (orc_set_cpu_order; bench.py passes the drop-in path's own placement), else on the t-th allowed CPU. */
+static int g_cpu_order[1024];
+static int g_cpu_order_n = 0;
+
+void orc_set_cpu_order(const int *cpus, int n) {
+    g_cpu_order_n = 0;
+    for (int i = 0; cpus && i < n && i < 1024; i++) g_cpu_order[g_cpu_order_n++] = cpus[i];
+}
+
 static void *shard_main(void *arg) {
     orc_shard_t *s = (orc_shard_t *)arg;
-    if (s->cpu >= 0) { /* pin to the cpu-th CPU of the allowed set (cgroup-safe) */
+    if (s->cpu >= 0 && g_cpu_order_n > 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(g_cpu_order[s->cpu % g_cpu_order_n], &set);
+        pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+    } else if (s->cpu >= 0) { /* pin to the cpu-th CPU of the allowed set (cgroup-safe) */
         cpu_set_t allowed, set;
         CPU_ZERO(&allowed);
         if (sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {

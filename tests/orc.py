@@ -44,6 +44,8 @@ def lib():
         L.orc_cpu_baseline_reps.restype = C.c_double
         L.orc_cpu_baseline_reps.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, C.c_uint64,
                                             C.c_uint32, C.c_int, C.c_int, C.c_uint32, _P]
+        L.orc_set_cpu_order.restype = None
+        L.orc_set_cpu_order.argtypes = [_P, C.c_int]
         L.orc_cpu_baseline_chain_reps.restype = C.c_double
         L.orc_cpu_baseline_chain_reps.argtypes = [_P, _P, C.c_uint64, _P, C.c_uint32, C.c_uint64, _P, _P, C.c_uint32,
                                                   _P, C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_uint32, _P]

@@ -162,3 +162,37 @@ def test_completion_slope_uses_the_middle_of_the_run():
     assert abs(bench.completion_slope(burst, batches) - 20e-6) < 1e-9
     assert bench.completion_slope(stamps[:50], batches) is None
     assert bench.completion_slope([(0.0, 0)], batches) is None
+
+
+def test_spread_cpus_deals_over_l3_caches(monkeypatch):
+    """spread_cpus (the drop-in threads' placement, also tried for the CPU baseline): CPUs dealt
+    round-robin over their L3 caches, the order within a cache kept, nothing lost or repeated."""
+    l3 = {c: f"{c // 8 * 8}-{c // 8 * 8 + 7}" for c in range(32)}
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path.startswith("/sys/devices/system/cpu/cpu") and path.endswith("shared_cpu_list"):
+            import io
+            return io.StringIO(l3[int(path.split("/cpu")[2].split("/")[0])])
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    got = bench.spread_cpus(list(range(16)))
+    assert got == [0, 8, 1, 9, 2, 10, 3, 11, 4, 12, 5, 13, 6, 14, 7, 15]
+    assert bench.spread_cpus(list(range(32)))[:4] == [0, 8, 16, 24]
+
+
+def test_cpu_baseline_reports_both_placements():
+    """cpu_baseline times the reference loop with the threads on the first allowed CPUs and dealt over
+    the L3 caches, and reports the faster as the baseline (a short sample over one 1M batch)."""
+    import numpy as np
+
+    import netbricks_amd as nb
+
+    buf, _, _ = nb.make_trace(bench.BATCH, 0, seed=5)
+    lut = nb.build_lut([f"backend-{i}" for i in range(bench.N_BACKENDS)], bench.TABLE)
+    r = bench.cpu_baseline([buf], lut, target_cpu_s=0.2)
+    assert r["packed_mpps"] > 0 and r["spread_l3_mpps"] > 0
+    assert r["value"] == round(max(r["packed_mpps"], r["spread_l3_mpps"]), 1) or \
+        abs(r["value"] - max(r["packed_mpps"], r["spread_l3_mpps"])) < 0.11
+    assert np.isfinite(r["single_core_mpps"])
