@@ -351,7 +351,7 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
  * (or, zero-copy, the offsets and frames) out of host memory and stores its results there, with no
  * DMA copy either way; larger batches are copied H2D / D2H around the kernels.
  */
-#define NBG_HOST_SLOTS 4
+#define NBG_HOST_SLOTS 8
 int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
                            uint32_t flags, uint16_t* backend_out, uint32_t* perm_out, uint32_t* counts_out,
                            uint64_t* ticket);

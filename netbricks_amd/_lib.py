@@ -31,7 +31,7 @@ NBG_DEFER_GROUP = 0x10
 NBG_LUT_TILED = 0x20
 NBG_STREAM_DESC = 0x40
 NBG_GROUP_LAG = 0x80
-NBG_HOST_SLOTS = 4
+NBG_HOST_SLOTS = 8
 NBG_MAX_MULTI = 16
 NBG_RING_SLOTS = 64
 NBG_RING_MAX_QUEUES = 16
@@ -124,6 +124,7 @@ DEBUG_SIGNATURES = {
     "nbg_debug_group_lds": (C.c_uint64, [C.c_uint32, C.c_int]),
     "nbg_debug_lds_beside_ring": (C.c_uint64, []),
     "nbg_debug_hold_cus": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, _P]),
+    "nbg_debug_host_win": (C.c_int, [_P, C.c_uint64]),
 }
 
 

@@ -142,6 +142,7 @@ struct nbg_maglev {
     uint32_t* h_flag = nullptr;
     uint32_t* dh_flag = nullptr;
     bool direct = false;        // the slot's batch took the direct path (completion = h_flag)
+    uint32_t win = 0;           // the stride its windows were staged at (32: frame bytes 8..39; 0: zero-copy)
     hipStream_t watch = nullptr;  // the direct batch's kernel runs on it (its end without the flag is a failure)
     bool on_ring = false;         // posted to the host-batch server: ra / rg relaunch it if the server ended first
     ClassifyArgs ra{};
@@ -705,7 +706,8 @@ int classify_lag(nbg_maglev* h, ClassifyArgs& a, bool fuse, uint32_t n_parts, ui
 int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const uint16_t* d_len, uint32_t stride,
                     uint16_t fixed_len, uint64_t n_pkts, uint32_t flags, uint16_t* d_backend, uint32_t* d_perm,
                     uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
-                    uint16_t* d_gate, void* stream, uint32_t* small_done = nullptr, uint32_t small_done_val = 0) {
+                    uint16_t* d_gate, void* stream, uint32_t* small_done = nullptr, uint32_t small_done_val = 0,
+                    bool win32 = false) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
   if (h->ring) return set_error(NBG_EBUSY, "classify: the handle's persistent ring is running (nbg_ring_stop first)");
   if (h->pending && !h->pending_lag)
@@ -843,6 +845,8 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const bool fuse = lag && h->pending_lag && h->pending_lg.n_parts <= static_cast<uint32_t>(h->cus);
   if (h->pending_lag && !fuse && (rc = flush_lag(h, static_cast<hipStream_t>(stream)))) return rc;
   if (small_done && !small) return set_error(NBG_EINVAL, "classify: a completion word needs the small kernel");
+  if (win32 && (!small || a.swap)) return set_error(NBG_EINVAL, "classify: 32-B windows need the small kernel, no swap");
+  a.win32 = win32 ? 1u : 0u;
   if (small) {
     GroupArgs g{};
     g.perm = d_perm;
@@ -2036,6 +2040,14 @@ int nbg_ring_group_burst(nbg_ring* r, uint64_t first_ticket, uint32_t n_batches,
   return ring_group_burst_locked(r, first_ticket, n_batches, d_perm, d_counts, static_cast<hipStream_t>(stream));
 }
 
+// Diagnostics (not in include/nbgpu.h): the window stride host batch `ticket` was staged at (32, 48,
+// 64 or 80; 0 for zero-copy), while its slot still holds it; -1 otherwise.
+int nbg_debug_host_win(nbg_maglev* h, uint64_t ticket) {
+  if (!h || ticket == 0 || ticket >= h->next_ticket) return -1;
+  const auto& t = h->slots[ticket % NBG_HOST_SLOTS];
+  return t.ticket == ticket ? static_cast<int>(t.win) : -1;
+}
+
 // Diagnostics (not in include/nbgpu.h): the host control line's 16 words.
 int nbg_debug_ring_ctl(nbg_ring* r, uint32_t* out) {
   if (!r || !out) return NBG_EINVAL;
@@ -2237,20 +2249,26 @@ namespace {
 // swap: apply MacHeader::swap_addresses (headers/mac.rs:140-145) to every frame of >= 14 B while its
 // line is in cache (the staged copy keeps the bytes as received; the flow hash reads none of the 12
 // swapped bytes), so no second pass over the mbufs writes the swap back after the GPU.
-uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint8_t* h_win,
-                     uint16_t* h_len, bool swap) {
+//
+// base = 8, win = 32 (a direct batch, whose small kernel takes 32-B windows): bytes 8..39 of every frame,
+// which hold every byte an IHL-5 parse reads once the MACs are swapped here; 32 comes back when every
+// frame longer than 40 B has IHL <= 5, else the stride a whole-window staging needs (the caller stages
+// the batch again from byte 0).  A third fewer bytes cross PCIe than with 48-B windows.
+uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint32_t base,
+                     uint8_t* h_win, uint16_t* h_len, bool swap) {
   constexpr uint64_t kAhead = 16;  // 32 and 64 measured no faster (profiles/r06_dropin_tune.json)
-  std::atomic<uint32_t> need{48};
+  const uint32_t top = base + win;  // frames longer than this are sized by their IP header
+  std::atomic<uint32_t> need{top};
   parallel_for(n, [&](uint64_t b, uint64_t e) {
-    uint32_t m = 48;
+    uint32_t m = top;
     for (uint64_t i = b; i < e; ++i) {
       if (i + kAhead < e) __builtin_prefetch(pkt_ptrs[i + kAhead], 1, 0);  // read, then (swap) written
-      const uint32_t l = lens[i], c = std::min<uint32_t>(l, win);
+      const uint32_t l = lens[i], c = l > base ? std::min<uint32_t>(l, top) - base : 0u;
       uint8_t* w = h_win + i * win;
       uint8_t* f = pkt_ptrs[i];
-      std::memcpy(w, f, c);
+      std::memcpy(w, f + base, c);
       h_len[i] = static_cast<uint16_t>(l);
-      if (l > 48) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (w[14] & 0xfu) * 4 + 4));
+      if (l > top) m = std::max<uint32_t>(m, 14 + std::max<uint32_t>(20, (w[14 - base] & 0xfu) * 4 + 4));
       if (swap && l >= 14) {
         uint8_t dst[6];
         std::memcpy(dst, f, 6);
@@ -2263,6 +2281,7 @@ uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
     }
   });
   const uint32_t m = need.load();
+  if (base == 8 && win == 32 && m <= 40) return 32;
   return m <= 48 ? 48 : (m <= 64 ? 64 : 80);
 }
 
@@ -2364,7 +2383,7 @@ int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
 // path): packets at pkts (+ off[i], or i * stride), lengths len[], outputs in pinned host memory.
 void small_args(const nbg_maglev* h, uint8_t* pkts, const uint32_t* off, const uint16_t* len, uint32_t stride,
                 uint64_t n, uint32_t flags, uint16_t* backend, uint32_t* perm, uint32_t* counts, ClassifyArgs& a,
-                GroupArgs& g) {
+                GroupArgs& g, bool win32 = false) {
   a = ClassifyArgs{};
   a.pkts = pkts;
   a.off = off;
@@ -2379,6 +2398,7 @@ void small_args(const nbg_maglev* h, uint8_t* pkts, const uint32_t* off, const u
   a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
   a.win_owned = (!off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
   a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
+  a.win32 = win32 ? 1u : 0u;
   a.backend = backend;
   g = GroupArgs{};
   g.perm = perm;
@@ -2437,6 +2457,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   if ((rc = slot_reserve(h, t, n))) return rc;
   t.direct = false;
   t.on_ring = false;
+  t.win = 0;
   const bool swap = flags & NBG_SWAP_MACS;
   t.n = n;
   t.backend_out = backend_out;
@@ -2477,7 +2498,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
         GroupArgs ga;
         small_args(h, reg.dev, reinterpret_cast<const uint32_t*>(t.dh_win), t.dh_len, 0, n, zflags, t.dh_backend,
                    perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, a, ga);
-        t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb), t.dh_flag,
+        t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb, false), t.dh_flag,
                                                static_cast<uint32_t>(tk));
         if (t.on_ring) {
           t.watch = h->hring->stream;
@@ -2510,10 +2531,23 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
       return NBG_OK;
     }
   }
-  // gather at 48-B windows, swapping the MACs in the mbufs on the way; a batch with longer IP headers
-  // is staged again (without swapping) at the stride it needs
-  uint32_t win = host_gather(pkt_ptrs, lens, n, 48, t.h_win, t.h_len, swap);
-  if (win > 48) host_gather(pkt_ptrs, lens, n, win, t.h_win, t.h_len, false);
+  // gather, swapping the MACs in the mbufs on the way: a direct batch at 32-B windows (frame bytes
+  // 8..39), a copied one at 48-B windows; a batch with longer IP headers is staged again (without
+  // swapping) from byte 0 at the stride it needs
+  const uint32_t sflags =
+      (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG | NBG_SWAP_MACS)) | NBG_OWNED_WINDOWS;
+  const bool direct = use_small(n, h->nb + 1, sflags, t.dh_win);
+  // NBG_HOST_WIN48=1 (measurement): direct batches at 48-B windows, as before the 32-B staging
+  static const bool win48 = [] {
+    const char* e = std::getenv("NBG_HOST_WIN48");
+    return e && std::atoi(e) == 1;
+  }();
+  uint32_t win = direct && !win48 ? host_gather(pkt_ptrs, lens, n, 32, 8, t.h_win, t.h_len, swap) : 0u;
+  if (win != 32) {
+    win = host_gather(pkt_ptrs, lens, n, 48, 0, t.h_win, t.h_len, swap && !(direct && !win48));
+    if (win > 48) host_gather(pkt_ptrs, lens, n, win, 0, t.h_win, t.h_len, false);
+  }
+  t.win = win;
   // copies and kernels in submit order on the handle's one host stream (the kernels share the
   // handle's grouping scratch).  No cross-stream event: with the copies on a stream of their own
   // and an event wait on the compute stream, kernels were seen reading windows whose H2D copy had
@@ -2521,9 +2555,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
   // the next batch while this one runs.
   hipStream_t hs = h->host_compute;
   const bool group = perm_out || counts_out;
-  const uint32_t sflags =
-      (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG | NBG_SWAP_MACS)) | NBG_OWNED_WINDOWS;
-  if (use_small(n, h->nb + 1, sflags, t.dh_win)) {
+  if (direct) {
     // direct: a batch of at most 2,048 packets (NetBricks' own bursts are 32) is classified and
     // grouped by one small-kernel launch that reads the staged windows out of pinned memory and
     // stores backend / perm / counts there.  The copies' fixed costs (a few us each on the DMA
@@ -2531,8 +2563,8 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     ClassifyArgs a;
     GroupArgs ga;
     small_args(h, t.dh_win, nullptr, t.dh_len, win, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
-               group ? t.dh_counts : nullptr, a, ga);
-    t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb), t.dh_flag,
+               group ? t.dh_counts : nullptr, a, ga, win == 32);
+    t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb, win == 32), t.dh_flag,
                                            static_cast<uint32_t>(tk));
     if (t.on_ring) {
       t.watch = h->hring->stream;
@@ -2541,7 +2573,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     } else {
       rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend,
                            perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr, nullptr, 0, nullptr,
-                           hs, t.dh_flag, static_cast<uint32_t>(tk));
+                           hs, t.dh_flag, static_cast<uint32_t>(tk), win == 32);
       if (rc) return rc;
       t.watch = hs;
     }

@@ -10,14 +10,15 @@
 // index of every transmitted frame (one per line) for order checks.  --zero-copy 1 registers the
 // port's mempool (nbg_host_register), so the GPU reads and rewrites the frames in place over PCIe.
 // The group queues have the reference's 1024 slots; --batch is capped at 992 (whole bursts, at most
-// 1023).  --depth batches are on the GPU at once (1..NBG_HOST_SLOTS = 4, nbg_maglev_host_submit's slots).  By default
+// 1023).  --depth batches are on the GPU at once (1..NBG_HOST_SLOTS = 8, nbg_maglev_host_submit's slots).  By default
 // the producer pulls a batch only while every queue could take a whole one, and a classified batch's
 // enqueue waits at a full queue (backpressure: nothing is dropped); --drop-on-full 1 pulls whenever
 // the pipeline has room and drops on a full queue, as the reference's producer does (group_by.rs:50).
 //
 // --loop TOTAL: each of P pipelines (--pipelines, default 1) runs on a thread of its own, pinned to
 // one of the process's CPUs, with its own replay port (LoopPort: the capture's frames in a pool of
-// --pool mbufs (default 8,192, rounded up to whole copies of the capture) with 2-KiB data rooms in
+// --pool mbufs (default: 8,192, or the batches in flight plus 2,048 if more; rounded up to whole copies
+// of the capture) with 2-KiB data rooms in
 // transparent huge pages, as DPDK's mempools are in hugepages; --hugepages 0 for 4-KiB pages; received
 // until TOTAL packets, freed by send — the reference's VirtualPort), its own
 // scheduler, its own Maglev handle and stream: the reference's one pipeline per RX queue and core
@@ -128,7 +129,9 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
       bool counted = false;
       try {
         pin_to(p, cpus);
-        auto port = std::make_shared<nb::LoopPort>(recs, total, pool_mbufs, 2048, huge);
+        const size_t mbufs = pool_mbufs ? pool_mbufs
+                                        : std::max<size_t>(8192, size_t{depth} * nb::cap_batch(batch) + 2048);
+        auto port = std::make_shared<nb::LoopPort>(recs, total, mbufs, 2048, huge);
         auto pool = port->mempool();
         uint8_t* dev = nullptr;
         if (zero_copy) nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
@@ -228,12 +231,12 @@ int main(int argc, char** argv) {
   uint64_t table = 65537, loop = 0;
   uint32_t batch = nb::kMaxGpuBatch, depth = nb::kMaxDepth;
   int pipelines = 1, hw_queues = 0, ring_blocks = -1;
-  // mbufs per replay port: at least 8,192 (up to 4 x 992 in flight plus the group queues), rounded up
-  // to whole copies of the capture by LoopPort.  The reference's default pool is 2,047 mbufs
+  // mbufs per replay port (0: at least 8,192 and the batches in flight plus two queues' worth,
+  // depth x batch + 2,048), rounded up to whole copies of the capture by LoopPort.  The reference's default pool is 2,047 mbufs
   // (DEFAULT_POOL_SIZE, config/config_reader.rs:8) for a producer that holds no batch in flight; a
   // pool far larger than needed only spreads the mbufs' lines over more cache (64k mbufs: 297 against
   // 370 Mpps at 16 pipelines, profiles/r06_dropin_pool.json)
-  size_t pool_mbufs = 8192;
+  size_t pool_mbufs = 0;
   bool profiled = true, local = true, spread = true;
   bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {

@@ -9,7 +9,7 @@ framework/src/operators/group_by.rs:43-55).
 scheduler/context.rs:55-69,241-255), each replaying a C1-style capture (10k 64-B UDP frames, 65
 backends / 65537) through a LoopPort (the reference's VirtualPort: recv hands out mbufs, send frees
 them).  Producer and consumer (merge + send) tasks share each pipeline's thread, as in the reference.
-Every pipeline's batches go to the device's host-batch server (nbg_host_ring_*, 32 blocks), up to 4
+Every pipeline's batches go to the device's host-batch server (nbg_host_ring_*, 64 blocks), up to 8
 in flight per pipeline; each pipeline's thread is pinned to a CPU on the GPU's socket and its port's
 mempool holds 10,000 mbufs (nb_maglev's defaults).
 
@@ -27,6 +27,8 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 NB = os.path.join(ROOT, "netbricks_amd", "host", "nb_maglev")
+SERVER_BLOCKS = 64  # the host-batch server's blocks (16 pipelines: 32 -> 468/387, 48 -> 492/494, 64 -> 543/491,
+                    # 96 -> 417/431 Mpps in two rounds, profiles/r06_dropin_server_sweep.json)
 
 
 def write_c1_pcap(path, n=10000, seed=2024):
@@ -40,12 +42,14 @@ def write_c1_pcap(path, n=10000, seed=2024):
             f.write(buf[o:o + l].tobytes())
 
 
-def run(pcap, pipelines, total, batch=992, depth=4, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
+def run(pcap, pipelines, total, batch=992, depth=None, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
         server=-1, pool=None, profile=True, local_cpus=True, spread=True, env=None, timeout=120):
-    args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--depth", str(depth), "--loop", str(total),
+    args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
             "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
             "--hugepages", "1" if huge else "0", "--host-ring", str(server)]
+    if depth:
+        args += ["--depth", str(depth)]
     if pool:
         args += ["--pool", str(pool)]
     if not profile:
@@ -69,6 +73,10 @@ def main():
                     help="also zero-copy, depth 3, drop-on-full, 4-KiB pages, and a kernel launch per batch")
     ap.add_argument("--write-pcap", help="only write the C1-style capture to this path")
     ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
+    ap.add_argument("--depth-sweep", action="store_true",
+                    help="only batches in flight per pipeline (4, 8) x server blocks (48, 64) at 16 pipelines")
+    ap.add_argument("--server-sweep", action="store_true",
+                    help="only the host-batch server's block count at 16 pipelines (and 4), 2 rounds")
     ap.add_argument("--ab-spread", action="store_true",
                     help="only the thread placement A/B at 16 pipelines (spread over L3 caches or not), 3 rounds")
     ap.add_argument("--pool-sweep", action="store_true",
@@ -83,7 +91,7 @@ def main():
         write_c1_pcap(pcap)
         # the rows: every pipeline's batches through the device's host-batch server (32 blocks), 4 in
         # flight per pipeline, staged 48-B windows; then (extra) each choice against its alternative
-        runs = [(f"p{p}", dict(pipelines=int(p), server=32)) for p in args.pipelines.split(",")]
+        runs = [(f"p{p}", dict(pipelines=int(p), server=SERVER_BLOCKS)) for p in args.pipelines.split(",")]
         if args.tune:
             runs = [(f"p16_server_ahead{a}", dict(pipelines=16, server=32, env={"NBG_GATHER_AHEAD": str(a)}))
                     for a in (16, 32, 64)]
@@ -91,6 +99,13 @@ def main():
                      ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
                      ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
                      ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
+        if args.depth_sweep:
+            runs = [(f"p16_depth{d}_server{b}_r{k}", dict(pipelines=16, server=b, depth=d))
+                    for k in range(2) for b in (48, 64) for d in (4, 8)]
+            runs += [(f"p1_depth{d}", dict(pipelines=1, server=64, depth=d)) for d in (4, 8)]
+        if args.server_sweep:
+            runs = [(f"p16_server{b}_r{k}", dict(pipelines=16, server=b)) for k in range(2) for b in (32, 48, 64, 96)]
+            runs += [(f"p4_server{b}", dict(pipelines=4, server=b)) for b in (16, 32)]
         if args.ab_spread:
             runs = [(f"p16_{'spread' if sp else 'packed'}_r{k}", dict(pipelines=16, server=32, spread=sp))
                     for k in range(3) for sp in (True, False)]
@@ -100,14 +115,20 @@ def main():
                     for p in (1, 4, 16) for m in (10000, 65536) for prof in (True, False)]
         if args.extra:
             top = max(int(p) for p in args.pipelines.split(","))
-            runs += [(f"p{top}_any_cpus", dict(pipelines=top, server=32, local_cpus=False)),
-                     (f"p{top}_packed_cpus", dict(pipelines=top, server=32, spread=False)),
-                     (f"p{top}_pool65536", dict(pipelines=top, server=32, pool=65536)),
-                     (f"p{top}_noprof", dict(pipelines=top, server=32, profile=False)),(f"p{top}_server_zero_copy", dict(pipelines=top, server=32, zero_copy=True)),
-                     ("p1_server_zero_copy", dict(pipelines=1, server=32, zero_copy=True)),
-                     (f"p{top}_server_depth3", dict(pipelines=top, server=32, depth=3)),
-                     (f"p{top}_server_drop_on_full", dict(pipelines=top, server=32, drop_on_full=True)),
-                     (f"p{top}_server_4k_pages", dict(pipelines=top, server=32, huge=False)),
+            S = SERVER_BLOCKS
+            runs += [(f"p{top}_any_cpus", dict(pipelines=top, server=S, local_cpus=False)),
+                     (f"p{top}_packed_cpus", dict(pipelines=top, server=S, spread=False)),
+                     (f"p{top}_pool65536", dict(pipelines=top, server=S, pool=65536)),
+                     (f"p{top}_noprof", dict(pipelines=top, server=S, profile=False)),
+                     (f"p{top}_server32", dict(pipelines=top, server=32)),
+                     (f"p{top}_depth4", dict(pipelines=top, server=S, depth=4)),
+                     ("p1_depth4", dict(pipelines=1, server=S, depth=4)),
+                     (f"p{top}_win48", dict(pipelines=top, server=S, env={"NBG_HOST_WIN48": "1"})),
+                     ("p1_win48", dict(pipelines=1, server=S, env={"NBG_HOST_WIN48": "1"})),
+                     (f"p{top}_server_zero_copy", dict(pipelines=top, server=S, zero_copy=True)),
+                     ("p1_server_zero_copy", dict(pipelines=1, server=S, zero_copy=True)),
+                     (f"p{top}_server_drop_on_full", dict(pipelines=top, server=S, drop_on_full=True)),
+                     (f"p{top}_server_4k_pages", dict(pipelines=top, server=S, huge=False)),
                      (f"p{top}_launch", dict(pipelines=top)),
                      ("p4_launch", dict(pipelines=4)),
                      ("p1_launch", dict(pipelines=1)),
@@ -130,8 +151,8 @@ def main():
             prod = sum(r["rx_per_pipeline"] / s for s in r["producer_seconds"] if s > 0)
             rows.append({"pipelines": r["pipelines"], "per_pipeline_mpps": round(sum(per) / len(per), 2),
                          "aggregate_mpps": r["aggregate_mpps"], "producer_only_mpps": round(prod / 1e6, 1)})
-    print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024, "depth": 4,
-                      "server_blocks": 32, "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, "
+    print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024, "depth": 8,
+                      "server_blocks": SERVER_BLOCKS, "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, "
                                                       "LoopPort replay (a pool of 10,000 2-KiB mbufs in huge pages, "
                                                       "one per frame of the capture); threads on the GPU's socket"}))
 
