@@ -2675,7 +2675,7 @@ int nbg_host_ring_start(int device, uint32_t blocks, uint32_t idle_ms, nbg_host_
   DeviceGuard g(device);
   int cus = 0;
   NBG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  if (blocks == 0) blocks = 32;
+  if (blocks == 0) blocks = 64;  // 16 pipelines: 32 -> 626, 64 -> 673 Mpps (profiles/r06_dropin_win32.json)
   if (blocks > static_cast<uint32_t>(cus) / 2)
     return set_error(NBG_EINVAL, "host_ring_start: %u blocks (one per CU, at most half of the %d CUs)", blocks, cus);
   // one resident server per device, and not beside a persistent RX ring (whose blocks need every CU)
