@@ -350,8 +350,8 @@ int nbg_maglev_classify_host(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint
  * A batch of at most 2,048 packets takes the direct path: one kernel launch reads the staged windows
  * (or, zero-copy, the offsets and frames) out of host memory and stores its results there, with no
  * DMA copy either way; larger batches are copied H2D / D2H around the kernels.  A direct batch whose
- * frames longer than 38 B all have IHL <= 5 is staged as 24-B header windows (frame bytes 14..37:
- * everything the parse reads once the MACs are swapped), half the bytes of 48-B windows over PCIe.
+ * frames longer than 40 B all have IHL <= 5 is staged as 32-B windows (frame bytes 8..39: everything
+ * the parse reads once the MACs are swapped), a third fewer bytes over PCIe.
  */
 #define NBG_HOST_SLOTS 8
 int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,

@@ -2141,24 +2141,26 @@ __global__ __launch_bounds__(kLookupNT) void tile_lookup_kernel(TileArgs a) {
 constexpr uint32_t kSmallNT = 1024, kSmallW = kSmallNT / 64;
 constexpr uint32_t kSmallMax = 4 * kSmallNT;
 
-// HDR (the host path's header staging, a.hdr24): window p (24 B at a.pkts + 24p) holds frame bytes
-// 14..37 — the IP header's first 20 B and the ports, everything the parse reads for IHL <= 5 once the
-// host has swapped the MACs — so c[0] is frame bytes 14..29 and c[1].xy bytes 30..37, and the frame
-// starts 14 B before its window (the host stages a batch with a longer IP header in whole 48/64/80-B
-// windows instead).
-template <int LUTM, bool F4, bool HDR = false>
+// W32 (the host path's 32-B staging, a.win32): window p holds frame bytes 8..39 (the host swapped the
+// MACs and staged no bytes below 8), so c[0] is frame bytes 8..23 and c[1] bytes 24..39, and the frame
+// starts 8 B before its window; every byte the parse reads for IHL <= 5 lies in it (the host stages a
+// batch with a longer IP header in whole 48/64/80-B windows instead).
+template <int LUTM, bool F4, bool W32 = false>
 __device__ __forceinline__ uint32_t small_classify(const ClassifyArgs& a, uint32_t p, uint32_t off, uint32_t len,
                                                    const uint4* c) {
-  if constexpr (HDR) {
+  if constexpr (W32) {
     uint8_t* w = a.pkts + off;
-    if (len >= 38u && (c[0].x & 0xfu) == 5u) {
-      // window bytes: IHL 0, protocol 9, src 12..15, dst 16..19, ports 20..23
+    if ((reinterpret_cast<uintptr_t>(w) & 15u) == 0 && len >= 40u && ((c[0].y >> 16) & 0xfu) == 5u) {
+      // frame bytes: IHL 14, protocol 23, src 26..29, dst 30..33, ports 34..37
+      const uint32_t src = (c[1].x >> 16) | (c[1].y << 16);
+      const uint32_t dst = (c[1].y >> 16) | (c[1].z << 16);
+      const uint32_t ports = (c[1].z >> 16) | (c[1].w << 16);
       uint32_t lo, hi;
-      fnv_flow(lo, hi, c[0].w, c[1].x, c[1].y, (c[0].z >> 8) & 0xffu);
+      fnv_flow(lo, hi, src, dst, ports, c[0].w >> 24);
       return lookup<LUTM, F4>(a, nullptr, lo, hi);
     }
-    uint32_t gate;  // reads frame bytes 14 .. min(len, 38) - 1 only (no swap on this path)
-    return classify_slow<LUTM, F4, false>(a, nullptr, w - 14, len, p, gate);
+    uint32_t gate;  // reads frame bytes 14 .. min(len, 40) - 1 only (no swap on this path)
+    return classify_slow<LUTM, F4, false>(a, nullptr, w - 8, len, p, gate);
   }
   uint8_t* pk = a.pkts + off;
   const bool vec = (reinterpret_cast<uintptr_t>(pk) & 15u) == 0 && len >= 48u;
@@ -2187,7 +2189,7 @@ __device__ __forceinline__ uint32_t small_classify(const ClassifyArgs& a, uint32
   return classify_slow<LUTM, F4, false>(a, nullptr, pk, len, p, gate);
 }
 
-template <int LUTM, bool F4, int BITS, bool HDR = false>
+template <int LUTM, bool F4, int BITS, bool W32 = false>
 __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArgs& g) {
   extern __shared__ __align__(16) uint32_t sm[];
   const uint32_t nbins = a.nb + 1, nbp = (nbins + 3) & ~3u;
@@ -2216,14 +2218,18 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
   // packet start are readable whatever its length, so the window loads do not wait for len[] (over
   // PCIe, for the host path's direct batches, one round trip less per batch)
   const bool owned = a.win_owned != 0;
+  constexpr uint32_t kCh = W32 ? 2u : 3u;  // 16-B chunks per window
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
-    if constexpr (HDR) {
-      // the round's 64 header windows are 1,536 contiguous bytes (96 chunks of 16 B): lane l loads
-      // chunks l and 64 + l (clamped; the staging holds whole rounds)
-      const uint8_t* base = a.pkts + static_cast<size_t>(wave * 256u + r * 64u) * 24u;
-      v[r][0] = *reinterpret_cast<const uint4*>(base + 16u * lane);
-      v[r][1] = *reinterpret_cast<const uint4*>(base + 16u * min(64u + lane, 95u));
+    if constexpr (W32) {
+      // 32-B windows: lane pair (2i, 2i + 1) reads window i of the round's first 32, then of the last
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t q = 64u * k + lane, pi = q >> 1, part = q & 1u;
+        const uint8_t* w = a.pkts + __shfl(off[r], static_cast<int>(pi));
+        const bool vec = (reinterpret_cast<uintptr_t>(w) & 15u) == 0;
+        v[r][k] = *reinterpret_cast<const uint4*>((vec ? w : a.pkts) + 16u * part);
+      }
       continue;
     }
 #pragma unroll
@@ -2244,30 +2250,19 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
   uint4* tp = reinterpret_cast<uint4*>(bin16 + kSmallMax) + wave * 192u;  // [192] chunks of one round
 #pragma unroll
   for (uint32_t r = 0; r < 4; ++r) {
+#pragma unroll
+    for (uint32_t k = 0; k < kCh; ++k) tp[64u * k + lane] = v[r][k];
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations run in issue order
     uint4 c[3];
-    if constexpr (HDR) {
-      tp[lane] = v[r][0];
-      tp[min(64u + lane, 95u)] = v[r][1];
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations run in issue order
-      const uint2* t8 = reinterpret_cast<const uint2*>(tp) + 3u * lane;  // this lane's 24 B
-      const uint2 u0 = t8[0], u1 = t8[1], u2 = t8[2];
-      c[0] = make_uint4(u0.x, u0.y, u1.x, u1.y);
-      c[1] = make_uint4(u2.x, u2.y, 0u, 0u);
-    } else {
 #pragma unroll
-      for (uint32_t k = 0; k < 3; ++k) tp[64u * k + lane] = v[r][k];
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_wave_barrier();  // one wave: its LDS operations run in issue order
-#pragma unroll
-      for (uint32_t k = 0; k < 3; ++k) c[k] = tp[3u * lane + k];
-    }
+    for (uint32_t k = 0; k < kCh; ++k) c[k] = tp[kCh * lane + k];
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();  // the next round's writes after these reads
     const uint32_t p = wave * 256u + r * 64u + lane;
     bin[r] = 0xffffffffu;
     if (r < rounds && p < a.n_pkts) {
-      bin[r] = small_classify<LUTM, F4, HDR>(a, p, off[r], len[r], c);
+      bin[r] = small_classify<LUTM, F4, W32>(a, p, off[r], len[r], c);
       a.backend[p] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
     }
   }
@@ -2329,9 +2324,9 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
 // to done_val once every output of the batch is visible to the host: each thread's stores are
 // released at system scope, then, behind the block barrier, one vector store of the word.  The host
 // polls it with plain loads instead of querying an event through the runtime.
-template <int LUTM, bool F4, int BITS, bool HDR>
+template <int LUTM, bool F4, int BITS, bool W32>
 __global__ __launch_bounds__(kSmallNT) void small_kernel(ClassifyArgs a, GroupArgs g, uint32_t* done, uint32_t done_val) {
-  small_body<LUTM, F4, BITS, HDR>(a, g);
+  small_body<LUTM, F4, BITS, W32>(a, g);
   if (done) {
     __threadfence_system();
     __syncthreads();
@@ -3493,7 +3488,7 @@ int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void*
       small_kernel<kGlobalU8, true, 7, true>,    small_kernel<kGlobalU16, true, 7, true>,
       small_kernel<kGlobalU8, false, 10, true>,  small_kernel<kGlobalU16, false, 10, true>,
       small_kernel<kGlobalU8, true, 10, true>,   small_kernel<kGlobalU16, true, 10, true>};
-  const Fn fn = kFns[small_variant(wide_lut, a.m, a.nb, a.hdr24 != 0)];
+  const Fn fn = kFns[small_variant(wide_lut, a.m, a.nb, a.win32 != 0)];
   const uint32_t waves = (a.n_pkts + 255u) / 256u;  // 1..16: a wave per 256 packets
   const size_t lds = small_lds(a.nb, waves);
   if (lds > 64 * 1024 &&
@@ -3509,8 +3504,8 @@ int launch_small(const ClassifyArgs& a, const GroupArgs& g, bool wide_lut, void*
 uint32_t small_max() { return kSmallMax; }
 
 // host_ring_kernel's dispatch over the small kernel's instantiations (as launch_small picks them)
-uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb, bool hdr24) {
-  return (wide_lut ? 1u : 0u) | (m == 65537u ? 2u : 0u) | (nb + 1 > 128 ? 4u : 0u) | (hdr24 ? 8u : 0u);
+uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb, bool win32) {
+  return (wide_lut ? 1u : 0u) | (m == 65537u ? 2u : 0u) | (nb + 1 > 128 ? 4u : 0u) | (win32 ? 8u : 0u);
 }
 
 int launch_host_ring(const HostRingArgs& r, uint32_t blocks, void* stream) {

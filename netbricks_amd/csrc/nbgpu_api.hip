@@ -142,7 +142,7 @@ struct nbg_maglev {
     uint32_t* h_flag = nullptr;
     uint32_t* dh_flag = nullptr;
     bool direct = false;        // the slot's batch took the direct path (completion = h_flag)
-    uint32_t win = 0;           // the stride its windows were staged at (24: frame bytes 14..37; 0: zero-copy)
+    uint32_t win = 0;           // the stride its windows were staged at (32: frame bytes 8..39; 0: zero-copy)
     hipStream_t watch = nullptr;  // the direct batch's kernel runs on it (its end without the flag is a failure)
     bool on_ring = false;         // posted to the host-batch server: ra / rg relaunch it if the server ended first
     ClassifyArgs ra{};
@@ -707,7 +707,7 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
                     uint16_t fixed_len, uint64_t n_pkts, uint32_t flags, uint16_t* d_backend, uint32_t* d_perm,
                     uint32_t* d_counts, uint8_t* d_mac_out, const nbg_lpm* lpm, uint32_t lpm_groups,
                     uint16_t* d_gate, void* stream, uint32_t* small_done = nullptr, uint32_t small_done_val = 0,
-                    bool hdr24 = false) {
+                    bool win32 = false) {
   if (!h) return set_error(NBG_EINVAL, "classify: null handle");
   if (h->ring) return set_error(NBG_EBUSY, "classify: the handle's persistent ring is running (nbg_ring_stop first)");
   if (h->pending && !h->pending_lag)
@@ -845,8 +845,8 @@ int classify_common(nbg_maglev* h, uint8_t* d_pkts, const uint32_t* d_off, const
   const bool fuse = lag && h->pending_lag && h->pending_lg.n_parts <= static_cast<uint32_t>(h->cus);
   if (h->pending_lag && !fuse && (rc = flush_lag(h, static_cast<hipStream_t>(stream)))) return rc;
   if (small_done && !small) return set_error(NBG_EINVAL, "classify: a completion word needs the small kernel");
-  if (hdr24 && (!small || a.swap)) return set_error(NBG_EINVAL, "classify: header windows need the small kernel, no swap");
-  a.hdr24 = hdr24 ? 1u : 0u;
+  if (win32 && (!small || a.swap)) return set_error(NBG_EINVAL, "classify: 32-B windows need the small kernel, no swap");
+  a.win32 = win32 ? 1u : 0u;
   if (small) {
     GroupArgs g{};
     g.perm = d_perm;
@@ -2040,7 +2040,7 @@ int nbg_ring_group_burst(nbg_ring* r, uint64_t first_ticket, uint32_t n_batches,
   return ring_group_burst_locked(r, first_ticket, n_batches, d_perm, d_counts, static_cast<hipStream_t>(stream));
 }
 
-// Diagnostics (not in include/nbgpu.h): the window stride host batch `ticket` was staged at (24, 48,
+// Diagnostics (not in include/nbgpu.h): the window stride host batch `ticket` was staged at (32, 48,
 // 64 or 80; 0 for zero-copy), while its slot still holds it; -1 otherwise.
 int nbg_debug_host_win(nbg_maglev* h, uint64_t ticket) {
   if (!h || ticket == 0 || ticket >= h->next_ticket) return -1;
@@ -2250,11 +2250,10 @@ namespace {
 // line is in cache (the staged copy keeps the bytes as received; the flow hash reads none of the 12
 // swapped bytes), so no second pass over the mbufs writes the swap back after the GPU.
 //
-// base = 14, win = 24 (a direct batch, whose small kernel takes header windows): bytes 14..37 of every
-// frame, the IP header's first 20 B and the ports, every byte an IHL-5 parse reads once the MACs are
-// swapped here; 24 comes back when every frame longer than 38 B has IHL <= 5, else the stride a
-// whole-window staging needs (the caller stages the batch again from byte 0).  Half the bytes of a
-// 48-B window cross PCIe.
+// base = 8, win = 32 (a direct batch, whose small kernel takes 32-B windows): bytes 8..39 of every frame,
+// which hold every byte an IHL-5 parse reads once the MACs are swapped here; 32 comes back when every
+// frame longer than 40 B has IHL <= 5, else the stride a whole-window staging needs (the caller stages
+// the batch again from byte 0).  A third fewer bytes cross PCIe than with 48-B windows.
 uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n, uint32_t win, uint32_t base,
                      uint8_t* h_win, uint16_t* h_len, bool swap) {
   constexpr uint64_t kAhead = 16;  // 32 and 64 measured no faster (profiles/r06_dropin_tune.json)
@@ -2282,7 +2281,7 @@ uint32_t host_gather(uint8_t* const* pkt_ptrs, const uint16_t* lens, uint64_t n,
     }
   });
   const uint32_t m = need.load();
-  if (base == 14 && win == 24 && m <= 38) return 24;
+  if (base == 8 && win == 32 && m <= 40) return 32;
   return m <= 48 ? 48 : (m <= 64 ? 64 : 80);
 }
 
@@ -2384,7 +2383,7 @@ int slot_complete(nbg_maglev* h, nbg_maglev::HostSlot& t) {
 // path): packets at pkts (+ off[i], or i * stride), lengths len[], outputs in pinned host memory.
 void small_args(const nbg_maglev* h, uint8_t* pkts, const uint32_t* off, const uint16_t* len, uint32_t stride,
                 uint64_t n, uint32_t flags, uint16_t* backend, uint32_t* perm, uint32_t* counts, ClassifyArgs& a,
-                GroupArgs& g, bool hdr24 = false) {
+                GroupArgs& g, bool win32 = false) {
   a = ClassifyArgs{};
   a.pkts = pkts;
   a.off = off;
@@ -2399,7 +2398,7 @@ void small_args(const nbg_maglev* h, uint8_t* pkts, const uint32_t* off, const u
   a.swap = (flags & NBG_SWAP_MACS) ? 1u : 0u;
   a.win_owned = (!off && stride >= 64) || (flags & NBG_OWNED_WINDOWS) ? 1u : 0u;
   a.wb_full = (flags & NBG_WB_PARTIAL) ? 0u : 1u;
-  a.hdr24 = hdr24 ? 1u : 0u;
+  a.win32 = win32 ? 1u : 0u;
   a.backend = backend;
   g = GroupArgs{};
   g.perm = perm;
@@ -2532,19 +2531,19 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
       return NBG_OK;
     }
   }
-  // gather, swapping the MACs in the mbufs on the way: a direct batch at 24-B header windows (frame
-  // bytes 14..37), a copied one at 48-B windows; a batch with longer IP headers is staged again
-  // (without swapping) from byte 0 at the stride it needs
+  // gather, swapping the MACs in the mbufs on the way: a direct batch at 32-B windows (frame bytes
+  // 8..39), a copied one at 48-B windows; a batch with longer IP headers is staged again (without
+  // swapping) from byte 0 at the stride it needs
   const uint32_t sflags =
       (flags & ~(NBG_DEFER_GROUP | NBG_WB_PARTIAL | NBG_GROUP_LAG | NBG_SWAP_MACS)) | NBG_OWNED_WINDOWS;
   const bool direct = use_small(n, h->nb + 1, sflags, t.dh_win);
-  // NBG_HOST_WIN48=1 (measurement): direct batches at 48-B windows, as before the header staging
+  // NBG_HOST_WIN48=1 (measurement): direct batches at 48-B windows, as before the 32-B staging
   static const bool win48 = [] {
     const char* e = std::getenv("NBG_HOST_WIN48");
     return e && std::atoi(e) == 1;
   }();
-  uint32_t win = direct && !win48 ? host_gather(pkt_ptrs, lens, n, 24, 14, t.h_win, t.h_len, swap) : 0u;
-  if (win != 24) {
+  uint32_t win = direct && !win48 ? host_gather(pkt_ptrs, lens, n, 32, 8, t.h_win, t.h_len, swap) : 0u;
+  if (win != 32) {
     win = host_gather(pkt_ptrs, lens, n, 48, 0, t.h_win, t.h_len, swap && !(direct && !win48));
     if (win > 48) host_gather(pkt_ptrs, lens, n, win, 0, t.h_win, t.h_len, false);
   }
@@ -2564,8 +2563,8 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     ClassifyArgs a;
     GroupArgs ga;
     small_args(h, t.dh_win, nullptr, t.dh_len, win, n, sflags, t.dh_backend, perm_out ? t.dh_perm : nullptr,
-               group ? t.dh_counts : nullptr, a, ga, win == 24);
-    t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb, win == 24), t.dh_flag,
+               group ? t.dh_counts : nullptr, a, ga, win == 32);
+    t.on_ring = h->hring && host_ring_post(h->hring, a, ga, small_variant(h->wide, a.m, h->nb, win == 32), t.dh_flag,
                                            static_cast<uint32_t>(tk));
     if (t.on_ring) {
       t.watch = h->hring->stream;
@@ -2574,7 +2573,7 @@ int nbg_maglev_host_submit(nbg_maglev* h, uint8_t* const* pkt_ptrs, const uint16
     } else {
       rc = classify_common(h, t.dh_win, nullptr, t.dh_len, win, 0, n, sflags, t.dh_backend,
                            perm_out ? t.dh_perm : nullptr, group ? t.dh_counts : nullptr, nullptr, nullptr, 0, nullptr,
-                           hs, t.dh_flag, static_cast<uint32_t>(tk), win == 24);
+                           hs, t.dh_flag, static_cast<uint32_t>(tk), win == 32);
       if (rc) return rc;
       t.watch = hs;
     }

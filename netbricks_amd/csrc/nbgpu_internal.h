@@ -62,8 +62,8 @@ struct ClassifyArgs {
   uint16_t* gate;
   uint32_t* idx_out;        // NBG_LUT_TILED: per-packet LUT index (0xffffffff = would panic)
   uint8_t* sink;            // descriptor streaming kernel: 1 KiB scratch for stores of lanes with none
-  uint32_t hdr24;           // small kernel: window i (pkts + 24 i) holds frame bytes 14..37 (the host path's
-                            // header staging; no MAC swap on the GPU)
+  uint32_t win32;           // small kernel: window i (pkts + i * stride) holds frame bytes 8..39 (the host
+                            // path's 32-B staging; no MAC swap on the GPU)
 };
 
 // Several batches in one streaming-classify launch (nbg_maglev_classify_device_multi): what differs
@@ -269,7 +269,7 @@ struct HostRingArgs {
   uint64_t idle_ticks;      // 100 MHz wall clock
 };
 int launch_host_ring(const HostRingArgs& r, uint32_t blocks, void* stream);
-uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb, bool hdr24);
+uint32_t small_variant(bool wide_lut, uint32_t m, uint32_t nb, bool win32);
 
 
 // Launchers (maglev_kernels.hip).  `wide_lut` = u16 entries; `lds_lut` = stage in LDS.

@@ -505,8 +505,8 @@ def _mbuf_pool(frames, room=2048):
 
 
 def _host_case(kind, seed):
-    """Host batches that select each header-window stride: 24 B (frame bytes 14..37 for a direct batch
-    whose frames longer than 38 B have IHL <= 5), 48 B (IHL <= 7), 64 B (IHL <= 11), 80 B (IHL up to
+    """Host batches that select each header-window stride: 32 B (frame bytes 8..39 for a direct batch
+    whose frames longer than 40 B have IHL <= 5), 48 B (IHL <= 7), 64 B (IHL <= 11), 80 B (IHL up to
     15); all with runts and non-IPv4 frames."""
     from netbricks_amd import make_trace
 
@@ -514,8 +514,8 @@ def _host_case(kind, seed):
     buf, off, ln = make_trace(3000 + seed, 1, seed=seed)
     frames = [bytearray(buf[o:o + l].tobytes()) for o, l in zip(off, ln)]
     edge = _edge_frames(rng)
-    if kind == 24:
-        edge = [f for f in edge if len(f) <= 38 or (f[14] & 0xF) <= 5]
+    if kind == 32:
+        edge = [f for f in edge if len(f) <= 40 or (f[14] & 0xF) <= 5]
     elif kind == 48:
         edge = [f for f in edge if len(f) <= 48 or (f[14] & 0xF) <= 7]
     elif kind == 64:
@@ -531,7 +531,7 @@ def test_host_pipeline_submit_wait(torch_cuda, mg65):
     from netbricks_amd import NBG_HOST_SLOTS  # noqa: F401  (exported constant)
 
     lut = orc.lut_build(NAMES65, 65537)
-    cases = [_host_case(k, s) for s, k in enumerate([48, 64, 80, 24, 48, 64, 80])]
+    cases = [_host_case(k, s) for s, k in enumerate([48, 64, 80, 32, 48, 64, 80])]
     batches, tickets = [], []
     for frames in cases:
         pool, ptrs, lens = _mbuf_pool(frames)
@@ -553,7 +553,7 @@ def test_host_pipeline_submit_wait(torch_cuda, mg65):
             assert pool[i * 2048:i * 2048 + l].tobytes() == exp[0][o:o + l].tobytes(), i
 
 
-@pytest.mark.parametrize("kind", [24, 48, 64, 80])
+@pytest.mark.parametrize("kind", [32, 48, 64, 80])
 def test_host_pipeline_direct_small_batches(torch_cuda, mg65, kind):
     """Batches of at most 2,048 frames take host_submit's direct path (the small kernel reads the
     staged windows out of pinned memory and stores backend / perm / counts / MAC records there): every
@@ -571,10 +571,10 @@ def test_host_pipeline_direct_small_batches(torch_cuda, mg65, kind):
     from netbricks_amd._lib import lib
 
     wins = [lib.nbg_debug_host_win(mg65._h, t) for *_, t in batches]
-    if kind == 24:  # the first two batches hold edge frames; every batch is staged at 24 B
-        assert wins == [24, 24, 24], wins
+    if kind == 32:  # the first two batches hold edge frames; every batch is staged at 32 B
+        assert wins == [32, 32, 32], wins
     else:  # a longer IP header in a batch stages it from byte 0 at the stride it needs
-        assert all(w in (24, 48, 64, 80) for w in wins) and max(wins) >= min(kind, 48), wins
+        assert all(w in (32, 48, 64, 80) for w in wins) and max(wins) >= min(kind, 48), wins
     for *_, t in batches:
         for _ in range(100000):
             if mg65.host_query(t):

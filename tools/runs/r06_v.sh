@@ -1,4 +1,4 @@
-# round 6: 24-B header windows (this tree) against 32-B windows (the previous commit's library, built by
+# round 6: 24-B header windows (this tree) against 32-B windows (commit c49d932's library, built by
 # tools/build_ab.sh into tools/ab/w32), drop-in at 16 and 1 pipelines, 3 alternating rounds on one box
 set -o pipefail
 cd $GRAFT_REPO_ROOT
