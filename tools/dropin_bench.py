@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
     ap.add_argument("--ab-lib", help="only an A/B of this tree's libnbgpu.so against the one in this directory "
                                      "(LD_LIBRARY_PATH; nb_maglev's RUNPATH yields to it) at 16 and 1 pipelines, 3 rounds")
+    ap.add_argument("--ab-env", help="only an A/B of this tree against KEY=VALUE in the environment (16 and 1 "
+                                     "pipelines, 3 alternating rounds)")
     ap.add_argument("--depth-sweep", action="store_true",
                     help="only batches in flight per pipeline (4, 8) x server blocks (48, 64) at 16 pipelines")
     ap.add_argument("--server-sweep", action="store_true",
@@ -101,8 +103,9 @@ def main():
                      ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
                      ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
                      ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
-        if args.ab_lib:
-            alt = {"LD_LIBRARY_PATH": os.path.abspath(args.ab_lib)}
+        if args.ab_lib or args.ab_env:
+            alt = ({"LD_LIBRARY_PATH": os.path.abspath(args.ab_lib)} if args.ab_lib
+                   else dict([args.ab_env.split("=", 1)]))
             runs = [(f"p{p}_{'alt' if k % 2 else 'tree'}_r{k // 2}",
                      dict(pipelines=p, server=SERVER_BLOCKS, env=alt if k % 2 else None))
                     for p in (16, 1) for k in range(6)]
