@@ -2261,10 +2261,15 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
     __builtin_amdgcn_wave_barrier();  // the next round's writes after these reads
     const uint32_t p = wave * 256u + r * 64u + lane;
     bin[r] = 0xffffffffu;
-    if (r < rounds && p < a.n_pkts) {
-      bin[r] = small_classify<LUTM, F4, W32>(a, p, off[r], len[r], c);
-      a.backend[p] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
-    }
+    if (r < rounds && p < a.n_pkts) bin[r] = small_classify<LUTM, F4, W32>(a, p, off[r], len[r], c);
+  }
+  // backend[] after every round's gathers: vmcnt counts stores too and retires in order, so a store
+  // issued between two rounds' LUT gathers made the second gather's wait also wait for the store (a
+  // PCIe round trip for the host path's direct batches)
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint32_t p = wave * 256u + r * 64u + lane;
+    if (r < rounds && p < a.n_pkts) a.backend[p] = static_cast<uint16_t>(bin[r] == a.nb ? kSentinel : bin[r]);
   }
   if (!group) return;
   lds_sync();  // counters zeroed
@@ -2316,8 +2321,26 @@ __device__ __forceinline__ void small_body(const ClassifyArgs& a, const GroupArg
     }
   }
   lds_sync();
-  if (g.perm)
-    for (uint32_t p = tid; p < a.n_pkts; p += blockDim.x) g.perm[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
+  if (g.perm) {
+    // perm is scattered in LDS (the load-transpose area, free now: 3 KB per wave >= 4 B per packet)
+    // and stored in order, 16 B per lane: scattered 4-B stores were a partial line each, and over
+    // PCIe (the host path's direct batches) a write of its own for the block's system fence to wait
+    // for (host-batch server at 16 pipelines: 41.5 us body + 27.4 us fence per 992-packet batch)
+    uint32_t* pl = reinterpret_cast<uint32_t*>(bin16 + kSmallMax);
+    for (uint32_t p = tid; p < a.n_pkts; p += blockDim.x) pl[cnt[(p >> 8) * nbp + bin16[p]] + rank16[p]] = p;
+    lds_sync();
+    if ((reinterpret_cast<uintptr_t>(g.perm) & 15u) == 0) {
+      for (uint32_t i = 4u * tid; i < a.n_pkts; i += 4u * blockDim.x) {
+        if (i + 4u <= a.n_pkts) {
+          *reinterpret_cast<uint4*>(g.perm + i) = *reinterpret_cast<const uint4*>(pl + i);
+        } else {
+          for (uint32_t j = i; j < a.n_pkts; ++j) g.perm[j] = pl[j];
+        }
+      }
+    } else {
+      for (uint32_t i = tid; i < a.n_pkts; i += blockDim.x) g.perm[i] = pl[i];
+    }
+  }
 }
 
 // done (nullable): a completion word in pinned host memory (nbg_maglev_host_submit's direct path), set
