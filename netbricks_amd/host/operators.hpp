@@ -456,7 +456,11 @@ class GroupBy {
         }
         if (!deliver(b)) break;  // a full queue (backpressure): resumed at the next execution
       }
-      if (n_in_flight == depth || !admit_batch(queues, max_batch, admission)) return;
+      if (n_in_flight == depth) return;
+      // every queue has room for a whole batch: checked over all ct queues only until it holds, then
+      // kept until this producer enqueues again (the consumers only ever free slots)
+      if (!room) room = admit_batch(queues, max_batch, admission);
+      if (!room) return;
       const Clock::tick t0 = tnow();
       InFlight& b = slots[(head + n_in_flight) % depth];
       b.batch.clear();
@@ -498,6 +502,7 @@ class GroupBy {
       const Clock::tick t1 = tnow();
       const bool all = enqueue_grouped_from(b.batch.data(), b.perm.data(), b.counts.data(), queues, stats, b.cur,
                                             admission == Admission::kBackpressure);
+      room = false;
       prof.enqueue += since(t1);
       if (!all) return false;
       processed += b.batch.size();
@@ -513,6 +518,7 @@ class GroupBy {
     Admission admission;
     uint32_t depth;
     std::vector<InFlight> slots;  // a ring of `depth` batches: [head, head + n_in_flight) are on the GPU
+    bool room = false;            // admit_batch held and no enqueue since
     uint32_t head = 0, n_in_flight = 0;
     uint64_t in_flight_pkts = 0;
     EnqueueStats stats;

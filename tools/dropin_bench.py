@@ -44,7 +44,7 @@ def write_c1_pcap(path, n=10000, seed=2024):
 
 def run(pcap, pipelines, total, batch=992, depth=None, zero_copy=False, drop_on_full=False, hw_queues=0, huge=True,
         server=-1, pool=None, profile=True, local_cpus=True, spread=True, env=None, timeout=120):
-    args = [NB, "--rx", pcap, "--backends", "65", "--batch", str(batch), "--loop", str(total),
+    args = [(env or {}).get("NB_BIN", NB), "--rx", pcap, "--backends", "65", "--batch", str(batch), "--loop", str(total),
             "--pipelines", str(pipelines), "--zero-copy", "1" if zero_copy else "0",
             "--drop-on-full", "1" if drop_on_full else "0", "--hw-queues", str(hw_queues),
             "--hugepages", "1" if huge else "0", "--host-ring", str(server)]
@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--tune", action="store_true", help="only the host-gather prefetch distance and server size A/B")
     ap.add_argument("--ab-lib", help="only an A/B of this tree's libnbgpu.so against the one in this directory "
                                      "(LD_LIBRARY_PATH; nb_maglev's RUNPATH yields to it) at 16 and 1 pipelines, 3 rounds")
+    ap.add_argument("--ab-bin", help="only an A/B of this tree's nb_maglev against this binary (16 and 1 pipelines, "
+                                     "3 alternating rounds)")
     ap.add_argument("--ab-env", help="only an A/B of this tree against KEY=VALUE in the environment (16 and 1 "
                                      "pipelines, 3 alternating rounds)")
     ap.add_argument("--depth-sweep", action="store_true",
@@ -103,8 +105,10 @@ def main():
                      ("p16_server_depth2", dict(pipelines=16, server=32, depth=2)),
                      ("p1_zero_copy", dict(pipelines=1, zero_copy=True)),
                      ("p1_zero_copy_ahead32", dict(pipelines=1, zero_copy=True, env={"NBG_GATHER_AHEAD": "32"}))]
-        if args.ab_lib or args.ab_env:
+        if args.ab_lib or args.ab_env or args.ab_bin:
             alt = ({"LD_LIBRARY_PATH": os.path.abspath(args.ab_lib)} if args.ab_lib
+                   else {"NB_BIN": os.path.abspath(args.ab_bin), "LD_LIBRARY_PATH": os.path.join(ROOT, "netbricks_amd")}
+                   if args.ab_bin
                    else dict([args.ab_env.split("=", 1)]))
             runs = [(f"p{p}_{'alt' if k % 2 else 'tree'}_r{k // 2}",
                      dict(pipelines=p, server=SERVER_BLOCKS, env=alt if k % 2 else None))
