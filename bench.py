@@ -269,6 +269,33 @@ def spread_cpus(cpus):
     return out
 
 
+def idle_cpus(cpus, sample_s=0.1):
+    """(idle, busy): the CPUs other processes kept busy over a short sample of /proc/stat (more than 20 %
+    of their time: a shared host's other jobs) apart from the rest, each in the given order (the drop-in
+    pipelines' placement, nb_maglev's idle_first, used for the baseline's threads too)."""
+    def sample():
+        out = {}
+        try:
+            for ln in open("/proc/stat"):
+                f = ln.split()
+                if f[0].startswith("cpu") and f[0] != "cpu":
+                    v = [int(x) for x in f[1:9]]
+                    out[int(f[0][3:])] = (v[0] + v[1] + v[2] + v[5] + v[6] + v[7], sum(v))
+        except OSError:
+            pass
+        return out
+    a = sample()
+    time.sleep(sample_s)
+    b = sample()
+    idle, busy = [], []
+    for c in cpus:
+        if c in a and c in b and b[c][1] > a[c][1] and (b[c][0] - a[c][0]) * 5 > b[c][1] - a[c][1]:
+            busy.append(c)
+        else:
+            idle.append(c)
+    return idle, busy
+
+
 def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
     """The reference's per-core producer loop restated in C (oracle/, kind "port"), timed on this
     host's cores: MAC swap, ipv4_extract_flow, FNV-1a, the FNV-keyed memo map (nf.rs:91,104),
@@ -295,15 +322,21 @@ def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
         s = run(n, threads, reps, cache)
         return n * reps / s / 1e6, reps, s * threads
 
-    single, r1, c1 = measure(BATCH, 1, True, 2.0)
-    packed, ra, ca = measure(n_all, cores, True, target_cpu_s)
-    nocache, rn, cn = measure(n_all, cores, False, target_cpu_s / 2)
-    # the same threads placed as the drop-in path places its pipelines (dealt over the L3 caches):
-    # the baseline is the faster of the two placements
-    order = spread_cpus(sorted(os.sched_getaffinity(0)))[:cores]
-    arr = (C.c_int * len(order))(*order)
-    L.orc_set_cpu_order(arr, len(order))
+    # the threads on idle CPUs first (as the drop-in path's pipelines: a shared host's other jobs keep
+    # some cores busy), in CPU order, then dealt over the L3 caches as the drop-in path deals its
+    # pipelines: the baseline is the faster of the two placements
+    idle, busy = idle_cpus(sorted(os.sched_getaffinity(0)))
+
+    def placed(order):
+        arr = (C.c_int * len(order))(*order)
+        L.orc_set_cpu_order(arr, len(order))
+
     try:
+        placed((idle + busy)[:cores])
+        single, r1, c1 = measure(BATCH, 1, True, 2.0)
+        packed, ra, ca = measure(n_all, cores, True, target_cpu_s)
+        nocache, rn, cn = measure(n_all, cores, False, target_cpu_s / 2)
+        placed((spread_cpus(idle) + spread_cpus(busy))[:cores])
         spread, rs, cs = measure(n_all, cores, True, target_cpu_s)
     finally:
         L.orc_set_cpu_order(None, 0)
@@ -311,7 +344,8 @@ def cpu_baseline(host_bufs, lut, target_cpu_s=8.0):
     return {"value": round(allc, 1), "unit": "Mpps", "cores": cores, "kind": "port",
             "single_core_mpps": round(single, 2), "no_cache_mpps": round(nocache, 1),
             "packed_mpps": round(packed, 1), "spread_l3_mpps": round(spread, 1),
-            "placement": "spread over L3 caches" if spread > packed else "first allowed CPUs",
+            "placement": "idle CPUs, spread over L3 caches" if spread > packed else "idle CPUs in order",
+            "busy_cpus_skipped": len(busy),
             "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "cpu_model": model,
             "sample": f"C port of the reference loop (FNV-keyed memo map nf.rs:91,104, 32-pkt bursts, per-group "
                       f"1024-slot rings) over the {len(host_bufs)} C2 batches ({n_all:,} 64-B UDP packets, 65 backends, "

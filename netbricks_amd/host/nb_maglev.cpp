@@ -26,8 +26,9 @@
 // over its wall time, producer and consumer tasks included) and the aggregate (all packets over the
 // slowest pipeline's time).  --host-ring B attaches every pipeline's handle to one host-batch server
 // of B blocks (nbg_host_ring_*: one persistent kernel takes the batches; no kernel launch per batch).
-// Pipeline p runs on the p-th CPU local to the GPU (--local-cpus 0: of all the process may use), the
-// CPUs dealt over their L3 caches first (--spread-l3 0: in the kernel's order).
+// Pipeline p runs on the p-th CPU local to the GPU (--local-cpus 0: of all the process may use), CPUs
+// that other processes keep busy last, the rest dealt over their L3 caches (--spread-l3 0: in the
+// kernel's order).
 // The JSON's per-phase profile and producer seconds come from TSC reads around every task execution and
 // producer phase; --profile 0 turns them off (the NF rate without them: within ~2 %).
 #include <pthread.h>
@@ -106,6 +107,38 @@ std::vector<int> spread_over_l3(const std::vector<int>& cpus) {
   return out;
 }
 
+// The CPUs other processes kept busy over a 100-ms sample of /proc/stat (more than 20 % of their time:
+// a shared host's other jobs) apart from the idle ones, the order otherwise kept: the pipelines take
+// idle cores first.  The aggregate is set by the slowest pipeline's core, so a DPDK lcore gets an
+// isolated one.
+std::pair<std::vector<int>, std::vector<int>> idle_first(const std::vector<int>& cpus) {
+  auto sample = [](std::vector<std::pair<uint64_t, uint64_t>>& v) {  // (busy, total) jiffies per CPU
+    v.assign(CPU_SETSIZE, {0, 0});
+    FILE* f = std::fopen("/proc/stat", "r");
+    if (!f) return false;
+    char line[512];
+    while (std::fgets(line, sizeof line, f)) {
+      int c = -1;
+      unsigned long long u, n, sy, id, io, irq, sirq, st;
+      if (std::sscanf(line, "cpu%d %llu %llu %llu %llu %llu %llu %llu %llu", &c, &u, &n, &sy, &id, &io, &irq, &sirq,
+                      &st) == 9 && c >= 0 && c < CPU_SETSIZE)
+        v[c] = {u + n + sy + irq + sirq + st, u + n + sy + id + io + irq + sirq + st};
+    }
+    std::fclose(f);
+    return true;
+  };
+  std::vector<std::pair<uint64_t, uint64_t>> a, b;
+  if (!sample(a)) return {cpus, {}};
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  if (!sample(b)) return {cpus, {}};
+  std::vector<int> idle, busy;
+  for (int c : cpus) {
+    const uint64_t tot = b[c].second - a[c].second, use = b[c].first - a[c].first;
+    (tot && use * 5 > tot ? busy : idle).push_back(c);
+  }
+  return {idle, busy};
+}
+
 void pin_to(int k, const std::vector<int>& cpus) {
   if (cpus.empty()) return;
   cpu_set_t one;
@@ -118,7 +151,9 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
              uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge,
              nbg_host_ring* server, size_t pool_mbufs, bool profiled, bool local, bool spread) {
   const auto recs = nb::read_pcap(rx);
-  const std::vector<int> cpus = spread ? spread_over_l3(pipeline_cpus(local)) : pipeline_cpus(local);
+  const auto near = idle_first(pipeline_cpus(local));  // (idle, busy)
+  std::vector<int> cpus = spread ? spread_over_l3(near.first) : near.first;
+  for (int c : spread ? spread_over_l3(near.second) : near.second) cpus.push_back(c);
   std::vector<LoopResult> res(pipelines);
   std::atomic<int> ready{0};
   std::atomic<bool> go{false};
