@@ -196,3 +196,24 @@ def test_cpu_baseline_reports_both_placements():
     assert r["value"] == round(max(r["packed_mpps"], r["spread_l3_mpps"]), 1) or \
         abs(r["value"] - max(r["packed_mpps"], r["spread_l3_mpps"])) < 0.11
     assert np.isfinite(r["single_core_mpps"])
+
+
+def test_idle_cpus_puts_busy_cpus_last(monkeypatch):
+    """idle_cpus (the drop-in pipelines' and the CPU baseline's placement): CPUs busier than 20 % over
+    the sample go last, the order otherwise kept."""
+    import io
+
+    samples = iter([
+        "cpu  0 0 0 0 0 0 0 0\ncpu0 100 0 0 900 0 0 0 0\ncpu1 100 0 0 900 0 0 0 0\ncpu2 100 0 0 900 0 0 0 0\n",
+        "cpu  0 0 0 0 0 0 0 0\ncpu0 105 0 0 995 0 0 0 0\ncpu1 190 0 0 910 0 0 0 0\ncpu2 110 0 0 990 0 0 0 0\n",
+    ])
+    real_open = open
+
+    def fake_open(path, *a, **k):
+        if path == "/proc/stat":
+            return io.StringIO(next(samples))
+        return real_open(path, *a, **k)
+
+    monkeypatch.setattr("builtins.open", fake_open)
+    idle, busy = bench.idle_cpus([0, 1, 2], sample_s=0.0)
+    assert idle == [0, 2] and busy == [1]
