@@ -149,7 +149,7 @@ void pin_to(int k, const std::vector<int>& cpus) {
 
 int run_loop(const std::string& rx, const std::vector<std::string>& names, uint64_t table, uint32_t batch,
              uint32_t depth, bool zero_copy, bool drop_on_full, uint64_t total, int pipelines, bool huge,
-             nbg_host_ring* server, size_t pool_mbufs, bool profiled, bool local, bool spread) {
+             nbg_host_ring* server, size_t pool_mbufs, bool profiled, bool local, bool spread, uint32_t object) {
   const auto recs = nb::read_pcap(rx);
   const auto near = idle_first(pipeline_cpus(local));  // (idle, busy)
   std::vector<int> cpus = spread ? spread_over_l3(near.first) : near.first;
@@ -166,7 +166,7 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
         pin_to(p, cpus);
         const size_t mbufs = pool_mbufs ? pool_mbufs
                                         : std::max<size_t>(8192, size_t{depth} * nb::cap_batch(batch) + 2048);
-        auto port = std::make_shared<nb::LoopPort>(recs, total, mbufs, 2048, huge);
+        auto port = std::make_shared<nb::LoopPort>(recs, total, mbufs, 2048, huge, object);
         auto pool = port->mempool();
         uint8_t* dev = nullptr;
         if (zero_copy) nb::check(nbg_host_register(pool.first, pool.second, 0, &dev), "nbg_host_register");
@@ -241,12 +241,12 @@ int run_loop(const std::string& rx, const std::vector<std::string>& names, uint6
   for (int p = 0; p < pipelines && !cpus.empty(); ++p)
     cpu_list += (p ? "," : "") + std::to_string(cpus[static_cast<size_t>(p) % cpus.size()]);
   std::printf("{\"mode\": \"loop\", \"pipelines\": %d, \"backends\": %zu, \"max_batch\": %u, \"depth\": %u, "
-              "\"host_ring\": %s, \"profiled\": %s, \"cpus\": \"%s\", \"pool_mbufs\": %zu, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
+              "\"host_ring\": %s, \"profiled\": %s, \"cpus\": \"%s\", \"pool_mbufs\": %zu, \"mbuf_stride\": %u, \"huge_pages\": %s, \"hw_queues\": \"%s\", \"zero_copy\": %s, \"drop_on_full\": %s, \"rx_per_pipeline\": %llu, \"rx\": %llu, \"tx\": %llu, "
               "\"dropped\": %llu, \"would_panic\": %llu, \"batches\": %llu, \"enqueue_stalls\": %llu, \"seconds_max\": %.6f, "
               "\"aggregate_mpps\": %.2f, \"per_pipeline_mpps\": [%s], \"producer_seconds\": [%s], "
               "\"us_per_batch\": {\"pull\": %.2f, \"submit\": %.2f, \"query\": %.2f, \"queries\": %.1f, "
               "\"wait\": %.2f, \"enqueue\": %.2f}}\n",
-              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", profiled ? "true" : "false", cpu_list.c_str(), res[0].pool, huge_all ? "true" : "false",
+              pipelines, names.size(), nb::cap_batch(batch), depth, server ? "true" : "false", profiled ? "true" : "false", cpu_list.c_str(), res[0].pool, object, huge_all ? "true" : "false",
               std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "", zero_copy ? "true" : "false",
               drop_on_full ? "true" : "false", static_cast<unsigned long long>(total),
               static_cast<unsigned long long>(rx_all), static_cast<unsigned long long>(tx_all),
@@ -273,6 +273,9 @@ int main(int argc, char** argv) {
   // 370 Mpps at 16 pipelines, profiles/r06_dropin_pool.json)
   size_t pool_mbufs = 0;
   bool profiled = true, local = true, spread = true;
+  // mempool object stride: 128-B rte_mbuf + 128-B headroom + 2,048-B data room + 64-B object header
+  // (37 lines: consecutive frames fall on different cache sets, as rte_mempool spreads them)
+  uint32_t object = 2368;
   bool zero_copy = false, drop_on_full = false, huge = true;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string k = argv[i], v = argv[i + 1];
@@ -291,6 +294,7 @@ int main(int argc, char** argv) {
     else if (k == "--profile") profiled = std::atoi(v.c_str()) != 0;
     else if (k == "--local-cpus") local = std::atoi(v.c_str()) != 0;
     else if (k == "--spread-l3") spread = std::atoi(v.c_str()) != 0;
+    else if (k == "--mbuf-stride") object = static_cast<uint32_t>(std::strtoul(v.c_str(), nullptr, 10));
     else if (k == "--zero-copy") zero_copy = std::atoi(v.c_str()) != 0;
     else if (k == "--drop-on-full") drop_on_full = std::atoi(v.c_str()) != 0;
     else if (k == "--backends") {
@@ -332,7 +336,7 @@ int main(int argc, char** argv) {
         if (s && nbg_host_ring_stop(s) != NBG_OK) std::fprintf(stderr, "nb_maglev: %s\n", nbg_last_error());
       }
     } stop_server{server};
-    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server, pool_mbufs, profiled, local, spread);
+    if (loop) return run_loop(rx, names, table, batch, depth, zero_copy, drop_on_full, loop, pipelines, huge, server, pool_mbufs, profiled, local, spread, object);
     auto port = std::make_shared<nb::PcapPort>(rx);
     auto pool = port->mempool();
     if (zero_copy && pool.second) {

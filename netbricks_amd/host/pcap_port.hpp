@@ -143,12 +143,17 @@ class LoopPort : public PacketRx, public PacketTx {
  public:
   // huge: the mempool in 2-MiB transparent huge pages, as a DPDK mempool lives in hugepages (for the
   // GPU's reads of a registered pool, and the host's, one TLB entry per 2 MiB instead of per 4 KiB)
+  // object: the stride of the pool's objects (0: the data room itself).  A DPDK mempool object is
+  // larger than its data room (the 128-B rte_mbuf, 128 B of headroom, the mempool's own header) and
+  // rte_mempool pads objects so that consecutive ones do not start on the same cache sets; a stride
+  // of exactly 2 KiB would put every frame's first line into 1/32 of the L2's sets.
   LoopPort(const std::vector<PcapRecord>& recs, uint64_t total, size_t min_pool = 65536, uint32_t data_room = 2048,
-           bool huge = true)
+           bool huge = true, uint32_t object = 0)
       : total_(total) {
     if (recs.empty()) throw std::invalid_argument("LoopPort: empty capture");
     room_ = data_room;
     for (auto& r : recs) room_ = std::max<size_t>(room_, (r.data.size() + 63) & ~size_t{63});
+    if (object) room_ = std::max<size_t>(room_, (object + 63) & ~size_t{63});
     const size_t n = (std::max(min_pool, recs.size()) + recs.size() - 1) / recs.size() * recs.size();
     constexpr size_t kHuge = 2u << 20;
     map_bytes_ = (n * room_ + 2 * kHuge - 1) / kHuge * kHuge;

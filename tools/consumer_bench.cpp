@@ -3,7 +3,7 @@
 // consumer (GroupBy::get_group's RestoreHeader over each group's queue, MergeSend to the port), on one
 // thread as nb_maglev --loop runs them.  Measurement tool (no GPU, no oracle): ns per packet of each
 // half, for A/B builds of operators.hpp.
-//   g++ -O2 -std=c++17 -I. -o /tmp/consumer_bench tools/consumer_bench.cpp && /tmp/consumer_bench
+//   g++ -O2 -std=c++17 -I. -o /tmp/consumer_bench tools/consumer_bench.cpp && /tmp/consumer_bench [packets] [mbuf stride]
 #include <chrono>
 #include <cstdio>
 #include <memory>
@@ -25,7 +25,8 @@ int main(int argc, char** argv) {
   const uint64_t total = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 20000000ull;
   std::vector<nb::PcapRecord> recs(10000);
   for (auto& r : recs) r.data.assign(60, 0x11);
-  auto port = std::make_shared<nb::LoopPort>(recs, total, 8192, 2048, true);
+  const uint32_t stride = argc > 2 ? static_cast<uint32_t>(std::strtoul(argv[2], nullptr, 10)) : 0u;
+  auto port = std::make_shared<nb::LoopPort>(recs, total, 8192, 2048, true, stride);
   std::vector<std::shared_ptr<nb::MpscQueue>> queues;
   std::vector<std::shared_ptr<nb::Batch>> outs;
   for (uint32_t g = 0; g < groups; ++g) {

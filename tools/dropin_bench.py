@@ -52,6 +52,7 @@ def run(pcap, pipelines, total, batch=992, depth=None, zero_copy=False, drop_on_
         args += ["--depth", str(depth)]
     if pool:
         args += ["--pool", str(pool)]
+    args += (env or {}).get("NB_EXTRA_ARGS", "").split()  # an A/B of nb_maglev options (--ab-env)
     if not profile:
         args += ["--profile", "0"]
     if not local_cpus:
@@ -167,8 +168,9 @@ def main():
                          "aggregate_mpps": r["aggregate_mpps"], "producer_only_mpps": round(prod / 1e6, 1)})
     print(json.dumps({"dropin": rows, "runs": out, "batch": 992, "queue_slots": 1024, "depth": 8,
                       "server_blocks": SERVER_BLOCKS, "capture": "10k 64-B UDP frames (C1 style), 65 backends / 65537, "
-                                                      "LoopPort replay (a pool of 10,000 2-KiB mbufs in huge pages, "
-                                                      "one per frame of the capture); threads on the GPU's socket"}))
+                                                      "LoopPort replay (a pool of 10,000 2-KiB mbufs in huge pages at a "
+                                                      "2,368-B object stride, one per frame of the capture); threads on "
+                                                      "the GPU's socket, idle cores first"}))
 
 
 if __name__ == "__main__":
