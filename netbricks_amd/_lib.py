@@ -37,6 +37,7 @@ NBG_RING_SLOTS = 64
 NBG_RING_MAX_QUEUES = 16
 NBG_EBUSY = -16
 NBG_EINVAL = -22
+NBG_EIO = -5
 NBG_TRACE_UNIQUE = 0x1
 NBG_LPM_TBL24_SIZE = (1 << 24) + 1
 

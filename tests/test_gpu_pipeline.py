@@ -147,9 +147,14 @@ def test_device_local_cpus(torch_cuda):
 
     from netbricks_amd._lib import lib
 
+    from netbricks_amd._lib import NBG_EIO
+
     buf = (C.c_int32 * 4096)()
     n = C.c_uint32()
-    assert lib.nbg_device_local_cpus(0, buf, 4096, C.byref(n)) == 0
+    rc = lib.nbg_device_local_cpus(0, buf, 4096, C.byref(n))
+    if rc == NBG_EIO:  # the documented answer where sysfs has no local_cpulist for the device
+        pytest.skip("no local_cpulist for the GPU's PCI function on this host")
+    assert rc == 0
     cpus = list(buf[:n.value])
     assert 0 < n.value <= os.cpu_count() and len(set(cpus)) == n.value
     assert all(0 <= c < os.cpu_count() for c in cpus)
