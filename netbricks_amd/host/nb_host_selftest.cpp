@@ -201,6 +201,32 @@ int main(int argc, char** argv) {
     }
     EXPECT(got == recs.size() && port.tx_index().back() == recs.size() - 1);
   }
+  {  // LoopPort (nb_maglev --loop's replay): pool rounded up to whole captures, objects at the given
+     // stride, every frame handed out in capture order and recycled by send
+    std::vector<nb::PcapRecord> recs(100);
+    for (size_t i = 0; i < recs.size(); ++i) recs[i].data.assign(60, static_cast<uint8_t>(i));
+    nb::LoopPort port(recs, 1000, 150, 2048, false, 2368);
+    EXPECT(port.pool_size() == 200);
+    EXPECT(port.mempool().second == 200u * 2368u);
+    std::vector<nb::MBuf*> got(32);
+    uint64_t seen = 0;
+    while (!port.rx_done()) {
+      const uint32_t n = port.recv(got.data(), 32);
+      EXPECT(n > 0);
+      for (uint32_t i = 0; i < n; ++i, ++seen) {
+        EXPECT(got[i]->data_len == 60 && got[i]->data()[0] == static_cast<uint8_t>(seen % 200 % 100));
+        EXPECT((got[i]->data() - port.mempool().first) % 2368 == 0);
+      }
+      EXPECT(port.send(got.data(), n) == n);
+    }
+    EXPECT(seen == 1000 && port.tx_total() == 1000);
+  }
+  {  // the profile clock: monotonic, calibrated to a plausible rate
+    const auto t0 = nb::TscClock::now();
+    const double s = nb::TscClock::seconds_per_tick();
+    EXPECT(s > 1e-12 && s < 1e-6);
+    EXPECT(nb::TscClock::now() >= t0);
+  }
   std::printf("nb_host_selftest ok\n");
   return 0;
 }
